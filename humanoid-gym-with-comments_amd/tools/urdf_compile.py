@@ -1,0 +1,167 @@
+"""URDF -> compact articulated-model table for the XBot-L humanoid.
+
+This is the build's "asset loader" (it replaces Isaac Gym's ``gym.load_asset`` with
+``collapse_fixed_joints=True``; reference call site ``humanoid/envs/custom/humanoid_env.py:455``,
+asset options ``humanoid_config.py:93-119``).  It runs ONCE, in a container where the reference
+URDF is readable, and writes ``model/xbotl_model.json``; the JSON (derived data, not reference
+source) is what ships to the GPU box.
+
+What it does
+  * walks the URDF tree from ``base_link``;
+  * collapses every fixed joint into its nearest movable ancestor ("body"), composing the fixed
+    transforms and merging mass / COM / inertia with the parallel-axis theorem;
+  * emits bodies in Isaac Gym's depth-first order (base, left leg 6, right leg 6), so
+    ``feet = [6, 12]`` and ``knees = [4, 10]`` as in SURVEY App. A;
+  * derives contact candidate points: the 4 sole corners of each ``*_ankle_roll_link`` STL hull
+    (bottom plane y = -0.056 in the link frame) and the 8 corners of the base-link collision box.
+
+Usage:  python tools/urdf_compile.py /root/reference/resources/robots/XBot [out.json]
+"""
+import json
+import os
+import struct
+import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+
+def rpy_to_R(r, p, y):
+    cr, sr, cp, sp, cy, sy = np.cos(r), np.sin(r), np.cos(p), np.sin(p), np.cos(y), np.sin(y)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx  # URDF fixed-axis roll-pitch-yaw
+
+
+def parse_origin(el):
+    if el is None:
+        return np.zeros(3), np.eye(3)
+    xyz = np.array([float(v) for v in el.get("xyz", "0 0 0").split()])
+    rpy = [float(v) for v in el.get("rpy", "0 0 0").split()]
+    return xyz, rpy_to_R(*rpy)
+
+
+def T(p, R):
+    M = np.eye(4)
+    M[:3, :3] = R
+    M[:3, 3] = p
+    return M
+
+
+def load_stl(fn):
+    d = open(fn, "rb").read()
+    n = struct.unpack("<I", d[80:84])[0]
+    a = np.frombuffer(d[84:84 + n * 50],
+                      dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
+    return a["v"].reshape(-1, 3).astype(np.float64)
+
+
+def compile_urdf(robot_dir):
+    urdf = os.path.join(robot_dir, "urdf", "XBot-L.urdf")
+    root = ET.parse(urdf).getroot()
+    links = {l.get("name"): l for l in root.findall("link")}
+    joints = root.findall("joint")
+    child_joint = {j.find("child").get("link"): j for j in joints}
+    children = {}
+    for j in joints:
+        children.setdefault(j.find("parent").get("link"), []).append(j)
+
+    # depth-first body order over movable joints (Isaac Gym asset order)
+    bodies = []          # (link_name, joint_el or None, parent_body_index, T_parentbody_jointframe)
+    link_body = {}       # link name -> (body index, T_body_link)
+
+    def visit(link, body_idx, T_b_l):
+        link_body[link] = (body_idx, T_b_l)
+        for j in children.get(link, []):
+            c = j.find("child").get("link")
+            p, R = parse_origin(j.find("origin"))
+            T_l_c = T(p, R)
+            if j.get("type") == "fixed":
+                visit(c, body_idx, T_b_l @ T_l_c)
+            else:
+                bodies.append((c, j, body_idx, T_b_l @ T_l_c))
+                visit(c, len(bodies) - 1, np.eye(4))
+
+    bodies.append(("base_link", None, -1, np.eye(4)))
+    visit("base_link", 0, np.eye(4))
+    assert len(bodies) == 13, len(bodies)
+
+    # merge inertials into bodies
+    acc = [dict(m=0.0, mc=np.zeros(3), items=[]) for _ in bodies]
+    for lname, (b, T_b_l) in link_body.items():
+        inert = links[lname].find("inertial")
+        if inert is None:
+            continue
+        m = float(inert.find("mass").get("value"))
+        p, R = parse_origin(inert.find("origin"))
+        ia = inert.find("inertia").attrib
+        I = np.array([[float(ia["ixx"]), float(ia["ixy"]), float(ia["ixz"])],
+                      [float(ia["ixy"]), float(ia["iyy"]), float(ia["iyz"])],
+                      [float(ia["ixz"]), float(ia["iyz"]), float(ia["izz"])]])
+        Rb = T_b_l[:3, :3] @ R
+        c = T_b_l[:3, :3] @ p + T_b_l[:3, 3]
+        acc[b]["m"] += m
+        acc[b]["mc"] += m * c
+        acc[b]["items"].append((m, c, Rb @ I @ Rb.T))
+
+    out_bodies = []
+    for bi, (lname, j, parent, T_pj) in enumerate(bodies):
+        m = acc[bi]["m"]
+        com = acc[bi]["mc"] / m
+        I = np.zeros((3, 3))
+        for (mi, ci, Ii) in acc[bi]["items"]:
+            d = ci - com
+            I += Ii + mi * (np.dot(d, d) * np.eye(3) - np.outer(d, d))
+        body = dict(name=lname, parent=parent, mass=m, com=com.tolist(),
+                    inertia=[I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]])
+        if j is not None:
+            lim = j.find("limit").attrib
+            dyn = j.find("dynamics")
+            body["joint"] = dict(
+                name=j.get("name"),
+                origin_pos=T_pj[:3, 3].tolist(),
+                origin_rot=T_pj[:3, :3].tolist(),
+                axis=[float(v) for v in j.find("axis").get("xyz").split()],
+                lower=float(lim["lower"]), upper=float(lim["upper"]),
+                effort=float(lim["effort"]), velocity=float(lim["velocity"]),
+                friction=float(dyn.get("friction", 0)) if dyn is not None else 0.0,
+                damping=float(dyn.get("damping", 0)) if dyn is not None else 0.0)
+        out_bodies.append(body)
+
+    # contact candidates
+    contacts = []
+    for bi, b in enumerate(out_bodies):
+        if b["name"].endswith("ankle_roll_link"):
+            v = load_stl(os.path.join(robot_dir, "meshes", b["name"] + ".STL"))
+            ymin = v[:, 1].min()
+            sole = v[v[:, 1] < ymin + 0.003]
+            x0, x1 = sole[:, 0].min(), sole[:, 0].max()
+            z0, z1 = sole[:, 2].min(), sole[:, 2].max()
+            for (x, z) in [(x0, z0), (x1, z0), (x0, z1), (x1, z1)]:
+                contacts.append(dict(body=bi, pos=[float(x), float(ymin), float(z)]))
+    base_col = links["base_link"].find("collision")
+    bp, _ = parse_origin(base_col.find("origin"))
+    size = [float(s) for s in base_col.find("geometry").find("box").get("size").split()]
+    for sx in (-1, 1):
+        for sy in (-1, 1):
+            for sz in (-1, 1):
+                contacts.append(dict(body=0, pos=[bp[0] + sx * size[0] / 2, bp[1] + sy * size[1] / 2,
+                                                  bp[2] + sz * size[2] / 2]))
+    return dict(
+        robot="XBot-L",
+        source="resources/robots/XBot/urdf/XBot-L.urdf (collapse_fixed_joints=True)",
+        bodies=out_bodies,
+        contacts=contacts,
+        total_mass=float(sum(b["mass"] for b in out_bodies)),
+    )
+
+
+if __name__ == "__main__":
+    robot_dir = sys.argv[1] if len(sys.argv) > 1 else "/root/reference/resources/robots/XBot"
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "model", "xbotl_model.json")
+    model = compile_urdf(robot_dir)
+    with open(out, "w") as f:
+        json.dump(model, f, indent=1)
+    print("wrote", out, "bodies", len(model["bodies"]), "mass %.3f" % model["total_mass"])

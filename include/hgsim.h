@@ -1,0 +1,194 @@
+/*
+ * hgsim.h — C ABI of the MI355X-native humanoid simulator ("hg_sim").
+ *
+ * This is the drop-in boundary that replaces, for the rollout + update hot path of
+ * Rengar-Yang/humanoid-gym-with-comments, the Isaac Gym / PhysX tensor API and the eager-torch
+ * env arithmetic.  Every entry point cites the reference interface it replaces (paths relative
+ * to the reference repo root).  The Python facade (humanoid/envs/custom/humanoid_env.py in this
+ * repo) binds it with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All functions return int status (0 = HG_OK); no exceptions cross the ABI.  A per-handle
+ *     message is available from hg_last_error().
+ *   - Device memory is owned by the CALLER: hg_arena_bytes() says how many bytes the library
+ *     needs, the caller allocates one device buffer (e.g. a torch uint8 tensor) and passes it to
+ *     hg_create().  hg_tensor() returns offset/shape/strides of each named buffer inside that
+ *     arena so the caller can wrap them zero-copy (what gymtorch.wrap_tensor did,
+ *     humanoid_env.py:246-254).  Per-env state is SoA ([field][num_envs]).
+ *   - All work is enqueued on the caller's stream (hipStream_t passed as void*), asynchronous
+ *     to the host, with no host synchronisation inside any step/post/gae call.
+ *   - The host API is not thread-safe per handle; one handle per GPU/process.
+ */
+#ifndef HGSIM_H
+#define HGSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HG_OK 0
+#define HG_ERR_ARG 1
+#define HG_ERR_HIP 2
+#define HG_ERR_STATE 3
+
+#define HG_MAX_BODIES 16
+#define HG_MAX_DOF 12
+#define HG_MAX_CONTACTS 16
+#define HG_NUM_REWARDS 22
+
+/* Articulated model table (output of tools/urdf_compile.py; replaces gym.load_asset +
+ * get_asset_* queries, humanoid_env.py:455-470).  Body 0 is the floating base; body b>=1 is
+ * attached to parent[b] by revolute joint (dof index b-1).  Frames follow URDF conventions. */
+typedef struct hg_model {
+  int32_t num_bodies;
+  int32_t num_dof;
+  int32_t num_contacts;     /* candidate contact points */
+  int32_t num_foot_contacts;/* the first num_foot_contacts candidates are foot-sole points */
+  int32_t parent[HG_MAX_BODIES];
+  int32_t contact_body[HG_MAX_CONTACTS];
+  float joint_pos[HG_MAX_BODIES][3];   /* joint origin in parent-body frame */
+  float joint_rot[HG_MAX_BODIES][9];   /* parent-body -> joint frame rotation, row-major */
+  float axis[HG_MAX_BODIES][3];        /* joint axis in child frame */
+  float mass[HG_MAX_BODIES];
+  float com[HG_MAX_BODIES][3];         /* body frame */
+  float inertia[HG_MAX_BODIES][6];     /* about COM, body frame: xx yy zz xy xz yz */
+  float armature[HG_MAX_BODIES];
+  float lower[HG_MAX_BODIES], upper[HG_MAX_BODIES];
+  float contact_pos[HG_MAX_CONTACTS][3];
+} hg_model;
+
+/* Simulation + env-logic configuration.  Field meanings follow XBotLCfg
+ * (humanoid/envs/custom/humanoid_config.py); comments give the source line. */
+typedef struct hg_cfg {
+  int32_t num_envs;
+  int32_t decimation;          /* control.decimation :271 */
+  int32_t pgs_iterations;      /* contact solver sweeps (PhysX TGS 4 pos + 1 vel :295-299) */
+  int32_t fix_base_link;       /* asset.fix_base_link :116 */
+  float sim_dt;                /* sim.dt :279 */
+  float gravity_z;             /* sim.gravity :285 */
+  float contact_offset;        /* physx.contact_offset :301 */
+  float max_depenetration_vel; /* physx.max_depenetration_velocity :307 */
+  float baumgarte;             /* build-defined position-error feedback fraction */
+  float ground_friction;       /* terrain.static_friction :143 */
+  /* actuation (humanoid_env.py:910-925) */
+  float action_scale;          /* control.action_scale :264 */
+  float clip_actions;          /* normalization.clip_actions :458 */
+  float dynamic_randomization; /* domain_rand.dynamic_randomization :339 */
+  float kp[HG_MAX_DOF], kd[HG_MAX_DOF], torque_limit[HG_MAX_DOF], default_dof_pos[HG_MAX_DOF];
+  /* terrain: 0 plane, 1 heightfield (device int16 [hf_rows][hf_cols], row = x) */
+  int32_t terrain_type;
+  int32_t hf_rows, hf_cols;
+  float hf_horizontal_scale, hf_vertical_scale, hf_border;
+  const int16_t* heightfield;  /* device pointer, caller-owned; NULL for plane */
+  /* env logic (humanoid_env.py:770-1163) */
+  int32_t frame_stack, c_frame_stack;   /* env.frame_stack / c_frame_stack :43,45 */
+  int32_t max_episode_length;           /* ceil(episode_length_s / dt) :187 */
+  int32_t resample_interval;            /* resampling_time / dt :1012 */
+  int32_t push_interval;                /* ceil(push_interval_s / dt) :191 */
+  int32_t push_robots, add_noise, heading_command, only_positive_rewards;
+  float dt;                             /* decimation * sim_dt */
+  float cycle_time, target_joint_pos_scale, target_feet_height, base_height_target;
+  float min_dist, max_dist, tracking_sigma, max_contact_force;
+  float max_push_vel_xy, max_push_ang_vel;
+  float cmd_lin_x[2], cmd_lin_y[2], cmd_ang_yaw[2], cmd_heading[2];
+  float noise_level, noise_dof_pos, noise_dof_vel, noise_ang_vel, noise_quat;
+  float obs_lin_vel, obs_ang_vel, obs_dof_pos, obs_dof_vel, obs_quat;
+  float clip_observations;
+  float init_pos[3], init_rot[4], init_lin_vel[3], init_ang_vel[3];
+  float reward_scale[HG_NUM_REWARDS];   /* already multiplied by dt; alphabetical order */
+  int32_t feet_body[2], knee_body[2];   /* [6,12], [4,10] */
+  int32_t ref_idx[6];                   /* left pitch,knee,ankle ; right pitch,knee,ankle dofs */
+  int32_t yaw_roll_idx[4];              /* default_joint_pos reward dof indices */
+  uint64_t seed;
+} hg_cfg;
+
+typedef struct hg_desc {
+  size_t offset_bytes;  /* into the arena */
+  int32_t dtype;        /* 0 f32, 1 i64, 2 u8(bool), 3 i32 */
+  int32_t ndim;
+  int64_t shape[4];
+  int64_t strides[4];   /* in elements */
+} hg_desc;
+
+/* tensor ids for hg_tensor() */
+enum hg_tensor_id {
+  HG_T_ROOT_STATE = 0,   /* [N,13] pos3 quat(xyzw)4 linvel3 angvel3, world   (actor_root_state) */
+  HG_T_DOF_POS,          /* [N,D]                                            (dof_state[...,0]) */
+  HG_T_DOF_VEL,          /* [N,D]                                            (dof_state[...,1]) */
+  HG_T_CONTACT_FORCES,   /* [N,B,3] net contact force per body, world        (net_contact_force) */
+  HG_T_RIGID_STATE,      /* [N,B,13] per-body pos quat linvel angvel         (rigid_body_state) */
+  HG_T_TORQUES,          /* [N,D] last applied torques                       (self.torques) */
+  HG_T_ACTIONS, HG_T_LAST_ACTIONS, HG_T_LAST_LAST_ACTIONS,
+  HG_T_LAST_DOF_VEL, HG_T_LAST_ROOT_VEL,
+  HG_T_COMMANDS,         /* [N,4] */
+  HG_T_OBS_BUF,          /* [N, frame_stack*47] row-major (policy input) */
+  HG_T_PRIV_BUF,         /* [N, c_frame_stack*73] row-major */
+  HG_T_REW_BUF,          /* [N] */
+  HG_T_RESET_BUF,        /* [N] bool */
+  HG_T_TIME_OUT_BUF,     /* [N] bool */
+  HG_T_EPISODE_LENGTH,   /* [N] int64 */
+  HG_T_EPISODE_SUMS,     /* [22,N] */
+  HG_T_FEET_AIR_TIME, HG_T_LAST_CONTACTS, HG_T_FEET_HEIGHT, HG_T_LAST_FEET_Z,
+  HG_T_ENV_FRICTION, HG_T_BODY_MASS, HG_T_PUSH_FORCE, HG_T_PUSH_TORQUE,
+  HG_T_BASE_LIN_VEL, HG_T_BASE_ANG_VEL, HG_T_PROJ_GRAVITY, HG_T_BASE_EULER,
+  HG_T_REF_DOF_POS, HG_T_ENV_ORIGINS,
+  HG_T_EP_STATS,         /* [22 + 2] episode reward means of the last resetting step, n_reset, any */
+  HG_T_CONTACT_LAMBDA,   /* solver warm-start impulses [C*3 + D, N] */
+  HG_T_NONFINITE,        /* [N] int32 count of non-finite recoveries */
+  HG_T_COUNT
+};
+
+/* ---- lifecycle ---- */
+size_t hg_arena_bytes(const hg_cfg* cfg);
+/* replaces gym.create_sim + _create_envs + prepare_sim (humanoid_env.py:333-524,
+ * base_task.py:101-102).  *out_sim receives an opaque handle. */
+int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t arena_bytes,
+              void** out_sim);
+void hg_destroy(void* sim);
+/* NULL sim -> last error of the most recent failed hg_create on this thread */
+const char* hg_last_error(void* sim);
+/* replaces acquire_*_tensor + gymtorch.wrap_tensor (humanoid_env.py:235-254) */
+int hg_tensor(void* sim, int id, hg_desc* out);
+
+/* ---- hot path ---- */
+/* replaces the step() preamble + decimation x (_compute_torques, set_dof_actuation_force_tensor,
+ * simulate, refresh_dof_state_tensor) + post-physics refreshes
+ * (humanoid_env.py:620-649, 776-778).  actions: device [N,D] row-major, caller-owned. */
+int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream);
+/* replaces post_physics_step minus the refreshes (humanoid_env.py:780-806) and the obs clip
+ * (:654-657): derived state, commands, push, termination, rewards, masked reset, observations.
+ * common_step_counter is the reference's host-side counter (:781). */
+int hg_post(void* sim, uint64_t common_step_counter, void* stream);
+/* replaces reset_idx() (humanoid_env.py:1109-1163) for an explicit device mask [N] (u8). */
+int hg_reset_masked(void* sim, const uint8_t* mask, uint64_t counter, void* stream);
+
+/* ---- indexed state writes (replace set_*_tensor_indexed, humanoid_env.py:1046-1048,1070-1072,680-681) ---- */
+/* env_ids: device int32 [n]; dof_pos/dof_vel: device [n,D]; root: device [n,13] */
+int hg_set_dof_state_indexed(void* sim, const int32_t* env_ids, int n, const float* dof_pos,
+                             const float* dof_vel, void* stream);
+int hg_set_root_state_indexed(void* sim, const int32_t* env_ids, int n, const float* root, void* stream);
+
+/* ---- rollout storage: fused GAE (replaces RolloutStorage.compute_returns,
+ * humanoid/algo/ppo/rollout_storage.py:122-143) ---- */
+/* Pass 1: reverse-time scan.  rewards/values/returns/advantages [T,N] f32, dones [T,N] u8,
+ * last_values [N].  Writes returns and raw advantages, and accumulates (sum A, sum A^2) in
+ * float64 into stats[0..1] (stats must be zeroed by the caller or by hg_gae_scan when
+ * zero_stats != 0). */
+int hg_gae_scan(const float* rewards, const uint8_t* dones, const float* values,
+                const float* last_values, float* returns, float* advantages, double* stats,
+                int T, int N, float gamma, float lam, int zero_stats, void* stream);
+/* Pass 2: advantages = (A - mean) / (std_unbiased + 1e-8) with mean/std from stats over
+ * `count` elements (count = T*N*world_size after an all-reduce of stats). */
+int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int64_t n_local,
+                     void* stream);
+
+/* library build info */
+const char* hg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGSIM_H */
