@@ -1,0 +1,348 @@
+// hg_api.hip — host side of the hg_sim C ABI (include/hgsim.h): arena layout, tensor
+// descriptors, launches.  No host synchronisation on any step/post path.
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "hg_common.h"
+
+extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
+extern "C" int hg_launch_post(const HgState* S, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
+                              float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
+                              float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
+                              hipStream_t stream);
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Field {
+  int id;
+  int dtype;      // 0 f32, 1 i64, 2 u8, 3 i32
+  int rows;       // SoA rows per env (ignored for special)
+  int ndim;       // view ndim
+  int64_t shp[3]; // trailing dims of the [N, ...] view (row index = r0*shp... see make_desc)
+};
+
+size_t esize(int dtype) { return dtype == 1 ? 8 : (dtype == 2 ? 1 : 4); }
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Layout {
+  size_t off[HG_T_COUNT + 8];
+  size_t bytes;
+  // extra regions
+  size_t obs_buf[2], priv_buf[2], frame_obs, frame_priv, cfg, model;
+};
+
+enum { X_OBS0 = HG_T_COUNT, X_OBS1, X_PRIV0, X_PRIV1, X_FOBS, X_FPRIV, X_CFG, X_MODEL };
+
+int soa_rows(int id) {
+  switch (id) {
+    case HG_T_ROOT_STATE: return 13;
+    case HG_T_DOF_POS: case HG_T_DOF_VEL: case HG_T_TORQUES: case HG_T_ACTIONS: case HG_T_LAST_ACTIONS:
+    case HG_T_LAST_LAST_ACTIONS: case HG_T_LAST_DOF_VEL: case HG_T_REF_DOF_POS: return HG_ND;
+    case HG_T_CONTACT_FORCES: return HG_NB * 3;
+    case HG_T_RIGID_STATE: return HG_NB * 13;
+    case HG_T_LAST_ROOT_VEL: return 6;
+    case HG_T_COMMANDS: return 4;
+    case HG_T_REW_BUF: case HG_T_RESET_BUF: case HG_T_TIME_OUT_BUF: case HG_T_EPISODE_LENGTH:
+    case HG_T_ENV_FRICTION: case HG_T_BODY_MASS: case HG_T_NONFINITE: return 1;
+    case HG_T_EPISODE_SUMS: return HG_NUM_REWARDS;
+    case HG_T_FEET_AIR_TIME: case HG_T_LAST_CONTACTS: case HG_T_FEET_HEIGHT: case HG_T_LAST_FEET_Z: return 2;
+    case HG_T_PUSH_FORCE: case HG_T_PUSH_TORQUE: case HG_T_BASE_LIN_VEL: case HG_T_BASE_ANG_VEL:
+    case HG_T_PROJ_GRAVITY: case HG_T_BASE_EULER: case HG_T_ENV_ORIGINS: return 3;
+    case HG_T_CONTACT_LAMBDA: return HG_LAMW;
+    default: return 0;
+  }
+}
+int dtype_of(int id) {
+  switch (id) {
+    case HG_T_RESET_BUF: case HG_T_TIME_OUT_BUF: case HG_T_LAST_CONTACTS: return 2;
+    case HG_T_EPISODE_LENGTH: return 1;
+    case HG_T_NONFINITE: return 3;
+    default: return 0;
+  }
+}
+
+Layout make_layout(const hg_cfg* c) {
+  Layout L;
+  const int n = c->num_envs;
+  const int np = (n + 63) & ~63;
+  size_t o = 0;
+  for (int id = 0; id < HG_T_COUNT; id++) {
+    L.off[id] = o;
+    if (id == HG_T_OBS_BUF || id == HG_T_PRIV_BUF) continue;  // below
+    if (id == HG_T_EP_STATS) { o += align256(48 * sizeof(float)); continue; }
+    o += align256((size_t)soa_rows(id) * np * esize(dtype_of(id)));
+  }
+  const size_t ob = (size_t)n * c->frame_stack * HG_OBS1 * 4, pb = (size_t)n * c->c_frame_stack * HG_PRIV1 * 4;
+  L.obs_buf[0] = o; o += align256(ob);
+  L.obs_buf[1] = o; o += align256(ob);
+  L.priv_buf[0] = o; o += align256(pb);
+  L.priv_buf[1] = o; o += align256(pb);
+  L.frame_obs = o; o += align256((size_t)n * HG_OBS1 * 4);
+  L.frame_priv = o; o += align256((size_t)n * HG_PRIV1 * 4);
+  L.cfg = o; o += align256(sizeof(hg_cfg));
+  L.model = o; o += align256(sizeof(hg_model));
+  L.off[HG_T_OBS_BUF] = L.obs_buf[0];
+  L.off[HG_T_PRIV_BUF] = L.priv_buf[0];
+  L.bytes = o;
+  return L;
+}
+
+struct Sim {
+  hg_cfg cfg;
+  hg_model model;
+  char* arena;
+  size_t bytes;
+  Layout L;
+  HgState S;
+  int parity;  // which obs/priv buffer holds the latest stack
+  std::string err;
+};
+
+int fail(Sim* s, int code, const std::string& m) {
+  if (s) s->err = m; else g_create_error = m;
+  return code;
+}
+
+__global__ void k_init(HgState S) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  const hg_cfg* c = S.cfg;
+  const int np = S.np;
+  for (int i = 0; i < 3; i++) S.root[i * np + e] = c->init_pos[i] + S.env_origins[i * np + e];
+  for (int i = 0; i < 4; i++) S.root[(3 + i) * np + e] = c->init_rot[i];
+  for (int i = 0; i < 3; i++) {
+    S.root[(7 + i) * np + e] = c->init_lin_vel[i];
+    S.root[(10 + i) * np + e] = c->init_ang_vel[i];
+  }
+  for (int j = 0; j < HG_ND; j++) S.dof_pos[j * np + e] = c->default_dof_pos[j];
+  S.last_feet_z[0 * np + e] = 0.05f;  // self.last_feet_z = 0.05 (humanoid_env.py:175)
+  S.last_feet_z[1 * np + e] = 0.05f;
+  S.body_mass[e] = S.model->mass[0];
+  S.friction[e] = 1.0f;
+  S.proj_gravity[2 * np + e] = -1.0f;
+  S.reset_buf[e] = 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t hg_arena_bytes(const hg_cfg* cfg) {
+  if (!cfg || cfg->num_envs <= 0) return 0;
+  return make_layout(cfg).bytes;
+}
+
+int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t arena_bytes, void** out_sim) {
+  if (!cfg || !model || !arena || !out_sim) return fail(nullptr, HG_ERR_ARG, "null argument");
+  if (cfg->num_envs <= 0) return fail(nullptr, HG_ERR_ARG, "num_envs must be > 0");
+  if (model->num_bodies != HG_NB || model->num_dof != HG_ND)
+    return fail(nullptr, HG_ERR_ARG, "model must have 13 bodies / 12 dofs (XBot-L profile)");
+  if (model->num_contacts <= 0 || model->num_contacts > HG_NC) return fail(nullptr, HG_ERR_ARG, "bad contact count");
+  for (int b = 1; b < HG_NB; b++)
+    if (model->parent[b] < 0 || model->parent[b] >= b) return fail(nullptr, HG_ERR_ARG, "bodies must be topologically ordered");
+  if (cfg->decimation <= 0 || cfg->sim_dt <= 0.f || cfg->frame_stack <= 0 || cfg->c_frame_stack <= 0)
+    return fail(nullptr, HG_ERR_ARG, "bad timing / stacking config");
+  if (cfg->resample_interval <= 0 || cfg->push_interval <= 0) return fail(nullptr, HG_ERR_ARG, "bad intervals");
+  if (cfg->terrain_type != 0 && (!cfg->heightfield || cfg->hf_rows < 2 || cfg->hf_cols < 2))
+    return fail(nullptr, HG_ERR_ARG, "heightfield terrain needs a device heightfield");
+  Sim* s = new Sim();
+  s->cfg = *cfg;
+  s->model = *model;
+  s->L = make_layout(cfg);
+  if (arena_bytes < s->L.bytes) {
+    delete s;
+    return fail(nullptr, HG_ERR_ARG, "arena too small");
+  }
+  if (((uintptr_t)arena & 255) != 0) {
+    delete s;
+    return fail(nullptr, HG_ERR_ARG, "arena must be 256-byte aligned");
+  }
+  s->arena = (char*)arena;
+  s->bytes = arena_bytes;
+  s->parity = 0;
+  const int n = cfg->num_envs;
+  HgState& S = s->S;
+  S.n = n;
+  S.np = (n + 63) & ~63;
+  auto P = [&](int id) { return (void*)(s->arena + s->L.off[id]); };
+  S.root = (float*)P(HG_T_ROOT_STATE);
+  S.dof_pos = (float*)P(HG_T_DOF_POS);
+  S.dof_vel = (float*)P(HG_T_DOF_VEL);
+  S.contact = (float*)P(HG_T_CONTACT_FORCES);
+  S.rigid = (float*)P(HG_T_RIGID_STATE);
+  S.torques = (float*)P(HG_T_TORQUES);
+  S.actions = (float*)P(HG_T_ACTIONS);
+  S.last_actions = (float*)P(HG_T_LAST_ACTIONS);
+  S.last_last_actions = (float*)P(HG_T_LAST_LAST_ACTIONS);
+  S.last_dof_vel = (float*)P(HG_T_LAST_DOF_VEL);
+  S.last_root_vel = (float*)P(HG_T_LAST_ROOT_VEL);
+  S.commands = (float*)P(HG_T_COMMANDS);
+  S.obs = (float*)(s->arena + s->L.obs_buf[0]);
+  S.priv = (float*)(s->arena + s->L.priv_buf[0]);
+  S.rew = (float*)P(HG_T_REW_BUF);
+  S.reset_buf = (uint8_t*)P(HG_T_RESET_BUF);
+  S.time_out = (uint8_t*)P(HG_T_TIME_OUT_BUF);
+  S.ep_len = (int64_t*)P(HG_T_EPISODE_LENGTH);
+  S.ep_sums = (float*)P(HG_T_EPISODE_SUMS);
+  S.feet_air_time = (float*)P(HG_T_FEET_AIR_TIME);
+  S.last_contacts = (uint8_t*)P(HG_T_LAST_CONTACTS);
+  S.feet_height = (float*)P(HG_T_FEET_HEIGHT);
+  S.last_feet_z = (float*)P(HG_T_LAST_FEET_Z);
+  S.friction = (float*)P(HG_T_ENV_FRICTION);
+  S.body_mass = (float*)P(HG_T_BODY_MASS);
+  S.push_force = (float*)P(HG_T_PUSH_FORCE);
+  S.push_torque = (float*)P(HG_T_PUSH_TORQUE);
+  S.base_lin_vel = (float*)P(HG_T_BASE_LIN_VEL);
+  S.base_ang_vel = (float*)P(HG_T_BASE_ANG_VEL);
+  S.proj_gravity = (float*)P(HG_T_PROJ_GRAVITY);
+  S.base_euler = (float*)P(HG_T_BASE_EULER);
+  S.ref_dof_pos = (float*)P(HG_T_REF_DOF_POS);
+  S.env_origins = (float*)P(HG_T_ENV_ORIGINS);
+  S.ep_stats = (float*)P(HG_T_EP_STATS);
+  S.lambda = (float*)P(HG_T_CONTACT_LAMBDA);
+  S.nonfinite = (int32_t*)P(HG_T_NONFINITE);
+  S.cfg = (const hg_cfg*)(s->arena + s->L.cfg);
+  S.model = (const hg_model*)(s->arena + s->L.model);
+  // zero the arena, upload cfg/model, initial state (synchronous: creation is not on the hot path)
+  if (hipMemset(arena, 0, s->L.bytes) != hipSuccess ||
+      hipMemcpy((void*)S.cfg, &s->cfg, sizeof(hg_cfg), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy((void*)S.model, &s->model, sizeof(hg_model), hipMemcpyHostToDevice) != hipSuccess) {
+    delete s;
+    return fail(nullptr, HG_ERR_HIP, "hip memset/memcpy failed (is the arena device memory?)");
+  }
+  hipLaunchKernelGGL(k_init, dim3((n + 255) / 256), dim3(256), 0, 0, S);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    delete s;
+    return fail(nullptr, HG_ERR_HIP, "init kernel failed");
+  }
+  *out_sim = s;
+  return HG_OK;
+}
+
+void hg_destroy(void* sim) { delete (Sim*)sim; }
+
+const char* hg_last_error(void* sim) {
+  if (!sim) return g_create_error.c_str();
+  return ((Sim*)sim)->err.c_str();
+}
+
+int hg_tensor(void* sim, int id, hg_desc* d) {
+  Sim* s = (Sim*)sim;
+  if (!s || !d || id < 0 || id >= HG_T_COUNT) return fail(s, HG_ERR_ARG, "bad tensor id");
+  const int64_t n = s->cfg.num_envs, np = s->S.np;
+  memset(d, 0, sizeof(*d));
+  d->offset_bytes = s->L.off[id];
+  d->dtype = dtype_of(id);
+  switch (id) {
+    case HG_T_OBS_BUF:  // both halves of the double buffer: [2, N, F*47]
+    case HG_T_PRIV_BUF: {
+      const int64_t w = id == HG_T_OBS_BUF ? (int64_t)s->cfg.frame_stack * HG_OBS1 : (int64_t)s->cfg.c_frame_stack * HG_PRIV1;
+      const size_t b1 = id == HG_T_OBS_BUF ? s->L.obs_buf[1] : s->L.priv_buf[1];
+      d->ndim = 3;
+      d->shape[0] = 2; d->shape[1] = n; d->shape[2] = w;
+      d->strides[0] = (int64_t)(b1 - d->offset_bytes) / 4; d->strides[1] = w; d->strides[2] = 1;
+      return HG_OK;
+    }
+    case HG_T_EP_STATS:
+      d->ndim = 1; d->shape[0] = 24; d->strides[0] = 1;
+      return HG_OK;
+    case HG_T_CONTACT_FORCES:
+      d->ndim = 3; d->shape[0] = n; d->shape[1] = HG_NB; d->shape[2] = 3;
+      d->strides[0] = 1; d->strides[1] = 3 * np; d->strides[2] = np;
+      return HG_OK;
+    case HG_T_RIGID_STATE:
+      d->ndim = 3; d->shape[0] = n; d->shape[1] = HG_NB; d->shape[2] = 13;
+      d->strides[0] = 1; d->strides[1] = 13 * np; d->strides[2] = np;
+      return HG_OK;
+    case HG_T_EPISODE_SUMS:
+      d->ndim = 2; d->shape[0] = HG_NUM_REWARDS; d->shape[1] = n; d->strides[0] = np; d->strides[1] = 1;
+      return HG_OK;
+    default: {
+      const int rows = soa_rows(id);
+      if (rows == 1) { d->ndim = 1; d->shape[0] = n; d->strides[0] = 1; }
+      else { d->ndim = 2; d->shape[0] = n; d->shape[1] = rows; d->strides[0] = 1; d->strides[1] = np; }
+      return HG_OK;
+    }
+  }
+}
+
+int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s || !actions) return fail(s, HG_ERR_ARG, "null argument");
+  if (hg_launch_step(&s->S, actions, step_counter, (hipStream_t)stream) != 0) return fail(s, HG_ERR_HIP, "k_step launch failed");
+  return HG_OK;
+}
+
+static int do_post(Sim* s, uint64_t counter, int mode, const uint8_t* mask, void* stream) {
+  const int p = s->parity;
+  float* ob0 = (float*)(s->arena + s->L.obs_buf[p]);
+  float* ob1 = (float*)(s->arena + s->L.obs_buf[1 - p]);
+  float* pb0 = (float*)(s->arena + s->L.priv_buf[p]);
+  float* pb1 = (float*)(s->arena + s->L.priv_buf[1 - p]);
+  const float inv_len_s = 1.0f / ((float)s->cfg.max_episode_length * s->cfg.dt);
+  int rc = hg_launch_post(&s->S, counter, mode, mask, (float*)(s->arena + s->L.frame_obs),
+                          (float*)(s->arena + s->L.frame_priv), ob0, ob1, pb0, pb1, s->cfg.frame_stack,
+                          s->cfg.c_frame_stack, inv_len_s, (hipStream_t)stream);
+  if (rc != 0) return fail(s, HG_ERR_HIP, "k_post launch failed");
+  s->parity = 1 - p;
+  return HG_OK;
+}
+
+int hg_post(void* sim, uint64_t common_step_counter, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s) return HG_ERR_ARG;
+  return do_post(s, common_step_counter, 0, nullptr, stream);
+}
+
+int hg_reset_masked(void* sim, const uint8_t* mask, uint64_t counter, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s) return HG_ERR_ARG;
+  return do_post(s, counter, 1, mask, stream);
+}
+
+}  // extern "C"
+
+// ---- indexed state writes
+__global__ void k_set_dof(HgState S, const int32_t* ids, int n, const float* pos, const float* vel) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int e = ids[i];
+  if (e < 0 || e >= S.n) return;
+  for (int j = 0; j < HG_ND; j++) {
+    if (pos) S.dof_pos[j * S.np + e] = pos[(size_t)i * HG_ND + j];
+    if (vel) S.dof_vel[j * S.np + e] = vel[(size_t)i * HG_ND + j];
+  }
+  for (int c = HG_NC * 3; c < HG_LAMW; c++) S.lambda[c * S.np + e] = 0.f;
+}
+__global__ void k_set_root(HgState S, const int32_t* ids, int n, const float* root) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int e = ids[i];
+  if (e < 0 || e >= S.n) return;
+  for (int f = 0; f < 13; f++) S.root[f * S.np + e] = root[(size_t)i * 13 + f];
+  for (int c = 0; c < HG_NC * 3; c++) S.lambda[c * S.np + e] = 0.f;
+}
+
+extern "C" int hg_set_dof_state_indexed(void* sim, const int32_t* env_ids, int n, const float* dof_pos,
+                                        const float* dof_vel, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s || !env_ids || n < 0) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  hipLaunchKernelGGL(k_set_dof, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, s->S, env_ids, n, dof_pos, dof_vel);
+  return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_dof launch failed");
+}
+
+extern "C" int hg_set_root_state_indexed(void* sim, const int32_t* env_ids, int n, const float* root, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s || !env_ids || !root || n < 0) return HG_ERR_ARG;
+  if (n == 0) return HG_OK;
+  hipLaunchKernelGGL(k_set_root, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, s->S, env_ids, n, root);
+  return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_root launch failed");
+}
+
+extern "C" const char* hg_version(void) { return "hg_sim 0.1 (gfx950, physics v1: lane-per-env)"; }

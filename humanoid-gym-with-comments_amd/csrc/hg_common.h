@@ -1,0 +1,132 @@
+// hg_common.h — device-side helpers shared by the hg_sim kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hgsim.h"
+
+#define HG_NB 13
+#define HG_ND 12
+#define HG_NV 18
+#define HG_NC 16
+#define HG_LAMW (HG_NC * 3 + HG_ND)
+#define HG_OBS1 47
+#define HG_PRIV1 73
+
+// ------------------------------------------------------------------------------------------------
+// arena: SoA per-env fields, each row padded to `np` elements (np = N rounded up to 64)
+// ------------------------------------------------------------------------------------------------
+struct HgState {
+  int n, np;
+  float* root;        // [13][np]
+  float* dof_pos;     // [12][np]
+  float* dof_vel;     // [12][np]
+  float* contact;     // [13*3][np]
+  float* rigid;       // [13*13][np]
+  float* torques;     // [12][np]
+  float* actions;     // [12][np]
+  float* last_actions;
+  float* last_last_actions;
+  float* last_dof_vel;    // [12][np]
+  float* last_root_vel;   // [6][np]
+  float* commands;        // [4][np]
+  float* obs;             // [n][frame_stack*47] row-major
+  float* priv;            // [n][c_frame_stack*73] row-major
+  float* rew;             // [np]
+  uint8_t* reset_buf;     // [np]
+  uint8_t* time_out;      // [np]
+  int64_t* ep_len;        // [np]
+  float* ep_sums;         // [22][np]
+  float* feet_air_time;   // [2][np]
+  uint8_t* last_contacts; // [2][np]
+  float* feet_height;     // [2][np]
+  float* last_feet_z;     // [2][np]
+  float* friction;        // [np]
+  float* body_mass;       // [np]
+  float* push_force;      // [3][np]
+  float* push_torque;     // [3][np]
+  float* base_lin_vel;    // [3][np]
+  float* base_ang_vel;    // [3][np]
+  float* proj_gravity;    // [3][np]
+  float* base_euler;      // [3][np]
+  float* ref_dof_pos;     // [12][np]
+  float* env_origins;     // [3][np]
+  float* ep_stats;        // [24] (+ accumulators [24] after)
+  float* lambda;          // [60][np]
+  int32_t* nonfinite;     // [np]
+  const hg_cfg* cfg;      // device copy
+  const hg_model* model;  // device copy
+};
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. SC'11).  Keyed by the run seed; counter = (a, b, c, purpose).
+// ------------------------------------------------------------------------------------------------
+struct u4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    u4 n = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+enum HgRngPurpose : uint32_t {
+  RNG_ACT_DELAY = 1, RNG_ACT_NOISE = 2, RNG_OBS_NOISE = 3, RNG_CMD = 4, RNG_PUSH = 5,
+  RNG_RESET_DOF = 6, RNG_RESET_ROOT = 7,
+};
+
+// uniform in [0,1): 24 high bits
+__host__ __device__ inline float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+// uniform in (0,1]
+__host__ __device__ inline float u01_open0(uint32_t x) { return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f); }
+
+__device__ inline u4 rng4(const hg_cfg* cfg, uint32_t env, uint64_t step, uint32_t block, uint32_t purpose) {
+  u4 c = {env, (uint32_t)step, (block & 0xFFFFu) | ((uint32_t)(step >> 32) << 16), purpose};
+  return philox4x32_10(c, (uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32));
+}
+
+// Box–Muller: 4 uniforms -> 4 standard normals
+__device__ inline void normals4(u4 r, float* z) {
+  const float two_pi = 6.283185307179586f;
+  float r0 = sqrtf(-2.0f * logf(u01_open0(r.x)));
+  float r1 = sqrtf(-2.0f * logf(u01_open0(r.z)));
+  float s0, c0, s1, c1;
+  sincosf(two_pi * u01(r.y), &s0, &c0);
+  sincosf(two_pi * u01(r.w), &s1, &c1);
+  z[0] = r0 * c0; z[1] = r0 * s0; z[2] = r1 * c1; z[3] = r1 * s1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// small vector math
+// ------------------------------------------------------------------------------------------------
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// xyzw quaternion rotate-inverse, as isaacgym.torch_utils.quat_rotate_inverse
+__device__ __forceinline__ f3 quat_rotate_inverse(float qx, float qy, float qz, float qw, f3 v) {
+  f3 qv = mk(qx, qy, qz);
+  f3 a = (2.0f * qw * qw - 1.0f) * v;
+  f3 b = (qw * 2.0f) * cross(qv, v);
+  f3 c = (2.0f * dot(qv, v)) * qv;
+  return a - b + c;
+}
+__device__ __forceinline__ f3 quat_apply(float qx, float qy, float qz, float qw, f3 v) {
+  f3 xyz = mk(qx, qy, qz);
+  f3 t = 2.0f * cross(xyz, v);
+  return v + qw * t + cross(xyz, t);
+}

@@ -1,0 +1,474 @@
+// hg_envlogic.hip — K_post: post-physics env logic for every env, one lane per env, no host sync.
+//
+// Replaces reference humanoid/envs/custom/humanoid_env.py:
+//   post_physics_step :770-809 (minus refreshes), _post_physics_step_callback :1000-1016,
+//   _resample_commands :1018-1032, _push_robots :665-681, check_termination :811-816,
+//   compute_reward :889-907 + the 22 _reward_* terms :1170-1437, reset_idx :1109-1163
+//   (+ _reset_dofs :1034-1048, _reset_root_states :1049-1072), compute_observations :818-887,
+//   _get_phase/_get_gait_phase/compute_ref_state :683-744, _get_noise_scale_vec :748-768,
+//   and the obs/priv clip in step() :654-657.
+// Reset is mask-based (the reference's reset_buf.nonzero() host sync :796 is gone).
+// Frame stacking (deque append + stack, :880-887) is k_stack below: a coalesced double-buffered
+// shift of the [N, frames*width] row-major history.
+#include "hg_common.h"
+
+namespace {
+
+constexpr float kPiF = 3.14159265358979323846f;     // float(np.pi)
+constexpr float kTwoPiF = 6.28318530717958647692f;  // float(2*np.pi)
+
+// isaacgym get_euler_xyz (components mod 2pi) followed by get_euler_xyz_tensor's
+// "euler[euler > pi] -= 2pi" (humanoid_env.py:51-56)
+__device__ __forceinline__ float wrap_euler(float a) {
+  a = a - kTwoPiF * floorf(a / kTwoPiF);
+  if (a > kPiF) a -= kTwoPiF;
+  return a;
+}
+__device__ f3 euler_xyz(float x, float y, float z, float w) {
+  float sinr = 2.0f * (w * x + y * z);
+  float cosr = w * w - x * x - y * y + z * z;
+  float roll = atan2f(sinr, cosr);
+  float sinp = 2.0f * (w * y - z * x);
+  float pitch = fabsf(sinp) >= 1.0f ? copysignf(kPiF / 2.0f, sinp) : asinf(sinp);
+  float siny = 2.0f * (w * z + x * y);
+  float cosy = w * w + x * x - y * y - z * z;
+  float yaw = atan2f(siny, cosy);
+  return mk(wrap_euler(roll), wrap_euler(pitch), wrap_euler(yaw));
+}
+// humanoid/utils/math.py:46-49
+__device__ __forceinline__ float wrap_to_pi(float a) {
+  a = a - kTwoPiF * floorf(a / kTwoPiF);
+  if (a > kPiF) a -= kTwoPiF;
+  return a;
+}
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+struct Gait { float sin_pos, cos_pos, stance[2]; };
+
+// _get_phase / _get_gait_phase (humanoid_env.py:683-703)
+__device__ Gait gait(const hg_cfg* cfg, int64_t ep) {
+  float phase = (float)ep * cfg->dt / cfg->cycle_time;
+  Gait g;
+  g.sin_pos = sinf(kTwoPiF * phase);
+  g.cos_pos = cosf(kTwoPiF * phase);
+  g.stance[0] = g.sin_pos >= 0.f ? 1.f : 0.f;
+  g.stance[1] = g.sin_pos < 0.f ? 1.f : 0.f;
+  if (fabsf(g.sin_pos) < 0.1f) g.stance[0] = g.stance[1] = 1.f;
+  return g;
+}
+
+// _resample_commands (humanoid_env.py:1018-1032) for one env
+__device__ void resample_commands(const hg_cfg* cfg, HgState& S, int e, uint64_t step, uint32_t salt) {
+  const int np = S.np;
+  u4 r = rng4(cfg, e, step, salt, RNG_CMD);
+  float cx = (cfg->cmd_lin_x[1] - cfg->cmd_lin_x[0]) * u01(r.x) + cfg->cmd_lin_x[0];
+  float cy = (cfg->cmd_lin_y[1] - cfg->cmd_lin_y[0]) * u01(r.y) + cfg->cmd_lin_y[0];
+  S.commands[0 * np + e] = cx;
+  S.commands[1 * np + e] = cy;
+  if (cfg->heading_command)
+    S.commands[3 * np + e] = (cfg->cmd_heading[1] - cfg->cmd_heading[0]) * u01(r.z) + cfg->cmd_heading[0];
+  else
+    S.commands[2 * np + e] = (cfg->cmd_ang_yaw[1] - cfg->cmd_ang_yaw[0]) * u01(r.z) + cfg->cmd_ang_yaw[0];
+  float keep = sqrtf(cx * cx + cy * cy) > 0.2f ? 1.f : 0.f;
+  S.commands[0 * np + e] = cx * keep;
+  S.commands[1 * np + e] = cy * keep;
+}
+
+// reset_idx for one env (humanoid_env.py:1109-1163); episode stats accumulate into ep_stats[24..]
+__device__ void reset_env(const hg_cfg* cfg, HgState& S, int e, uint64_t step, int nrew) {
+  const int np = S.np;
+  // _reset_dofs
+  for (int b = 0; b < 3; b++) {
+    u4 r = rng4(cfg, e, step, b, RNG_RESET_DOF);
+    uint32_t u[4] = {r.x, r.y, r.z, r.w};
+    for (int i = 0; i < 4; i++) {
+      int j = b * 4 + i;
+      S.dof_pos[j * np + e] = cfg->default_dof_pos[j] + (0.1f - (-0.1f)) * u01(u[i]) + (-0.1f);
+      S.dof_vel[j * np + e] = 0.f;
+    }
+  }
+  // _reset_root_states
+  float root[13];
+  for (int i = 0; i < 3; i++) root[i] = cfg->init_pos[i] + S.env_origins[i * np + e];
+  for (int i = 0; i < 4; i++) root[3 + i] = cfg->init_rot[i];
+  for (int i = 0; i < 3; i++) { root[7 + i] = cfg->init_lin_vel[i]; root[10 + i] = cfg->init_ang_vel[i]; }
+  if (cfg->terrain_type != 0) {  // custom origins: xy within 1 m of the centre
+    u4 r = rng4(cfg, e, step, 0, RNG_RESET_ROOT);
+    root[0] += 2.0f * u01(r.x) - 1.0f;
+    root[1] += 2.0f * u01(r.y) - 1.0f;
+  }
+  if (cfg->fix_base_link) {
+    for (int i = 7; i < 13; i++) root[i] = 0.f;
+    root[2] += 1.8f;
+  }
+  for (int i = 0; i < 13; i++) S.root[i * np + e] = root[i];
+  for (int i = 0; i < HG_LAMW; i++) S.lambda[i * np + e] = 0.f;
+  resample_commands(cfg, S, e, step, 1);
+  for (int j = 0; j < HG_ND; j++) {
+    S.last_last_actions[j * np + e] = 0.f;
+    S.actions[j * np + e] = 0.f;
+    S.last_actions[j * np + e] = 0.f;
+    S.last_dof_vel[j * np + e] = 0.f;
+  }
+  S.feet_air_time[0 * np + e] = 0.f;
+  S.feet_air_time[1 * np + e] = 0.f;
+  S.ep_len[e] = 0;
+  S.reset_buf[e] = 1;
+  float* acc = S.ep_stats + 24;
+  for (int k = 0; k < nrew; k++) {
+    atomicAdd(&acc[k], S.ep_sums[k * np + e]);
+    S.ep_sums[k * np + e] = 0.f;
+  }
+  atomicAdd(&acc[22], 1.0f);
+  // refresh base quat -> projected gravity (euler is recomputed by the obs pass)
+  f3 g = quat_rotate_inverse(root[3], root[4], root[5], root[6], mk(0, 0, -1));
+  S.proj_gravity[0 * np + e] = g.x;
+  S.proj_gravity[1 * np + e] = g.y;
+  S.proj_gravity[2 * np + e] = g.z;
+}
+
+}  // namespace
+
+// mode 0: full post_physics_step; mode 1: reset envs in `mask` (all if null) + observe
+__global__ void __launch_bounds__(256) k_post(HgState S, uint64_t counter, int mode, const uint8_t* mask,
+                                              float* frame_obs, float* frame_priv) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  const hg_cfg* cfg = S.cfg;
+  const int np = S.np;
+  const int nrew = HG_NUM_REWARDS;
+  float q[HG_ND], qd[HG_ND], a[HG_ND];
+  bool do_reset;
+
+  if (mode == 0) {
+    int64_t ep = S.ep_len[e] + 1;
+    S.ep_len[e] = ep;
+    float qx = S.root[3 * np + e], qy = S.root[4 * np + e], qz = S.root[5 * np + e], qw = S.root[6 * np + e];
+    f3 lv = mk(S.root[7 * np + e], S.root[8 * np + e], S.root[9 * np + e]);
+    f3 av = mk(S.root[10 * np + e], S.root[11 * np + e], S.root[12 * np + e]);
+    f3 blv = quat_rotate_inverse(qx, qy, qz, qw, lv);
+    f3 bav = quat_rotate_inverse(qx, qy, qz, qw, av);
+    f3 pg = quat_rotate_inverse(qx, qy, qz, qw, mk(0, 0, -1));
+    f3 eul = euler_xyz(qx, qy, qz, qw);
+    S.base_lin_vel[0 * np + e] = blv.x; S.base_lin_vel[1 * np + e] = blv.y; S.base_lin_vel[2 * np + e] = blv.z;
+    S.base_ang_vel[0 * np + e] = bav.x; S.base_ang_vel[1 * np + e] = bav.y; S.base_ang_vel[2 * np + e] = bav.z;
+    S.proj_gravity[0 * np + e] = pg.x; S.proj_gravity[1 * np + e] = pg.y; S.proj_gravity[2 * np + e] = pg.z;
+    // ---- _post_physics_step_callback
+    if (ep % cfg->resample_interval == 0) resample_commands(cfg, S, e, counter, 0);
+    if (cfg->heading_command) {
+      f3 fwd = quat_apply(qx, qy, qz, qw, mk(1, 0, 0));
+      float heading = atan2f(fwd.y, fwd.x);
+      float c2 = 0.5f * wrap_to_pi(S.commands[3 * np + e] - heading);
+      S.commands[2 * np + e] = fminf(fmaxf(c2, -1.f), 1.f);
+    }
+    if (cfg->push_robots && (counter % (uint64_t)cfg->push_interval == 0)) {
+      u4 r0 = rng4(cfg, e, counter, 0, RNG_PUSH), r1 = rng4(cfg, e, counter, 1, RNG_PUSH);
+      const float mv = cfg->max_push_vel_xy, ma = cfg->max_push_ang_vel;
+      float px = 2.f * mv * u01(r0.x) - mv, py = 2.f * mv * u01(r0.y) - mv;
+      S.push_force[0 * np + e] = px; S.push_force[1 * np + e] = py;
+      S.root[7 * np + e] = px; S.root[8 * np + e] = py;
+      float t0 = 2.f * ma * u01(r0.z) - ma, t1 = 2.f * ma * u01(r0.w) - ma, t2 = 2.f * ma * u01(r1.x) - ma;
+      S.push_torque[0 * np + e] = t0; S.push_torque[1 * np + e] = t1; S.push_torque[2 * np + e] = t2;
+      S.root[10 * np + e] = t0; S.root[11 * np + e] = t1; S.root[12 * np + e] = t2;
+    }
+    // ---- check_termination
+    f3 fb = mk(S.contact[0 * np + e], S.contact[1 * np + e], S.contact[2 * np + e]);
+    float fbn = sqrtf(dot(fb, fb));
+    bool timeout = ep > (int64_t)cfg->max_episode_length;
+    do_reset = (fbn > 1.0f) || timeout;
+    S.time_out[e] = timeout;
+    S.reset_buf[e] = do_reset;
+    // ---- compute_reward
+    for (int j = 0; j < HG_ND; j++) {
+      q[j] = S.dof_pos[j * np + e];
+      qd[j] = S.dof_vel[j * np + e];
+      a[j] = S.actions[j * np + e];
+    }
+    Gait g = gait(cfg, ep);
+    const int f0 = cfg->feet_body[0], f1 = cfg->feet_body[1];
+    const int k0 = cfg->knee_body[0], k1 = cfg->knee_body[1];
+    auto rig = [&](int b, int f) { return S.rigid[((size_t)b * 13 + f) * np + e]; };
+    auto cfz = [&](int b, int i) { return S.contact[((size_t)b * 3 + i) * np + e]; };
+    bool contact[2] = {cfz(f0, 2) > 5.f, cfz(f1, 2) > 5.f};
+    float term[HG_NUM_REWARDS];
+    // 0 action_smoothness
+    {
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f;
+      for (int j = 0; j < HG_ND; j++) {
+        float la = S.last_actions[j * np + e], lla = S.last_last_actions[j * np + e];
+        float d1 = la - a[j], d2 = a[j] + lla - 2.f * la;
+        t1 += d1 * d1; t2 += d2 * d2; t3 += fabsf(a[j]);
+      }
+      term[0] = t1 + t2 + 0.05f * t3;
+    }
+    // 1 base_acc
+    {
+      float s = 0.f;
+      for (int i = 0; i < 6; i++) { float d = S.last_root_vel[i * np + e] - S.root[(7 + i) * np + e]; s += d * d; }
+      term[1] = expf(-sqrtf(s) * 3.f);
+    }
+    // 2 base_height
+    {
+      float mh = (rig(f0, 2) * g.stance[0] + rig(f1, 2) * g.stance[1]) / (g.stance[0] + g.stance[1]);
+      float bh = S.root[2 * np + e] - (mh - 0.05f);
+      term[2] = expf(-fabsf(bh - cfg->base_height_target) * 100.f);
+    }
+    // 3 collision (penalised body = base)
+    term[3] = fbn > 0.1f ? 1.f : 0.f;
+    // 4 default_joint_pos
+    {
+      float dn = 0.f, d[HG_ND];
+      for (int j = 0; j < HG_ND; j++) { d[j] = q[j] - cfg->default_dof_pos[j]; dn += d[j] * d[j]; }
+      const int* yr = cfg->yaw_roll_idx;
+      float l = sqrtf(d[yr[0]] * d[yr[0]] + d[yr[1]] * d[yr[1]]);
+      float r = sqrtf(d[yr[2]] * d[yr[2]] + d[yr[3]] * d[yr[3]]);
+      float y = fminf(fmaxf(l + r - 0.1f, 0.f), 50.f);
+      term[4] = expf(-y * 100.f) - 0.01f * sqrtf(dn);
+    }
+    // 5 dof_acc, 6 dof_vel, 17 torques
+    {
+      float sa = 0.f, sv = 0.f, st = 0.f;
+      for (int j = 0; j < HG_ND; j++) {
+        float acc = (S.last_dof_vel[j * np + e] - qd[j]) / cfg->dt;
+        sa += acc * acc;
+        sv += qd[j] * qd[j];
+        float t = S.torques[j * np + e];
+        st += t * t;
+      }
+      term[5] = sa; term[6] = sv; term[17] = st;
+    }
+    // 7 feet_air_time (mutates last_contacts, feet_air_time)
+    {
+      float r = 0.f;
+      for (int f = 0; f < 2; f++) {
+        bool lc = S.last_contacts[f * np + e] != 0;
+        bool filt = contact[f] || (g.stance[f] != 0.f) || lc;
+        float air = S.feet_air_time[f * np + e];
+        float first = (air > 0.f && filt) ? 1.f : 0.f;
+        if (cfg->reward_scale[7] != 0.f) {
+          S.last_contacts[f * np + e] = contact[f];
+          air += cfg->dt;
+          r += fminf(fmaxf(air, 0.f), 0.5f) * first;
+          S.feet_air_time[f * np + e] = filt ? 0.f : air;
+        }
+      }
+      term[7] = r;
+    }
+    // 8 feet_clearance (mutates feet_height, last_feet_z)
+    {
+      float r = 0.f;
+      for (int f = 0; f < 2; f++) {
+        const int fb2 = f == 0 ? f0 : f1;
+        float fz = rig(fb2, 2) - 0.05f;
+        float fh = S.feet_height[f * np + e] + (fz - S.last_feet_z[f * np + e]);
+        float swing = 1.f - g.stance[f];
+        float pos = fabsf(fh - cfg->target_feet_height) < 0.01f ? 1.f : 0.f;
+        r += pos * swing;
+        if (cfg->reward_scale[8] != 0.f) {
+          S.last_feet_z[f * np + e] = fz;
+          S.feet_height[f * np + e] = contact[f] ? 0.f : fh;
+        }
+      }
+      term[8] = r;
+    }
+    // 9 feet_contact_forces, 10 feet_contact_number, 12 foot_slip
+    {
+      float s9 = 0.f, s10 = 0.f, s12 = 0.f;
+      for (int f = 0; f < 2; f++) {
+        const int fb2 = f == 0 ? f0 : f1;
+        float fx = cfz(fb2, 0), fy = cfz(fb2, 1), fz = cfz(fb2, 2);
+        s9 += fminf(fmaxf(sqrtf(fx * fx + fy * fy + fz * fz) - cfg->max_contact_force, 0.f), 400.f);
+        s10 += ((contact[f] ? 1.f : 0.f) == g.stance[f]) ? 1.f : -0.3f;
+        float wx = rig(fb2, 10), wy = rig(fb2, 11);
+        s12 += contact[f] ? sqrtf(sqrtf(wx * wx + wy * wy)) : 0.f;
+      }
+      term[9] = s9; term[10] = s10 / 2.f; term[12] = s12;
+    }
+    // 11 feet_distance, 14 knee_distance
+    {
+      float dx = rig(f0, 0) - rig(f1, 0), dy = rig(f0, 1) - rig(f1, 1);
+      float d = sqrtf(dx * dx + dy * dy);
+      float dmin = fminf(fmaxf(d - cfg->min_dist, -0.5f), 0.f);
+      float dmax = fminf(fmaxf(d - cfg->max_dist, 0.f), 0.5f);
+      term[11] = (expf(-fabsf(dmin) * 100.f) + expf(-fabsf(dmax) * 100.f)) / 2.f;
+      dx = rig(k0, 0) - rig(k1, 0); dy = rig(k0, 1) - rig(k1, 1);
+      d = sqrtf(dx * dx + dy * dy);
+      dmin = fminf(fmaxf(d - cfg->min_dist, -0.5f), 0.f);
+      dmax = fminf(fmaxf(d - cfg->max_dist / 2.f, 0.f), 0.5f);
+      term[14] = (expf(-fabsf(dmin) * 100.f) + expf(-fabsf(dmax) * 100.f)) / 2.f;
+    }
+    // 13 joint_pos (ref_dof_pos from the previous observation pass)
+    {
+      float s = 0.f;
+      for (int j = 0; j < HG_ND; j++) { float d = q[j] - S.ref_dof_pos[j * np + e]; s += d * d; }
+      float nrm = sqrtf(s);
+      term[13] = expf(-2.f * nrm) - 0.2f * fminf(fmaxf(nrm, 0.f), 0.5f);
+    }
+    const float cmd0 = S.commands[0 * np + e], cmd1 = S.commands[1 * np + e], cmd2 = S.commands[2 * np + e];
+    // 15 low_speed
+    {
+      float as = fabsf(blv.x), ac = fabsf(cmd0);
+      bool low = as < 0.5f * ac, high = as > 1.2f * ac, des = !(low || high);
+      bool mis = sgnf(blv.x) != sgnf(cmd0);
+      float r = 0.f;
+      if (low) r = -1.f;
+      if (high) r = 0.f;
+      if (des) r = 1.2f;
+      if (mis) r = -2.f;
+      term[15] = r * (fabsf(cmd0) > 0.1f ? 1.f : 0.f);
+    }
+    // 16 orientation
+    term[16] = (expf(-(fabsf(eul.x) + fabsf(eul.y)) * 10.f) + expf(-sqrtf(pg.x * pg.x + pg.y * pg.y) * 20.f)) / 2.f;
+    // 18 track_vel_hard, 19 tracking_ang_vel, 20 tracking_lin_vel, 21 vel_mismatch_exp
+    {
+      float ex = cmd0 - blv.x, ey = cmd1 - blv.y;
+      float lin_err = sqrtf(ex * ex + ey * ey);
+      float ang_err = fabsf(cmd2 - bav.z);
+      term[18] = (expf(-lin_err * 10.f) + expf(-ang_err * 10.f)) / 2.f - 0.2f * (lin_err + ang_err);
+      float ae = cmd2 - bav.z;
+      term[19] = expf(-(ae * ae) * cfg->tracking_sigma);
+      term[20] = expf(-(ex * ex + ey * ey) * cfg->tracking_sigma);
+      term[21] = (expf(-(blv.z * blv.z) * 10.f) + expf(-sqrtf(bav.x * bav.x + bav.y * bav.y) * 5.f)) / 2.f;
+    }
+    float rew = 0.f;
+    for (int k = 0; k < nrew; k++) {
+      float r = term[k] * cfg->reward_scale[k];
+      rew += r;
+      S.ep_sums[k * np + e] += r;
+    }
+    if (cfg->only_positive_rewards) rew = fmaxf(rew, 0.f);
+    S.rew[e] = rew;
+  } else {
+    do_reset = (mask == nullptr) || mask[e] != 0;
+    if (!do_reset) S.reset_buf[e] = 0;
+  }
+
+  // ---- reset_idx (masked)
+  if (do_reset) reset_env(cfg, S, e, counter, nrew);
+
+  // ---- compute_observations (humanoid_env.py:818-887)
+  {
+    int64_t ep = S.ep_len[e];
+    Gait g = gait(cfg, ep);
+    float qx = S.root[3 * np + e], qy = S.root[4 * np + e], qz = S.root[5 * np + e], qw = S.root[6 * np + e];
+    f3 eul = euler_xyz(qx, qy, qz, qw);
+    S.base_euler[0 * np + e] = eul.x; S.base_euler[1 * np + e] = eul.y; S.base_euler[2 * np + e] = eul.z;
+    // compute_ref_state
+    float ref[HG_ND];
+    for (int j = 0; j < HG_ND; j++) ref[j] = 0.f;
+    const float sl = fminf(g.sin_pos, 0.f), sr = fmaxf(g.sin_pos, 0.f);
+    const float s1 = cfg->target_joint_pos_scale, s2 = 2.f * s1;
+    const int* ri = cfg->ref_idx;
+    ref[ri[0]] = sl * s1; ref[ri[1]] = sl * s2; ref[ri[2]] = sl * s1;
+    ref[ri[3]] = sr * s1; ref[ri[4]] = sr * s2; ref[ri[5]] = sr * s1;
+    if (fabsf(g.sin_pos) < 0.1f)
+      for (int j = 0; j < HG_ND; j++) ref[j] = 0.f;
+    for (int j = 0; j < HG_ND; j++) S.ref_dof_pos[j * np + e] = ref[j];
+    const int f0 = cfg->feet_body[0], f1 = cfg->feet_body[1];
+    float cm0 = S.contact[((size_t)f0 * 3 + 2) * np + e] > 5.f ? 1.f : 0.f;
+    float cm1 = S.contact[((size_t)f1 * 3 + 2) * np + e] > 5.f ? 1.f : 0.f;
+    float c0 = S.commands[0 * np + e] * cfg->obs_lin_vel, c1 = S.commands[1 * np + e] * cfg->obs_lin_vel;
+    float c2 = S.commands[2 * np + e] * cfg->obs_ang_vel;
+    float* P = frame_priv + (size_t)e * HG_PRIV1;
+    float* O = frame_obs + (size_t)e * HG_OBS1;
+    const float clip = cfg->clip_observations;
+    auto cl = [clip](float v) { return fminf(fmaxf(v, -clip), clip); };
+    // privileged frame (73)
+    P[0] = cl(g.sin_pos); P[1] = cl(g.cos_pos); P[2] = cl(c0); P[3] = cl(c1); P[4] = cl(c2);
+    for (int j = 0; j < HG_ND; j++) {
+      float qj = S.dof_pos[j * np + e], qdj = S.dof_vel[j * np + e], aj = S.actions[j * np + e];
+      P[5 + j] = cl((qj - cfg->default_dof_pos[j]) * cfg->obs_dof_pos);
+      P[17 + j] = cl(qdj * cfg->obs_dof_vel);
+      P[29 + j] = cl(aj);
+      P[41 + j] = cl(qj - ref[j]);
+    }
+    f3 blv = mk(S.base_lin_vel[0 * np + e], S.base_lin_vel[1 * np + e], S.base_lin_vel[2 * np + e]);
+    f3 bav = mk(S.base_ang_vel[0 * np + e], S.base_ang_vel[1 * np + e], S.base_ang_vel[2 * np + e]);
+    P[53] = cl(blv.x * cfg->obs_lin_vel); P[54] = cl(blv.y * cfg->obs_lin_vel); P[55] = cl(blv.z * cfg->obs_lin_vel);
+    P[56] = cl(bav.x * cfg->obs_ang_vel); P[57] = cl(bav.y * cfg->obs_ang_vel); P[58] = cl(bav.z * cfg->obs_ang_vel);
+    P[59] = cl(eul.x * cfg->obs_quat); P[60] = cl(eul.y * cfg->obs_quat); P[61] = cl(eul.z * cfg->obs_quat);
+    P[62] = cl(S.push_force[0 * np + e]); P[63] = cl(S.push_force[1 * np + e]);
+    P[64] = cl(S.push_torque[0 * np + e]); P[65] = cl(S.push_torque[1 * np + e]); P[66] = cl(S.push_torque[2 * np + e]);
+    P[67] = cl(S.friction[e]);
+    P[68] = cl(S.body_mass[e] / 30.f);
+    P[69] = g.stance[0]; P[70] = g.stance[1];
+    P[71] = cm0; P[72] = cm1;
+    // observation frame (47) + noise
+    float z[48];
+    if (cfg->add_noise) {
+      for (int b = 0; b < 12; b++) normals4(rng4(cfg, e, counter, b, RNG_OBS_NOISE), z + 4 * b);
+    } else {
+      for (int i = 0; i < 48; i++) z[i] = 0.f;
+    }
+    const float nl = cfg->noise_level;
+    O[0] = cl(g.sin_pos); O[1] = cl(g.cos_pos); O[2] = cl(c0); O[3] = cl(c1); O[4] = cl(c2);
+    for (int j = 0; j < HG_ND; j++) {
+      float qj = S.dof_pos[j * np + e], qdj = S.dof_vel[j * np + e], aj = S.actions[j * np + e];
+      O[5 + j] = cl((qj - cfg->default_dof_pos[j]) * cfg->obs_dof_pos + z[5 + j] * (cfg->noise_dof_pos * cfg->obs_dof_pos) * nl);
+      O[17 + j] = cl(qdj * cfg->obs_dof_vel + z[17 + j] * (cfg->noise_dof_vel * cfg->obs_dof_vel) * nl);
+      O[29 + j] = cl(aj);
+    }
+    O[41] = cl(bav.x * cfg->obs_ang_vel + z[41] * (cfg->noise_ang_vel * cfg->obs_ang_vel) * nl);
+    O[42] = cl(bav.y * cfg->obs_ang_vel + z[42] * (cfg->noise_ang_vel * cfg->obs_ang_vel) * nl);
+    O[43] = cl(bav.z * cfg->obs_ang_vel + z[43] * (cfg->noise_ang_vel * cfg->obs_ang_vel) * nl);
+    O[44] = cl(eul.x * cfg->obs_quat + z[44] * (cfg->noise_quat * cfg->obs_quat) * nl);
+    O[45] = cl(eul.y * cfg->obs_quat + z[45] * (cfg->noise_quat * cfg->obs_quat) * nl);
+    O[46] = cl(eul.z * cfg->obs_quat + z[46] * (cfg->noise_quat * cfg->obs_quat) * nl);
+  }
+  // ---- last_* copies (post_physics_step :802-806)
+  if (mode == 0) {
+    for (int j = 0; j < HG_ND; j++) {
+      S.last_last_actions[j * np + e] = S.last_actions[j * np + e];
+      S.last_actions[j * np + e] = S.actions[j * np + e];
+      S.last_dof_vel[j * np + e] = S.dof_vel[j * np + e];
+    }
+    for (int i = 0; i < 6; i++) S.last_root_vel[i * np + e] = S.root[(7 + i) * np + e];
+  }
+}
+
+// history stacking: dst[e] = [src[e][W:], frame[e]] (src zeroed for reset envs); one thread per
+// output element so both the reads and the writes are contiguous.
+__global__ void __launch_bounds__(256) k_stack(const float* __restrict__ src, float* __restrict__ dst,
+                                               const float* __restrict__ frame, const uint8_t* __restrict__ reset,
+                                               int n, int width, int frames) {
+  const int row = frames * width;
+  const int64_t total = (int64_t)n * row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(i / row);
+    const int k = (int)(i - (int64_t)e * row);
+    float v;
+    if (k >= row - width) v = frame[(size_t)e * width + (k - (row - width))];
+    else v = reset[e] ? 0.f : src[(size_t)e * row + k + width];
+    dst[i] = v;
+  }
+}
+
+// episode statistics: ep_stats[k] = acc[k] / n_reset / episode_length_s when any env reset
+__global__ void k_ep_stats(float* ep_stats, float inv_len_s) {
+  const int k = threadIdx.x;
+  float* acc = ep_stats + 24;
+  const float cnt = acc[22];
+  __syncthreads();
+  if (k < HG_NUM_REWARDS && cnt > 0.f) ep_stats[k] = acc[k] / cnt * inv_len_s;
+  if (k == 22) ep_stats[22] = cnt;
+  if (k == 23) ep_stats[23] = cnt > 0.f ? 1.f : 0.f;
+  __syncthreads();
+  if (k < 24) acc[k] = 0.f;
+}
+
+extern "C" int hg_launch_post(const HgState* S, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
+                              float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
+                              float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
+                              hipStream_t stream) {
+  const int n = S->n;
+  hipLaunchKernelGGL(k_post, dim3((n + 255) / 256), dim3(256), 0, stream, *S, counter, mode, mask, frame_obs,
+                     frame_priv);
+  const int64_t to = (int64_t)n * frame_stack * HG_OBS1, tp = (int64_t)n * c_frame_stack * HG_PRIV1;
+  int go = (int)std::min<int64_t>((to + 255) / 256, 4096), gp = (int)std::min<int64_t>((tp + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_stack, dim3(go), dim3(256), 0, stream, obs_src, obs_dst, frame_obs, S->reset_buf, n, HG_OBS1,
+                     frame_stack);
+  hipLaunchKernelGGL(k_stack, dim3(gp), dim3(256), 0, stream, priv_src, priv_dst, frame_priv, S->reset_buf, n,
+                     HG_PRIV1, c_frame_stack);
+  hipLaunchKernelGGL(k_ep_stats, dim3(1), dim3(64), 0, stream, S->ep_stats, inv_len_s);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -1,0 +1,208 @@
+"""ctypes binding of the hg_sim C ABI (include/hgsim.h).
+
+This module is the Python side of the drop-in boundary: it mirrors the C structs, loads the
+in-tree HIP library ``csrc/libhgsim.so`` and wraps arena sub-buffers as zero-copy torch tensors
+(the role ``gymtorch.wrap_tensor`` plays in the reference, humanoid/envs/custom/humanoid_env.py:246-254).
+
+There is deliberately NO CPU fallback: if the library or a GPU is missing, ``lib()`` raises.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "csrc", "libhgsim.so")
+MODEL_PATH = os.path.join(PKG_ROOT, "model", "xbotl_model.json")
+
+HG_MAX_BODIES = 16
+HG_MAX_DOF = 12
+HG_MAX_CONTACTS = 16
+HG_NUM_REWARDS = 22
+
+f32 = ctypes.c_float
+i32 = ctypes.c_int32
+
+
+class HgModel(ctypes.Structure):
+    _fields_ = [
+        ("num_bodies", i32), ("num_dof", i32), ("num_contacts", i32), ("num_foot_contacts", i32),
+        ("parent", i32 * HG_MAX_BODIES), ("contact_body", i32 * HG_MAX_CONTACTS),
+        ("joint_pos", (f32 * 3) * HG_MAX_BODIES), ("joint_rot", (f32 * 9) * HG_MAX_BODIES),
+        ("axis", (f32 * 3) * HG_MAX_BODIES), ("mass", f32 * HG_MAX_BODIES),
+        ("com", (f32 * 3) * HG_MAX_BODIES), ("inertia", (f32 * 6) * HG_MAX_BODIES),
+        ("armature", f32 * HG_MAX_BODIES), ("lower", f32 * HG_MAX_BODIES), ("upper", f32 * HG_MAX_BODIES),
+        ("contact_pos", (f32 * 3) * HG_MAX_CONTACTS),
+    ]
+
+
+class HgCfg(ctypes.Structure):
+    _fields_ = [
+        ("num_envs", i32), ("decimation", i32), ("pgs_iterations", i32), ("fix_base_link", i32),
+        ("sim_dt", f32), ("gravity_z", f32), ("contact_offset", f32), ("max_depenetration_vel", f32),
+        ("baumgarte", f32), ("ground_friction", f32),
+        ("action_scale", f32), ("clip_actions", f32), ("dynamic_randomization", f32),
+        ("kp", f32 * HG_MAX_DOF), ("kd", f32 * HG_MAX_DOF), ("torque_limit", f32 * HG_MAX_DOF),
+        ("default_dof_pos", f32 * HG_MAX_DOF),
+        ("terrain_type", i32), ("hf_rows", i32), ("hf_cols", i32),
+        ("hf_horizontal_scale", f32), ("hf_vertical_scale", f32), ("hf_border", f32),
+        ("heightfield", ctypes.c_void_p),
+        ("frame_stack", i32), ("c_frame_stack", i32), ("max_episode_length", i32),
+        ("resample_interval", i32), ("push_interval", i32),
+        ("push_robots", i32), ("add_noise", i32), ("heading_command", i32), ("only_positive_rewards", i32),
+        ("dt", f32), ("cycle_time", f32), ("target_joint_pos_scale", f32), ("target_feet_height", f32),
+        ("base_height_target", f32), ("min_dist", f32), ("max_dist", f32), ("tracking_sigma", f32),
+        ("max_contact_force", f32), ("max_push_vel_xy", f32), ("max_push_ang_vel", f32),
+        ("cmd_lin_x", f32 * 2), ("cmd_lin_y", f32 * 2), ("cmd_ang_yaw", f32 * 2), ("cmd_heading", f32 * 2),
+        ("noise_level", f32), ("noise_dof_pos", f32), ("noise_dof_vel", f32), ("noise_ang_vel", f32),
+        ("noise_quat", f32),
+        ("obs_lin_vel", f32), ("obs_ang_vel", f32), ("obs_dof_pos", f32), ("obs_dof_vel", f32), ("obs_quat", f32),
+        ("clip_observations", f32),
+        ("init_pos", f32 * 3), ("init_rot", f32 * 4), ("init_lin_vel", f32 * 3), ("init_ang_vel", f32 * 3),
+        ("reward_scale", f32 * HG_NUM_REWARDS),
+        ("feet_body", i32 * 2), ("knee_body", i32 * 2), ("ref_idx", i32 * 6), ("yaw_roll_idx", i32 * 4),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class HgDesc(ctypes.Structure):
+    _fields_ = [("offset_bytes", ctypes.c_size_t), ("dtype", i32), ("ndim", i32),
+                ("shape", ctypes.c_int64 * 4), ("strides", ctypes.c_int64 * 4)]
+
+
+# tensor ids (enum hg_tensor_id)
+TENSOR_IDS = [
+    "ROOT_STATE", "DOF_POS", "DOF_VEL", "CONTACT_FORCES", "RIGID_STATE", "TORQUES", "ACTIONS",
+    "LAST_ACTIONS", "LAST_LAST_ACTIONS", "LAST_DOF_VEL", "LAST_ROOT_VEL", "COMMANDS", "OBS_BUF",
+    "PRIV_BUF", "REW_BUF", "RESET_BUF", "TIME_OUT_BUF", "EPISODE_LENGTH", "EPISODE_SUMS",
+    "FEET_AIR_TIME", "LAST_CONTACTS", "FEET_HEIGHT", "LAST_FEET_Z", "ENV_FRICTION", "BODY_MASS",
+    "PUSH_FORCE", "PUSH_TORQUE", "BASE_LIN_VEL", "BASE_ANG_VEL", "PROJ_GRAVITY", "BASE_EULER",
+    "REF_DOF_POS", "ENV_ORIGINS", "EP_STATS", "CONTACT_LAMBDA", "NONFINITE",
+]
+T = {name: i for i, name in enumerate(TENSOR_IDS)}
+
+# every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
+EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
+           "hg_post", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
+           "hg_gae_scan", "hg_gae_normalize", "hg_version"]
+
+_LIB = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libhgsim.so and declare signatures.  Raises if the HIP library is missing."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"hg_sim HIP library not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback on the product path)")
+    # torch first, so libamdhip64.so.7 resolves to the runtime torch already loaded (one HIP runtime)
+    import torch  # noqa: F401
+    L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.hg_arena_bytes.restype = sz
+    L.hg_arena_bytes.argtypes = [ctypes.POINTER(HgCfg)]
+    L.hg_create.restype = ctypes.c_int
+    L.hg_create.argtypes = [ctypes.POINTER(HgCfg), ctypes.POINTER(HgModel), vp, sz, ctypes.POINTER(vp)]
+    L.hg_destroy.restype = None
+    L.hg_destroy.argtypes = [vp]
+    L.hg_last_error.restype = ctypes.c_char_p
+    L.hg_last_error.argtypes = [vp]
+    L.hg_tensor.restype = ctypes.c_int
+    L.hg_tensor.argtypes = [vp, ctypes.c_int, ctypes.POINTER(HgDesc)]
+    L.hg_step.restype = ctypes.c_int
+    L.hg_step.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    L.hg_post.restype = ctypes.c_int
+    L.hg_post.argtypes = [vp, ctypes.c_uint64, vp]
+    L.hg_reset_masked.restype = ctypes.c_int
+    L.hg_reset_masked.argtypes = [vp, vp, ctypes.c_uint64, vp]
+    L.hg_set_dof_state_indexed.restype = ctypes.c_int
+    L.hg_set_dof_state_indexed.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp]
+    L.hg_set_root_state_indexed.restype = ctypes.c_int
+    L.hg_set_root_state_indexed.argtypes = [vp, vp, ctypes.c_int, vp, vp]
+    L.hg_gae_scan.restype = ctypes.c_int
+    L.hg_gae_scan.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                              ctypes.c_float, ctypes.c_int, vp]
+    L.hg_gae_normalize.restype = ctypes.c_int
+    L.hg_gae_normalize.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64, vp]
+    L.hg_version.restype = ctypes.c_char_p
+    L.hg_version.argtypes = []
+    return L
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = load_library()
+    return _LIB
+
+
+def check(status, handle=None):
+    if status != 0:
+        msg = lib().hg_last_error(handle)
+        raise RuntimeError(f"hg_sim error {status}: {msg.decode() if msg else '?'}")
+
+
+def stream_ptr(device):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# ------------------------------------------------------------------------------------------------
+# model table
+# ------------------------------------------------------------------------------------------------
+def load_model(path=MODEL_PATH, armature=0.01):
+    """Build an HgModel from model/xbotl_model.json (output of tools/urdf_compile.py).
+
+    armature: BUILD-DEFINED 0.01 kg m^2 per leg joint, from the robot's own MJCF
+    (resources/robots/XBot/mjcf/XBot-L.xml:37-39 `leg_joint_param armature=0.01`); the Isaac Gym
+    asset option is 0 (humanoid_config.py:114) — see DESIGN.md §Physics for why.
+    """
+    with open(path) as f:
+        js = json.load(f)
+    m = HgModel()
+    bodies = js["bodies"]
+    m.num_bodies = len(bodies)
+    m.num_dof = len(bodies) - 1
+    for b, bd in enumerate(bodies):
+        m.parent[b] = bd["parent"]
+        m.mass[b] = bd["mass"]
+        for i in range(3):
+            m.com[b][i] = bd["com"][i]
+        for i in range(6):
+            m.inertia[b][i] = bd["inertia"][i]
+        if b > 0:
+            j = bd["joint"]
+            for i in range(3):
+                m.joint_pos[b][i] = j["origin_pos"][i]
+                m.axis[b][i] = j["axis"][i]
+            R = np.array(j["origin_rot"]).reshape(9)
+            for i in range(9):
+                m.joint_rot[b][i] = R[i]
+            m.lower[b] = j["lower"]
+            m.upper[b] = j["upper"]
+            m.armature[b] = armature
+        else:
+            for i in range(9):
+                m.joint_rot[b][i] = 1.0 if i in (0, 4, 8) else 0.0
+    cs = js["contacts"]
+    m.num_contacts = len(cs)
+    m.num_foot_contacts = sum(1 for c in cs if c["body"] != 0)
+    for c, cd in enumerate(cs):
+        m.contact_body[c] = cd["body"]
+        for i in range(3):
+            m.contact_pos[c][i] = cd["pos"][i]
+    return m, js
+
+
+def model_names(js):
+    bodies = [b["name"] for b in js["bodies"]]
+    dofs = [b["joint"]["name"] for b in js["bodies"][1:]]
+    effort = [b["joint"]["effort"] for b in js["bodies"][1:]]
+    limits = [(b["joint"]["lower"], b["joint"]["upper"]) for b in js["bodies"][1:]]
+    velocity = [b["joint"]["velocity"] for b in js["bodies"][1:]]
+    return bodies, dofs, effort, limits, velocity

@@ -1,0 +1,209 @@
+"""OnPolicyRunner (humanoid/algo/ppo/on_policy_runner.py:45-322): same constructor, learn() loop
+order (T x [act -> env.step -> process_env_step], compute_returns, update), fps formula
+(Perf/total_fps = T * num_envs / (collection + learn)), scalar names and checkpoint dict.
+
+Logging backends: TensorBoard's SummaryWriter when importable, otherwise a JSONL scalar writer
+(wandb and tensorboard are absent in this image).  Book-keeping reads per-episode stats from
+device tensors; the only host syncs per step are the ones the reference also has when log_dir is
+set (done-id extraction), so with log_dir=None the rollout is sync-free.
+With world_size > 1 (one process per GPU) every rank runs its env shard; rank 0 logs/saves.
+"""
+import json
+import os
+import statistics
+import time
+from collections import deque
+from datetime import datetime
+
+import torch
+import torch.distributed as dist
+
+from .actor_critic import ActorCritic
+from .ppo import PPO
+
+
+class _JsonlWriter:
+    def __init__(self, log_dir):
+        os.makedirs(log_dir, exist_ok=True)
+        self._f = open(os.path.join(log_dir, "scalars.jsonl"), "a")
+
+    def add_scalar(self, tag, value, step):
+        self._f.write(json.dumps({"tag": tag, "value": float(value), "step": float(step)}) + "\n")
+        self._f.flush()
+
+    def close(self):
+        self._f.close()
+
+
+def _make_writer(log_dir):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(log_dir=log_dir, flush_secs=10)
+    except Exception:
+        return _JsonlWriter(log_dir)
+
+
+def _rank():
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+class OnPolicyRunner:
+    def __init__(self, env, train_cfg, log_dir=None, device="cpu"):
+        self.cfg = train_cfg["runner"]
+        self.alg_cfg = train_cfg["algorithm"]
+        self.policy_cfg = train_cfg["policy"]
+        self.all_cfg = train_cfg
+        self.wandb_run_name = (datetime.now().strftime("%b%d_%H-%M-%S") + "_" + train_cfg["runner"]["experiment_name"]
+                               + "_" + train_cfg["runner"]["run_name"])
+        self.device = device
+        self.env = env
+        num_critic_obs = env.num_privileged_obs if env.num_privileged_obs is not None else env.num_obs
+        policy_cls = {"ActorCritic": ActorCritic}[self.cfg["policy_class_name"]]
+        actor_critic = policy_cls(env.num_obs, num_critic_obs, env.num_actions, **self.policy_cfg).to(self.device)
+        alg_cls = {"PPO": PPO}[self.cfg["algorithm_class_name"]]
+        self.alg = alg_cls(actor_critic, device=self.device, **self.alg_cfg)
+        self.num_steps_per_env = self.cfg["num_steps_per_env"]
+        self.save_interval = self.cfg["save_interval"]
+        self.alg.init_storage(env.num_envs, self.num_steps_per_env, [env.num_obs], [env.num_privileged_obs],
+                              [env.num_actions])
+        self.log_dir = log_dir if _rank() == 0 else None
+        self.writer = None
+        self.tot_timesteps = 0
+        self.tot_time = 0
+        self.current_learning_iteration = 0
+        self.last_iteration_stats = {}
+        _, _ = self.env.reset()
+
+    def learn(self, num_learning_iterations, init_at_random_ep_len=False):
+        if self.log_dir is not None and self.writer is None:
+            self.writer = _make_writer(self.log_dir)
+        if init_at_random_ep_len:
+            self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
+                                                             high=int(self.env.max_episode_length))
+        obs = self.env.get_observations()
+        privileged_obs = self.env.get_privileged_observations()
+        critic_obs = privileged_obs if privileged_obs is not None else obs
+        obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
+        self.alg.actor_critic.train()
+        ep_infos = []
+        rewbuffer = deque(maxlen=100)
+        lenbuffer = deque(maxlen=100)
+        cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        tot_iter = self.current_learning_iteration + num_learning_iterations
+        for it in range(self.current_learning_iteration, tot_iter):
+            start = time.time()
+            with torch.inference_mode():
+                for _ in range(self.num_steps_per_env):
+                    actions = self.alg.act(obs, critic_obs)
+                    obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
+                    critic_obs = privileged_obs if privileged_obs is not None else obs
+                    obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
+                    rewards, dones = rewards.to(self.device), dones.to(self.device)
+                    self.alg.process_env_step(rewards, dones, infos)
+                    if self.log_dir is not None:
+                        if "episode" in infos:
+                            ep_infos.append(infos["episode"])
+                        cur_reward_sum += rewards
+                        cur_episode_length += 1
+                        new_ids = (dones > 0).nonzero(as_tuple=False)
+                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
+                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
+                        cur_reward_sum[new_ids] = 0
+                        cur_episode_length[new_ids] = 0
+                if self.device != "cpu" and torch.device(self.device).type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                stop = time.time()
+                collection_time = stop - start
+                self.env.course_gain *= self.env.course_ratio
+                self.env.course_gain = min(20, self.env.course_gain)
+                course_gain = self.env.course_gain
+                start = stop
+                self.alg.compute_returns(critic_obs)
+            mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss = self.alg.update()
+            stop = time.time()
+            learn_time = stop - start
+            self.last_iteration_stats = dict(collection_time=collection_time, learn_time=learn_time,
+                                             value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
+                                             lin_vel_loss=mean_base_lin_vel_loss)
+            if self.log_dir is not None:
+                self.log(locals())
+                if it % self.save_interval == 0:
+                    self.save(os.path.join(self.log_dir, "model_{}.pt".format(it)))
+            ep_infos.clear()
+        self.current_learning_iteration += num_learning_iterations
+        if self.log_dir is not None:
+            self.save(os.path.join(self.log_dir, "model_{}.pt".format(self.current_learning_iteration)))
+
+    def log(self, locs, width=90, pad=45):
+        self.tot_timesteps += self.num_steps_per_env * self.env.num_envs
+        iteration_time = locs["collection_time"] + locs["learn_time"]
+        self.tot_time += iteration_time
+        it = locs["it"]
+        ep_string = ""
+        if locs["ep_infos"]:
+            for key in locs["ep_infos"][0]:
+                vals = torch.stack([torch.as_tensor(ep[key], device=self.device, dtype=torch.float).reshape(-1)[0]
+                                    for ep in locs["ep_infos"]])
+                value = vals.mean()
+                self.writer.add_scalar("Episode/" + key, value, it)
+                ep_string += f"""{f'Mean episode {key}:':>{pad}} {value:.4f}\n"""
+        mean_std = self.alg.actor_critic.std.mean()
+        fps = int(self.num_steps_per_env * self.env.num_envs / iteration_time)
+        w = self.writer
+        w.add_scalar("Loss/value_function", locs["mean_value_loss"], it)
+        w.add_scalar("Loss/surrogate", locs["mean_surrogate_loss"], it)
+        w.add_scalar("Loss/sym_loss", locs["sym_loss"], it)
+        w.add_scalar("Train/course_gain", locs["course_gain"], it)
+        w.add_scalar("Loss/mean_base_lin_vel_loss", locs["mean_base_lin_vel_loss"], it)
+        w.add_scalar("Loss/learning_rate", self.alg.learning_rate, it)
+        w.add_scalar("Policy/mean_noise_std", mean_std.item(), it)
+        w.add_scalar("Perf/total_fps", fps, it)
+        w.add_scalar("Perf/collection time", locs["collection_time"], it)
+        w.add_scalar("Perf/learning_time", locs["learn_time"], it)
+        if len(locs["rewbuffer"]) > 0:
+            w.add_scalar("Train/mean_reward", statistics.mean(locs["rewbuffer"]), it)
+            w.add_scalar("Train/mean_episode_length", statistics.mean(locs["lenbuffer"]), it)
+            w.add_scalar("Train/mean_reward/time", statistics.mean(locs["rewbuffer"]), self.tot_time)
+            w.add_scalar("Train/mean_episode_length/time", statistics.mean(locs["lenbuffer"]), self.tot_time)
+        title = f" \033[1m Learning iteration {it}/{self.current_learning_iteration + locs['num_learning_iterations']} \033[0m "
+        s = (f"""{'#' * width}\n{title.center(width, ' ')}\n\n"""
+             f"""{'Computation:':>{pad}} {fps:.0f} steps/s (collection: {locs['collection_time']:.3f}s, learning {locs['learn_time']:.3f}s)\n"""
+             f"""{'Value function loss:':>{pad}} {locs['mean_value_loss']:.4f}\n"""
+             f"""{'Surrogate loss:':>{pad}} {locs['mean_surrogate_loss']:.4f}\n"""
+             f"""{'Base vel loss:':>{pad}} {locs['mean_base_lin_vel_loss']:.4f}\n"""
+             f"""{'Mean action noise std:':>{pad}} {mean_std.item():.2f}\n""")
+        if len(locs["rewbuffer"]) > 0:
+            s += (f"""{'Mean reward:':>{pad}} {statistics.mean(locs['rewbuffer']):.2f}\n"""
+                  f"""{'Mean episode length:':>{pad}} {statistics.mean(locs['lenbuffer']):.2f}\n""")
+        s += ep_string
+        s += (f"""{'-' * width}\n{'Total timesteps:':>{pad}} {self.tot_timesteps}\n"""
+              f"""{'Iteration time:':>{pad}} {iteration_time:.2f}s\n{'Total time:':>{pad}} {self.tot_time:.2f}s\n"""
+              f"""{'ETA:':>{pad}} {self.tot_time / (it + 1) * (locs['num_learning_iterations'] - it):.1f}s\n""")
+        print(s)
+
+    def save(self, path, infos=None):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        torch.save({"model_state_dict": self.alg.actor_critic.state_dict(),
+                    "optimizer_state_dict": self.alg.optimizer.state_dict(),
+                    "iter": self.current_learning_iteration, "infos": infos}, path)
+
+    def load(self, path, load_optimizer=True):
+        d = torch.load(path, map_location=self.device, weights_only=True)
+        self.alg.actor_critic.load_state_dict(d["model_state_dict"])
+        if load_optimizer:
+            self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
+        self.current_learning_iteration = d["iter"]
+        return d["infos"]
+
+    def get_inference_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_inference
+
+    def get_inference_critic(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.evaluate

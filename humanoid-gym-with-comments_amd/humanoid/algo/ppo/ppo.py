@@ -1,0 +1,192 @@
+"""PPO (constructor kwargs, act/process_env_step/compute_returns/update and the 4-tuple return of
+humanoid/algo/ppo/ppo.py:44-226).
+
+Update math (per minibatch, in the reference's order): adaptive-KL learning rate, clipped
+surrogate, clipped value loss, lin-vel MSE, entropy bonus, Adam step after global-norm clipping.
+
+Data parallel (new): when torch.distributed is initialised with world_size > 1
+(backend "nccl" = RCCL on ROCm), parameters are broadcast from rank 0 once, each rank's gradients
+live in ONE flat buffer that is all-reduced (SUM / world) before clip_grad_norm_, and kl_mean is
+all-reduced so the adaptive learning rate stays identical on every rank.  With world_size 1 the
+path is the reference's.
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+import torch.optim as optim
+
+from .actor_critic import ActorCritic
+from .rollout_storage import RolloutStorage
+
+
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
+class PPO:
+    actor_critic: ActorCritic
+
+    def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998,
+                 lam=0.95, value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
+                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu", sym_loss=False,
+                 obs_permutation=None, act_permutation=None, frame_stack=0, sym_coef=1.0, base_lin_vel_coef=1.0):
+        self.device = device
+        self.desired_kl = desired_kl
+        self.schedule = schedule
+        self.learning_rate = learning_rate
+        self.actor_critic = actor_critic
+        self.actor_critic.to(self.device)
+        self.storage = None
+        self.world_size = _world()
+        self._params = list(self.actor_critic.parameters())
+        if self.world_size > 1:
+            with torch.no_grad():
+                for p in self._params:
+                    dist.broadcast(p.data, src=0)
+            # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack copies
+            numel = sum(p.numel() for p in self._params)
+            self._flat_grad = torch.zeros(numel, device=self._params[0].device, dtype=torch.float32)
+            off = 0
+            for p in self._params:
+                p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
+                off += p.numel()
+        self.optimizer = optim.Adam(self._params, lr=learning_rate)
+        self.transition = RolloutStorage.Transition()
+        self.clip_param = clip_param
+        self.num_learning_epochs = num_learning_epochs
+        self.num_mini_batches = num_mini_batches
+        self.value_loss_coef = value_loss_coef
+        self.entropy_coef = entropy_coef
+        self.gamma = gamma
+        self.lam = lam
+        self.max_grad_norm = max_grad_norm
+        self.use_clipped_value_loss = use_clipped_value_loss
+        self.base_lin_vel_coef = base_lin_vel_coef
+        self.sym_loss = sym_loss
+        self.sym_coef = sym_coef
+        if self.sym_loss:
+            # mirror matrices built on the policy's device (the reference hard-codes .cuda(), ppo.py:96,103)
+            n_act = len(act_permutation)
+            self.act_perm_mat = torch.zeros(n_act, n_act, device=device)
+            for i, perm in enumerate(act_permutation):
+                self.act_perm_mat[int(abs(perm))][i] = float(torch.sign(torch.tensor(perm)))
+            stack = []
+            for i in range(frame_stack):
+                for p in obs_permutation:
+                    s = 1.0 if p >= 0 else -1.0
+                    stack.append(s * (abs(p) + i * len(obs_permutation)))
+            self.obs_perm_mat = torch.zeros(len(stack), len(stack), device=device)
+            for i, perm in enumerate(stack):
+                self.obs_perm_mat[int(abs(perm))][i] = 1.0 if perm >= 0 else -1.0
+
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
+        self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
+                                      action_shape, self.device)
+
+    def test_mode(self):
+        self.actor_critic.eval()
+
+    def train_mode(self):
+        self.actor_critic.train()
+
+    def act(self, obs, critic_obs):
+        t = self.transition
+        t.actions = self.actor_critic.act(obs)[0].detach()
+        t.values = self.actor_critic.evaluate(critic_obs).detach()
+        t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
+        t.action_mean = self.actor_critic.action_mean.detach()
+        t.action_sigma = self.actor_critic.action_std.detach()
+        t.observations = obs
+        t.critic_observations = critic_obs
+        return t.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        t = self.transition
+        t.rewards = rewards.clone()
+        t.dones = dones
+        if "time_outs" in infos:  # bootstrap on time-outs (ppo.py:132-133)
+            t.rewards += self.gamma * torch.squeeze(t.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        self.storage.add_transitions(t)
+        self.transition.clear()
+        self.actor_critic.reset(dones)
+
+    def compute_returns(self, last_critic_obs):
+        last_values = self.actor_critic.evaluate(last_critic_obs).detach()
+        self.storage.compute_returns(last_values, self.gamma, self.lam)
+
+    def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
+        with torch.inference_mode():
+            kl = torch.sum(torch.log(sigma / old_sigma + 1.0e-5)
+                           + (torch.square(old_sigma) + torch.square(old_mu - mu)) / (2.0 * torch.square(sigma))
+                           - 0.5, axis=-1)
+            kl_mean = torch.mean(kl)
+            if self.world_size > 1:
+                dist.all_reduce(kl_mean)
+                kl_mean /= self.world_size
+            kl_mean = kl_mean.item()
+        if kl_mean > self.desired_kl * 2.0:
+            self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+        elif kl_mean < self.desired_kl / 2.0 and kl_mean > 0.0:
+            self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+        for g in self.optimizer.param_groups:
+            g["lr"] = self.learning_rate
+
+    def update(self):
+        mean_value_loss = 0.0
+        mean_surrogate_loss = 0.0
+        mean_base_lin_vel_loss = 0.0
+        sym_loss = 0
+        ac = self.actor_critic
+        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        for (obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
+             old_sigma_b, hid_b, masks_b) in gen:
+            _, est_lin_vel = ac.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
+            logp_b = ac.get_actions_log_prob(actions_b)
+            value_b = ac.evaluate(critic_b, masks=masks_b, hidden_states=hid_b[1])
+            mu_b = ac.action_mean
+            sigma_b = ac.action_std
+            entropy_b = ac.entropy
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                self._adapt_lr(mu_b, sigma_b, old_mu_b, old_sigma_b)
+            # clipped surrogate
+            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+            adv = torch.squeeze(adv_b)
+            surrogate = -adv * ratio
+            surrogate_clipped = -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
+            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+            # value loss
+            if self.use_clipped_value_loss:
+                value_clipped = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
+                value_losses = (value_b - returns_b).pow(2)
+                value_losses_clipped = (value_clipped - returns_b).pow(2)
+                value_loss = torch.max(value_losses, value_losses_clipped).mean()
+            else:
+                value_loss = (returns_b - value_b).pow(2).mean()
+            if self.sym_loss:
+                mirror_act = ac.actor(torch.matmul(obs_b, self.obs_perm_mat))
+                sym_loss = (mu_b - torch.matmul(mirror_act, self.act_perm_mat)).pow(2).mean()
+            base_lin_vel_loss = F.mse_loss(est_lin_vel, lin_vel_b)
+            loss = (surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean()
+                    + self.sym_coef * sym_loss + self.base_lin_vel_coef * base_lin_vel_loss)
+            if self.world_size > 1:
+                self._flat_grad.zero_()
+                loss.backward()
+                dist.all_reduce(self._flat_grad)
+                self._flat_grad /= self.world_size
+            else:
+                self.optimizer.zero_grad()
+                loss.backward()
+            nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
+            self.optimizer.step()
+            mean_value_loss += value_loss.item()
+            mean_surrogate_loss += surrogate_loss.item()
+            mean_base_lin_vel_loss += base_lin_vel_loss.item()
+        num_updates = self.num_learning_epochs * self.num_mini_batches
+        mean_value_loss /= num_updates
+        mean_surrogate_loss /= num_updates
+        mean_base_lin_vel_loss /= num_updates
+        self.storage.clear()
+        return mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss

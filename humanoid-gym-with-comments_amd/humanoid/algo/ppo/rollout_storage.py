@@ -1,0 +1,136 @@
+"""RolloutStorage (API of humanoid/algo/ppo/rollout_storage.py:35-191).
+
+Buffers are [T, N, ...] device tensors as in the reference.  compute_returns runs the fused HIP
+GAE kernel (csrc/hg_gae.hip) — reverse-time scan + fp64 statistics + normalisation in two
+launches instead of T eager steps — and, when a torch.distributed group of size > 1 is active,
+all-reduces the (sum A, sum A^2) statistics between the two passes so advantages are normalised
+with global statistics (collective (3)).
+
+There is no CPU path: GAE needs the HIP kernel (tensors on a ROCm device).  Test code may set
+``storage.gae_fn`` to an oracle explicitly.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+
+class RolloutStorage:
+    class Transition:
+        def __init__(self):
+            self.observations = None
+            self.critic_observations = None
+            self.actions = None
+            self.rewards = None
+            self.dones = None
+            self.values = None
+            self.actions_log_prob = None
+            self.action_mean = None
+            self.action_sigma = None
+            self.hidden_states = None
+
+        def clear(self):
+            self.__init__()
+
+    def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, actions_shape,
+                 device="cpu"):
+        self.device = device
+        self.obs_shape = obs_shape
+        self.privileged_obs_shape = privileged_obs_shape
+        self.actions_shape = actions_shape
+        T, N = num_transitions_per_env, num_envs
+
+        def z(*shape, dtype=torch.float32):
+            return torch.zeros(T, N, *shape, device=device, dtype=dtype)
+
+        self.observations = z(*obs_shape)
+        self.privileged_observations = z(*privileged_obs_shape) if privileged_obs_shape[0] is not None else None
+        self.rewards = z(1)
+        self.actions = z(*actions_shape)
+        self.dones = z(1, dtype=torch.uint8)
+        self.actions_log_prob = z(1)
+        self.values = z(1)
+        self.returns = z(1)
+        self.advantages = z(1)
+        self.mu = z(*actions_shape)
+        self.sigma = z(*actions_shape)
+        self.num_transitions_per_env = T
+        self.num_envs = N
+        self.saved_hidden_states_a = None
+        self.saved_hidden_states_c = None
+        self.step = 0
+        self.gae_fn = None  # optional override (tests); default: HIP kernel
+        self._stats = torch.zeros(2, dtype=torch.float64, device=device)
+
+    def add_transitions(self, transition: Transition):
+        if self.step >= self.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        t = self.step
+        self.observations[t].copy_(transition.observations)
+        if self.privileged_observations is not None:
+            self.privileged_observations[t].copy_(transition.critic_observations)
+        self.actions[t].copy_(transition.actions)
+        self.rewards[t].copy_(transition.rewards.view(-1, 1))
+        self.dones[t].copy_(transition.dones.view(-1, 1))
+        self.values[t].copy_(transition.values)
+        self.actions_log_prob[t].copy_(transition.actions_log_prob.view(-1, 1))
+        self.mu[t].copy_(transition.action_mean)
+        self.sigma[t].copy_(transition.action_sigma)
+        self.step += 1
+
+    def clear(self):
+        self.step = 0
+
+    def compute_returns(self, last_values, gamma, lam):
+        """GAE(gamma, lam) + advantage normalisation (rollout_storage.py:122-143)."""
+        if self.gae_fn is not None:
+            self.returns, self.advantages = self.gae_fn(self.rewards, self.dones, self.values, last_values, gamma, lam)
+            return
+        if self.rewards.device.type != "cuda":
+            raise RuntimeError("RolloutStorage.compute_returns needs the HIP GAE kernel: storage must live on a "
+                               "ROCm device (no CPU fallback)")
+        from humanoid import _native as N
+        L = N.lib()
+        lv = last_values.detach().reshape(-1).contiguous().float()
+        T, Nn = self.num_transitions_per_env, self.num_envs
+        s = ctypes.c_void_p(torch.cuda.current_stream(self.rewards.device).cuda_stream)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        N.check(L.hg_gae_scan(p(self.rewards), p(self.dones), p(self.values), p(lv), p(self.returns),
+                              p(self.advantages), p(self._stats), T, Nn, ctypes.c_float(gamma), ctypes.c_float(lam), 1, s))
+        count = T * Nn
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self._stats)
+            count *= dist.get_world_size()
+        N.check(L.hg_gae_normalize(p(self.advantages), p(self._stats), ctypes.c_int64(count),
+                                   ctypes.c_int64(T * Nn), s))
+
+    def get_statistics(self):
+        done = self.dones
+        done[-1] = 1
+        flat_dones = done.permute(1, 0, 2).reshape(-1, 1)
+        done_indices = torch.cat((flat_dones.new_tensor([-1], dtype=torch.int64),
+                                  flat_dones.nonzero(as_tuple=False)[:, 0]))
+        trajectory_lengths = done_indices[1:] - done_indices[:-1]
+        return trajectory_lengths.float().mean(), self.rewards.mean()
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        """One randperm for all epochs; 12-tuple per minibatch (rollout_storage.py:153-191).
+        The lin-vel target is critic_obs[:, 53:56] (base_lin_vel * 2 of the oldest critic frame)."""
+        batch_size = self.num_envs * self.num_transitions_per_env
+        mb = batch_size // num_mini_batches
+        indices = torch.randperm(num_mini_batches * mb, requires_grad=False, device=self.device)
+        obs = self.observations.flatten(0, 1)
+        critic = self.privileged_observations.flatten(0, 1) if self.privileged_observations is not None else obs
+        lin_vel = critic[:, 53:56]
+        actions = self.actions.flatten(0, 1)
+        values = self.values.flatten(0, 1)
+        returns = self.returns.flatten(0, 1)
+        old_logp = self.actions_log_prob.flatten(0, 1)
+        adv = self.advantages.flatten(0, 1)
+        old_mu = self.mu.flatten(0, 1)
+        old_sigma = self.sigma.flatten(0, 1)
+        for _ in range(num_epochs):
+            for i in range(num_mini_batches):
+                idx = indices[i * mb:(i + 1) * mb]
+                yield (obs[idx], critic[idx], lin_vel[idx], actions[idx], values[idx], adv[idx], returns[idx],
+                       old_logp[idx], old_mu[idx], old_sigma[idx], (None, None), None)

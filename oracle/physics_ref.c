@@ -1,0 +1,577 @@
+/*
+ * physics_ref.c — CPU reference simulator for the XBot-L articulation.
+ *
+ * TEST INFRASTRUCTURE ONLY (the "oracle").  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library.  The product path (humanoid-gym-with-comments_amd/csrc)
+ * never links or calls it.
+ *
+ * What it restates.  The reference's physics is Isaac Gym Preview 4 / PhysX (gym.simulate,
+ * humanoid/envs/custom/humanoid_env.py:639-649), a closed third-party binary that is absent from
+ * /root/reference and not installable offline: physics parity against the reference is UNPINNED
+ * (SURVEY.md §8c).  This file is the build's documented algorithm, written
+ * as plainly as possible — dense matrices, serial loops — so the optimised HIP kernel can be
+ * checked against it, and pinned by analytic known-answer tests (free fall, pendulum energy,
+ * static standing support, momentum conservation) in tests/test_physics_oracle.py.
+ *
+ * Pieces that DO follow reference code line by line:
+ *   - PD torques: humanoid_env.py:910-925 (_compute_torques), applied every substep (:639-645)
+ *   - parameters: humanoid_config.py:273-315 (dt, gravity, contact offset, depenetration)
+ *
+ * Algorithm per substep (dt = sim.dt), generalized velocity nu = [v_base(3) w_base(3) qd(12)],
+ * all vectors in a world-aligned frame centred on the base origin:
+ *   1. forward kinematics, 2. bias forces h (RNEA, gravity as base acceleration),
+ *   3. joint-space inertia M (composite-rigid-body, + armature), 4. Cholesky M = L L^T,
+ *   5. nu* = nu + dt M^-1 (tau - h),
+ *   6. contacts (sole corners + base box corners vs plane/heightfield, speculative within
+ *      contact_offset) and joint limits as unilateral velocity constraints, solved by projected
+ *      Gauss-Seidel on impulses with Y = M^-1 J^T (warm-started from the previous substep),
+ *      friction cone |lambda_t| <= mu lambda_n, mu = mean(env friction, ground friction)
+ *      (PhysX average combine mode),
+ *   7. semi-implicit Euler: q += dt qd, p += dt v, quaternion by exact exponential map.
+ *
+ * Precision: `real` is double by default; -DREF_FLOAT builds an fp32 variant (used to size the
+ * fp32 parity tolerance: |gpu - ref64| <= k |ref32 - ref64| + eps).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/hgsim.h"
+
+#ifdef REF_FLOAT
+typedef float real;
+#define R(x) ((float)(x))
+#else
+typedef double real;
+#define R(x) ((double)(x))
+#endif
+
+#define NB 13
+#define ND 12
+#define NV 18
+#define NC_MAX HG_MAX_CONTACTS
+#define LAMW (NC_MAX * 3 + ND)
+
+typedef struct {
+  int nb, nc, nfoot;
+  int parent[NB];
+  int cbody[NC_MAX];
+  real jpos[NB][3], jrot[NB][9], axis[NB][3];
+  real mass[NB], com[NB][3], inertia[NB][6], armature[NB], lower[NB], upper[NB];
+  real cpos[NC_MAX][3];
+} Model;
+
+/* ---------------------------------------------------------------- small vector algebra */
+static inline void v3_cross(const real* a, const real* b, real* o) {
+  real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+static inline real v3_dot(const real* a, const real* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void mat3_vec(const real* Rm, const real* v, real* o) {
+  real x = Rm[0] * v[0] + Rm[1] * v[1] + Rm[2] * v[2];
+  real y = Rm[3] * v[0] + Rm[4] * v[1] + Rm[5] * v[2];
+  real z = Rm[6] * v[0] + Rm[7] * v[1] + Rm[8] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+static inline void mat3_mul(const real* A, const real* B, real* C) {
+  real T[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) T[i * 3 + j] = A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+  memcpy(C, T, sizeof(T));
+}
+/* symmetric 3x3 stored as xx yy zz xy xz yz */
+static inline void sym_vec(const real* S, const real* v, real* o) {
+  real x = S[0] * v[0] + S[3] * v[1] + S[4] * v[2];
+  real y = S[3] * v[0] + S[1] * v[1] + S[5] * v[2];
+  real z = S[4] * v[0] + S[5] * v[1] + S[2] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+/* world inertia R I R^T for symmetric I */
+static void rot_sym(const real* Rm, const real* I, real* o) {
+  real Im[9] = {I[0], I[3], I[4], I[3], I[1], I[5], I[4], I[5], I[2]};
+  real T[9], W[9];
+  mat3_mul(Rm, Im, T);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) W[i * 3 + j] = T[i * 3] * Rm[j * 3] + T[i * 3 + 1] * Rm[j * 3 + 1] + T[i * 3 + 2] * Rm[j * 3 + 2];
+  o[0] = W[0]; o[1] = W[4]; o[2] = W[8]; o[3] = W[1]; o[4] = W[2]; o[5] = W[5];
+}
+static void quat_to_mat(const real* q, real* Rm) { /* xyzw */
+  real x = q[0], y = q[1], z = q[2], w = q[3];
+  Rm[0] = 1 - 2 * (y * y + z * z); Rm[1] = 2 * (x * y - z * w);     Rm[2] = 2 * (x * z + y * w);
+  Rm[3] = 2 * (x * y + z * w);     Rm[4] = 1 - 2 * (x * x + z * z); Rm[5] = 2 * (y * z - x * w);
+  Rm[6] = 2 * (x * z - y * w);     Rm[7] = 2 * (y * z + x * w);     Rm[8] = 1 - 2 * (x * x + y * y);
+}
+static void mat_to_quat(const real* m, real* q) { /* xyzw, Shepperd */
+  real tr = m[0] + m[4] + m[8];
+  if (tr > 0) {
+    real s = sqrt(tr + 1) * 2;
+    q[3] = R(0.25) * s; q[0] = (m[7] - m[5]) / s; q[1] = (m[2] - m[6]) / s; q[2] = (m[3] - m[1]) / s;
+  } else if (m[0] > m[4] && m[0] > m[8]) {
+    real s = sqrt(1 + m[0] - m[4] - m[8]) * 2;
+    q[3] = (m[7] - m[5]) / s; q[0] = R(0.25) * s; q[1] = (m[1] + m[3]) / s; q[2] = (m[2] + m[6]) / s;
+  } else if (m[4] > m[8]) {
+    real s = sqrt(1 + m[4] - m[0] - m[8]) * 2;
+    q[3] = (m[2] - m[6]) / s; q[0] = (m[1] + m[3]) / s; q[1] = R(0.25) * s; q[2] = (m[5] + m[7]) / s;
+  } else {
+    real s = sqrt(1 + m[8] - m[0] - m[4]) * 2;
+    q[3] = (m[3] - m[1]) / s; q[0] = (m[2] + m[6]) / s; q[1] = (m[5] + m[7]) / s; q[2] = R(0.25) * s;
+  }
+  if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+}
+/* rotation by angle about unit axis (Rodrigues) */
+static void axis_angle(const real* k, real th, real* Rm) {
+  real c = cos(th), s = sin(th), v = 1 - c;
+  Rm[0] = c + k[0] * k[0] * v;        Rm[1] = k[0] * k[1] * v - k[2] * s; Rm[2] = k[0] * k[2] * v + k[1] * s;
+  Rm[3] = k[1] * k[0] * v + k[2] * s; Rm[4] = c + k[1] * k[1] * v;        Rm[5] = k[1] * k[2] * v - k[0] * s;
+  Rm[6] = k[2] * k[0] * v - k[1] * s; Rm[7] = k[2] * k[1] * v + k[0] * s; Rm[8] = c + k[2] * k[2] * v;
+}
+
+static void load_model(const hg_model* hm, Model* m) {
+  m->nb = hm->num_bodies; m->nc = hm->num_contacts; m->nfoot = hm->num_foot_contacts;
+  for (int b = 0; b < NB; b++) {
+    m->parent[b] = hm->parent[b];
+    for (int i = 0; i < 3; i++) { m->jpos[b][i] = hm->joint_pos[b][i]; m->axis[b][i] = hm->axis[b][i]; m->com[b][i] = hm->com[b][i]; }
+    for (int i = 0; i < 9; i++) m->jrot[b][i] = hm->joint_rot[b][i];
+    for (int i = 0; i < 6; i++) m->inertia[b][i] = hm->inertia[b][i];
+    m->mass[b] = hm->mass[b]; m->armature[b] = hm->armature[b];
+    m->lower[b] = hm->lower[b]; m->upper[b] = hm->upper[b];
+  }
+  for (int c = 0; c < NC_MAX; c++) {
+    m->cbody[c] = hm->contact_body[c];
+    for (int i = 0; i < 3; i++) m->cpos[c][i] = hm->contact_pos[c][i];
+  }
+}
+
+/* ---------------------------------------------------------------- terrain */
+/* plane z = 0, or the triangulated heightfield (row index = x, column = y, origin at -border) */
+static void ground(const hg_cfg* cfg, const int16_t* hf, real x, real y, real* h, real* n) {
+  if (cfg->terrain_type == 0 || hf == NULL) { *h = 0; n[0] = 0; n[1] = 0; n[2] = 1; return; }
+  real hs = cfg->hf_horizontal_scale, vs = cfg->hf_vertical_scale;
+  real fx = (x + cfg->hf_border) / hs, fy = (y + cfg->hf_border) / hs;
+  int i = (int)floor(fx), j = (int)floor(fy);
+  if (i < 0) i = 0; if (j < 0) j = 0;
+  if (i > cfg->hf_rows - 2) i = cfg->hf_rows - 2; if (j > cfg->hf_cols - 2) j = cfg->hf_cols - 2;
+  real u = fx - i, v = fy - j;
+  if (u < 0) u = 0; if (u > 1) u = 1; if (v < 0) v = 0; if (v > 1) v = 1;
+  real h00 = vs * hf[i * cfg->hf_cols + j], h10 = vs * hf[(i + 1) * cfg->hf_cols + j];
+  real h01 = vs * hf[i * cfg->hf_cols + j + 1], h11 = vs * hf[(i + 1) * cfg->hf_cols + j + 1];
+  real dhdx, dhdy;
+  if (u + v <= 1) { *h = h00 + u * (h10 - h00) + v * (h01 - h00); dhdx = (h10 - h00) / hs; dhdy = (h01 - h00) / hs; }
+  else { *h = h11 + (1 - u) * (h01 - h11) + (1 - v) * (h10 - h11); dhdx = (h11 - h01) / hs; dhdy = (h11 - h10) / hs; }
+  real inv = 1 / sqrt(dhdx * dhdx + dhdy * dhdy + 1);
+  n[0] = -dhdx * inv; n[1] = -dhdy * inv; n[2] = inv;
+}
+
+/* ---------------------------------------------------------------- one substep */
+typedef struct {
+  real Rb[NB][9], o[NB][3], c[NB][3], a[NB][3], Iw[NB][6], m[NB];
+  real w[NB][3], v[NB][3];
+} Kin;
+
+static void kinematics(const Model* m, const real* quat, const real* q, const real* nu, real mass0,
+                       Kin* k) {
+  quat_to_mat(quat, k->Rb[0]);
+  k->o[0][0] = k->o[0][1] = k->o[0][2] = 0;
+  for (int i = 0; i < 3; i++) { k->v[0][i] = nu[i]; k->w[0][i] = nu[3 + i]; }
+  for (int b = 1; b < NB; b++) {
+    int p = m->parent[b];
+    real Rj[9], Rq[9], t[3];
+    mat3_mul(k->Rb[p], m->jrot[b], Rj);
+    axis_angle(m->axis[b], q[b - 1], Rq);
+    mat3_mul(Rj, Rq, k->Rb[b]);
+    mat3_vec(k->Rb[p], m->jpos[b], t);
+    for (int i = 0; i < 3; i++) k->o[b][i] = k->o[p][i] + t[i];
+    mat3_vec(Rj, m->axis[b], k->a[b]);
+    /* velocities */
+    real r[3], wxr[3];
+    for (int i = 0; i < 3; i++) r[i] = k->o[b][i] - k->o[p][i];
+    v3_cross(k->w[p], r, wxr);
+    real qd = nu[5 + b];
+    for (int i = 0; i < 3; i++) { k->v[b][i] = k->v[p][i] + wxr[i]; k->w[b][i] = k->w[p][i] + k->a[b][i] * qd; }
+  }
+  real scale0 = mass0 / m->mass[0];
+  for (int b = 0; b < NB; b++) {
+    real t[3];
+    mat3_vec(k->Rb[b], m->com[b], t);
+    for (int i = 0; i < 3; i++) k->c[b][i] = k->o[b][i] + t[i];
+    rot_sym(k->Rb[b], m->inertia[b], k->Iw[b]);
+    k->m[b] = m->mass[b];
+    if (b == 0) { k->m[0] = mass0; for (int i = 0; i < 6; i++) k->Iw[0][i] *= scale0; }
+  }
+}
+
+/* bias forces h(q, nu) incl. gravity (RNEA with nu_dot = 0, base acceleration = -g) */
+static void bias_forces(const Model* m, const Kin* k, const real* nu, real gz, real* h) {
+  real alpha[NB][3], acc[NB][3], f[NB][3], n[NB][3];
+  for (int i = 0; i < 3; i++) { alpha[0][i] = 0; acc[0][i] = 0; }
+  acc[0][2] = -gz;
+  for (int b = 1; b < NB; b++) {
+    int p = m->parent[b];
+    real r[3], t1[3], t2[3], wqd[3];
+    real qd = nu[5 + b];
+    for (int i = 0; i < 3; i++) { r[i] = k->o[b][i] - k->o[p][i]; wqd[i] = k->a[b][i] * qd; }
+    v3_cross(k->w[p], wqd, t1);
+    for (int i = 0; i < 3; i++) alpha[b][i] = alpha[p][i] + t1[i];
+    v3_cross(alpha[p], r, t1);
+    v3_cross(k->w[p], r, t2);
+    v3_cross(k->w[p], t2, t2);
+    for (int i = 0; i < 3; i++) acc[b][i] = acc[p][i] + t1[i] + t2[i];
+  }
+  for (int b = 0; b < NB; b++) {
+    real d[3], t1[3], t2[3], ac[3], Iw_w[3], Ia[3];
+    for (int i = 0; i < 3; i++) d[i] = k->c[b][i] - k->o[b][i];
+    v3_cross(alpha[b], d, t1);
+    v3_cross(k->w[b], d, t2);
+    v3_cross(k->w[b], t2, t2);
+    for (int i = 0; i < 3; i++) ac[i] = acc[b][i] + t1[i] + t2[i];
+    sym_vec(k->Iw[b], k->w[b], Iw_w);
+    sym_vec(k->Iw[b], alpha[b], Ia);
+    v3_cross(k->w[b], Iw_w, t1);
+    for (int i = 0; i < 3; i++) { f[b][i] = k->m[b] * ac[i]; n[b][i] = Ia[i] + t1[i]; }
+    v3_cross(d, f[b], t2);
+    for (int i = 0; i < 3; i++) n[b][i] += t2[i];
+  }
+  for (int b = NB - 1; b >= 1; b--) {
+    int p = m->parent[b];
+    h[5 + b] = v3_dot(k->a[b], n[b]);
+    real r[3], t[3];
+    for (int i = 0; i < 3; i++) r[i] = k->o[b][i] - k->o[p][i];
+    v3_cross(r, f[b], t);
+    for (int i = 0; i < 3; i++) { f[p][i] += f[b][i]; n[p][i] += n[b][i] + t[i]; }
+  }
+  for (int i = 0; i < 3; i++) { h[i] = f[0][i]; h[3 + i] = n[0][i]; }
+}
+
+/* joint-space inertia by composite rigid bodies */
+static void mass_matrix(const Model* m, const Kin* k, real M[NV][NV]) {
+  real cm[NB], cs[NB][3], cJ[NB][6];
+  for (int b = 0; b < NB; b++) {
+    const real* c = k->c[b];
+    real mb = k->m[b], cc = v3_dot(c, c);
+    cm[b] = mb;
+    for (int i = 0; i < 3; i++) cs[b][i] = mb * c[i];
+    cJ[b][0] = k->Iw[b][0] + mb * (cc - c[0] * c[0]);
+    cJ[b][1] = k->Iw[b][1] + mb * (cc - c[1] * c[1]);
+    cJ[b][2] = k->Iw[b][2] + mb * (cc - c[2] * c[2]);
+    cJ[b][3] = k->Iw[b][3] - mb * c[0] * c[1];
+    cJ[b][4] = k->Iw[b][4] - mb * c[0] * c[2];
+    cJ[b][5] = k->Iw[b][5] - mb * c[1] * c[2];
+  }
+  for (int b = NB - 1; b >= 1; b--) {
+    int p = m->parent[b];
+    cm[p] += cm[b];
+    for (int i = 0; i < 3; i++) cs[p][i] += cs[b][i];
+    for (int i = 0; i < 6; i++) cJ[p][i] += cJ[b][i];
+  }
+  memset(M, 0, sizeof(real) * NV * NV);
+  /* base block */
+  const real* s = cs[0];
+  for (int i = 0; i < 3; i++) M[i][i] = cm[0];
+  real S[3][3] = {{0, -s[2], s[1]}, {s[2], 0, -s[0]}, {-s[1], s[0], 0}};
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) { M[3 + i][j] = S[i][j]; M[j][3 + i] = S[i][j]; }
+  real Jm[3][3] = {{cJ[0][0], cJ[0][3], cJ[0][4]}, {cJ[0][3], cJ[0][1], cJ[0][5]}, {cJ[0][4], cJ[0][5], cJ[0][2]}};
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) M[3 + i][3 + j] = Jm[i][j];
+  /* joint columns */
+  for (int b = 1; b < NB; b++) {
+    int col = 5 + b;
+    const real* a = k->a[b];
+    const real* o = k->o[b];
+    real sm[3], F[3], L[3], axo[3], t[3];
+    for (int i = 0; i < 3; i++) sm[i] = cs[b][i] - cm[b] * o[i];
+    v3_cross(a, sm, F);
+    sym_vec(cJ[b], a, L);
+    v3_cross(a, o, axo);
+    v3_cross(cs[b], axo, t);
+    for (int i = 0; i < 3; i++) L[i] -= t[i];
+    for (int i = 0; i < 3; i++) { M[i][col] = M[col][i] = F[i]; M[3 + i][col] = M[col][3 + i] = L[i]; }
+    for (int kb = b; kb >= 1; kb = m->parent[kb]) {
+      real ok[3], oxF[3], mom[3];
+      for (int i = 0; i < 3; i++) ok[i] = k->o[kb][i];
+      v3_cross(ok, F, oxF);
+      for (int i = 0; i < 3; i++) mom[i] = L[i] - oxF[i];
+      real val = v3_dot(k->a[kb], mom);
+      M[5 + kb][col] = val;
+      M[col][5 + kb] = val;
+    }
+    M[col][col] += m->armature[b];
+  }
+}
+
+static int cholesky(real* A, int n, int ld) { /* in-place lower */
+  for (int j = 0; j < n; j++) {
+    real d = A[j * ld + j];
+    for (int k = 0; k < j; k++) d -= A[j * ld + k] * A[j * ld + k];
+    if (!(d > 0)) return -1;
+    d = sqrt(d);
+    A[j * ld + j] = d;
+    for (int i = j + 1; i < n; i++) {
+      real s = A[i * ld + j];
+      for (int k = 0; k < j; k++) s -= A[i * ld + k] * A[j * ld + k];
+      A[i * ld + j] = s / d;
+    }
+  }
+  return 0;
+}
+static void chol_solve(const real* L, int n, int ld, real* x) {
+  for (int i = 0; i < n; i++) {
+    real s = x[i];
+    for (int k = 0; k < i; k++) s -= L[i * ld + k] * x[k];
+    x[i] = s / L[i * ld + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    real s = x[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * ld + i] * x[k];
+    x[i] = s / L[i * ld + i];
+  }
+}
+
+typedef struct {
+  int kind;      /* 0 contact normal, 1 tangent1, 2 tangent2, 3 joint limit */
+  int pt;        /* candidate contact / dof index */
+  real J[NV], Y[NV], D, target, lam;
+} Row;
+
+#define MAX_ROWS (NC_MAX * 3 + ND)
+
+/* full generalized solve: M x = b restricted to free dofs (fixed base -> 12 joint dofs) */
+static void msolve(const real* L, int off, int n, real* x) {
+  real t[NV];
+  for (int i = 0; i < n; i++) t[i] = x[off + i];
+  chol_solve(L, n, NV, t);
+  for (int i = 0; i < NV; i++) x[i] = (i >= off) ? t[i - off] : 0;
+}
+
+static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* root, real* q,
+                    real* qd, real* lamst, const real* tau, real mass0, real fric, real* cf_out,
+                    int* nonfinite) {
+  const real dt = cfg->sim_dt;
+  real nu[NV];
+  for (int i = 0; i < 3; i++) { nu[i] = root[7 + i]; nu[3 + i] = root[10 + i]; }
+  for (int j = 0; j < ND; j++) nu[6 + j] = qd[j];
+  const int fixed = cfg->fix_base_link;
+  if (fixed) for (int i = 0; i < 6; i++) nu[i] = 0;
+  Kin k;
+  kinematics(m, root + 3, q, nu, mass0, &k);
+  real h[NV], M[NV][NV];
+  bias_forces(m, &k, nu, cfg->gravity_z, h);
+  mass_matrix(m, &k, M);
+  const int off = fixed ? 6 : 0, n = NV - off;
+  real Lm[NV * NV];
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) Lm[i * NV + j] = M[off + i][off + j];
+  if (cholesky(Lm, n, NV) != 0) { *nonfinite = 1; return; }
+  real acc[NV];
+  for (int i = 0; i < NV; i++) acc[i] = (i >= 6 ? tau[i - 6] : 0) - h[i];
+  msolve(Lm, off, n, acc);
+  for (int i = 0; i < NV; i++) nu[i] += dt * acc[i];
+
+  /* ---- constraint rows ---- */
+  static __thread Row rows[MAX_ROWS];
+  int nr = 0;
+  const real mu = R(0.5) * (fric + cfg->ground_friction);
+  const real beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel, off_c = cfg->contact_offset;
+  int body_of_row[MAX_ROWS];
+  if (!fixed) {
+    for (int c = 0; c < m->nc; c++) {
+      int b = m->cbody[c];
+      real x[3];
+      mat3_vec(k.Rb[b], m->cpos[c], x);
+      for (int i = 0; i < 3; i++) x[i] += k.o[b][i];
+      real xw[3] = {x[0] + root[0], x[1] + root[1], x[2] + root[2]};
+      real hg, nrm[3];
+      ground(cfg, hf, xw[0], xw[1], &hg, nrm);
+      real phi = (xw[2] - hg) * nrm[2];
+      if (!(phi < off_c)) { for (int d = 0; d < 3; d++) lamst[c * 3 + d] = 0; continue; }
+      /* tangent basis */
+      real t1[3], t2[3];
+      real ref[3] = {1, 0, 0};
+      real dd = v3_dot(ref, nrm);
+      for (int i = 0; i < 3; i++) t1[i] = ref[i] - dd * nrm[i];
+      real tn = sqrt(v3_dot(t1, t1));
+      for (int i = 0; i < 3; i++) t1[i] /= tn;
+      v3_cross(nrm, t1, t2);
+      const real* dirs[3] = {nrm, t1, t2};
+      for (int d = 0; d < 3; d++) {
+        Row* r = &rows[nr];
+        r->kind = d; r->pt = c;
+        const real* e = dirs[d];
+        for (int i = 0; i < 3; i++) r->J[i] = e[i];
+        real xe[3];
+        v3_cross(x, e, xe);
+        for (int i = 0; i < 3; i++) r->J[3 + i] = xe[i];
+        for (int j = 0; j < ND; j++) r->J[6 + j] = 0;
+        for (int kb = b; kb >= 1; kb = m->parent[kb]) {
+          real rr[3], axr[3];
+          for (int i = 0; i < 3; i++) rr[i] = x[i] - k.o[kb][i];
+          v3_cross(k.a[kb], rr, axr);
+          r->J[5 + kb] = v3_dot(e, axr);
+        }
+        if (d == 0) r->target = phi >= 0 ? -phi / dt : fmin(-beta * phi / dt, vmax);
+        else r->target = 0;
+        r->lam = lamst[c * 3 + d];
+        body_of_row[nr] = b;
+        nr++;
+      }
+    }
+  }
+  const real lim_margin = R(0.01);
+  for (int j = 0; j < ND; j++) {
+    real glo = q[j] - m->lower[j + 1], ghi = m->upper[j + 1] - q[j];
+    real sgn, gap;
+    if (glo < lim_margin) { sgn = 1; gap = glo; }
+    else if (ghi < lim_margin) { sgn = -1; gap = ghi; }
+    else { lamst[NC_MAX * 3 + j] = 0; continue; }
+    Row* r = &rows[nr];
+    r->kind = 3; r->pt = j;
+    memset(r->J, 0, sizeof(r->J));
+    r->J[6 + j] = sgn;
+    r->target = gap >= 0 ? -gap / dt : fmin(-beta * gap / dt, vmax);
+    r->lam = lamst[NC_MAX * 3 + j];
+    body_of_row[nr] = -1;
+    nr++;
+  }
+  for (int r = 0; r < nr; r++) {
+    for (int i = 0; i < NV; i++) rows[r].Y[i] = rows[r].J[i];
+    msolve(Lm, off, n, rows[r].Y);
+    rows[r].D = 0;
+    for (int i = 0; i < NV; i++) rows[r].D += rows[r].J[i] * rows[r].Y[i];
+    /* warm start */
+    for (int i = 0; i < NV; i++) nu[i] += rows[r].Y[i] * rows[r].lam;
+  }
+  for (int it = 0; it < cfg->pgs_iterations; it++) {
+    for (int r = 0; r < nr; r++) {
+      Row* rn = &rows[r];
+      if (rn->kind == 0 || rn->kind == 3) {
+        real v = 0;
+        for (int i = 0; i < NV; i++) v += rn->J[i] * nu[i];
+        real ln = rn->lam + (rn->target - v) / rn->D;
+        if (ln < 0) ln = 0;
+        real dl = ln - rn->lam;
+        rn->lam = ln;
+        for (int i = 0; i < NV; i++) nu[i] += rn->Y[i] * dl;
+        if (rn->kind == 0) {
+          Row* r1 = &rows[r + 1];
+          Row* r2 = &rows[r + 2];
+          real v1 = 0, v2 = 0;
+          for (int i = 0; i < NV; i++) { v1 += r1->J[i] * nu[i]; v2 += r2->J[i] * nu[i]; }
+          real l1 = r1->lam - v1 / r1->D, l2 = r2->lam - v2 / r2->D;
+          real lim = mu * rn->lam, nn = sqrt(l1 * l1 + l2 * l2);
+          if (nn > lim) { real s = lim / nn; l1 *= s; l2 *= s; }
+          real d1 = l1 - r1->lam, d2 = l2 - r2->lam;
+          r1->lam = l1; r2->lam = l2;
+          for (int i = 0; i < NV; i++) nu[i] += r1->Y[i] * d1 + r2->Y[i] * d2;
+          r += 2;
+        }
+      }
+    }
+  }
+  /* contact forces (last substep) and warm-start store */
+  for (int b = 0; b < NB * 3; b++) cf_out[b] = 0;
+  for (int r = 0; r < nr; r++) {
+    Row* rr = &rows[r];
+    if (rr->kind == 3) { lamst[NC_MAX * 3 + rr->pt] = rr->lam; continue; }
+    lamst[rr->pt * 3 + rr->kind] = rr->lam;
+    int b = body_of_row[r];
+    for (int i = 0; i < 3; i++) cf_out[b * 3 + i] += rr->J[i] * rr->lam / dt;
+  }
+  /* integrate */
+  int bad = 0;
+  for (int i = 0; i < NV; i++) if (!isfinite(nu[i])) bad = 1;
+  if (bad) { *nonfinite = 1; return; }
+  for (int j = 0; j < ND; j++) { qd[j] = nu[6 + j]; q[j] += dt * qd[j]; }
+  if (!fixed) {
+    for (int i = 0; i < 3; i++) { root[7 + i] = nu[i]; root[10 + i] = nu[3 + i]; root[i] += dt * nu[i]; }
+    real* Q = root + 3;
+    real w[3] = {nu[3], nu[4], nu[5]};
+    real th = sqrt(v3_dot(w, w)) * dt;
+    if (th > 0) {
+      real s = sin(th / 2) / (th / dt), c = cos(th / 2);
+      real dq[4] = {w[0] * s, w[1] * s, w[2] * s, c};
+      real x = dq[3] * Q[0] + dq[0] * Q[3] + dq[1] * Q[2] - dq[2] * Q[1];
+      real y = dq[3] * Q[1] - dq[0] * Q[2] + dq[1] * Q[3] + dq[2] * Q[0];
+      real z = dq[3] * Q[2] + dq[0] * Q[1] - dq[1] * Q[0] + dq[2] * Q[3];
+      real ww = dq[3] * Q[3] - dq[0] * Q[0] - dq[1] * Q[1] - dq[2] * Q[2];
+      real nq = sqrt(x * x + y * y + z * z + ww * ww);
+      Q[0] = x / nq; Q[1] = y / nq; Q[2] = z / nq; Q[3] = ww / nq;
+    }
+  } else {
+    for (int i = 7; i < 13; i++) root[i] = 0;
+  }
+}
+
+static void rigid_states(const Model* m, const real* root, const real* q, const real* qd, real mass0,
+                         real* out) {
+  real nu[NV];
+  for (int i = 0; i < 3; i++) { nu[i] = root[7 + i]; nu[3 + i] = root[10 + i]; }
+  for (int j = 0; j < ND; j++) nu[6 + j] = qd[j];
+  Kin k;
+  kinematics(m, root + 3, q, nu, mass0, &k);
+  for (int b = 0; b < NB; b++) {
+    real* o = out + b * 13;
+    for (int i = 0; i < 3; i++) o[i] = k.o[b][i] + root[i];
+    mat_to_quat(k.Rb[b], o + 3);
+    for (int i = 0; i < 3; i++) { o[7 + i] = k.v[b][i]; o[10 + i] = k.w[b][i]; }
+  }
+}
+
+/* ---------------------------------------------------------------- public (ctypes) API */
+/* One policy step (cfg->decimation substeps) for n envs, AoS arrays:
+ *   root[n][13], q[n][12], qd[n][12], lam[n][LAMW] (in/out), actions[n][12] (already
+ *   delayed/noised/clipped as in humanoid_env.py:620-635), mass0[n] (base mass after DR),
+ *   fric[n];  outputs torques[n][12] (last substep), contact[n][13][3], rigid[n][13][13],
+ *   nonfinite[n].  Returns 0. */
+#ifdef REF_FLOAT
+#define API(name) name##_f32
+#else
+#define API(name) name##_f64
+#endif
+int API(ref_step)(const hg_cfg* cfg, const hg_model* hm, const int16_t* hf, int n, real* root,
+                  real* q, real* qd, real* lam, const real* actions, const real* mass0,
+                  const real* fric, real* torques, real* contact, real* rigid, int32_t* nonfinite) {
+  Model m;
+  load_model(hm, &m);
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < n; e++) {
+    real* re = root + (size_t)e * 13;
+    real* qe = q + (size_t)e * ND;
+    real* qde = qd + (size_t)e * ND;
+    const real* ae = actions + (size_t)e * ND;
+    real tau[ND];
+    int bad = 0;
+    for (int s = 0; s < cfg->decimation && !bad; s++) {
+      for (int j = 0; j < ND; j++) {
+        real t = R(cfg->kp[j]) * (ae[j] * R(cfg->action_scale) + R(cfg->default_dof_pos[j]) - qe[j]) -
+                 R(cfg->kd[j]) * qde[j];
+        real lim = cfg->torque_limit[j];
+        tau[j] = t < -lim ? -lim : (t > lim ? lim : t);
+      }
+      substep(cfg, &m, hf, re, qe, qde, lam + (size_t)e * LAMW, tau, mass0[e], fric[e],
+              contact + (size_t)e * NB * 3, &bad);
+    }
+    for (int j = 0; j < ND; j++) torques[(size_t)e * ND + j] = tau[j];
+    nonfinite[e] = bad;
+    rigid_states(&m, re, qe, qde, mass0[e], rigid + (size_t)e * NB * 13);
+  }
+  return 0;
+}
+
+/* Expose the dynamics terms for analytic tests: M (18x18 incl. armature) and h. */
+int API(ref_dynamics)(const hg_model* hm, const real* root, const real* q, const real* qd,
+                      real mass0, real gz, real* M_out, real* h_out) {
+  Model m;
+  load_model(hm, &m);
+  real nu[NV];
+  for (int i = 0; i < 3; i++) { nu[i] = root[7 + i]; nu[3 + i] = root[10 + i]; }
+  for (int j = 0; j < ND; j++) nu[6 + j] = qd[j];
+  Kin k;
+  kinematics(&m, root + 3, q, nu, mass0, &k);
+  real M[NV][NV];
+  mass_matrix(&m, &k, M);
+  bias_forces(&m, &k, nu, gz, h_out);
+  memcpy(M_out, M, sizeof(M));
+  return 0;
+}
+
+int API(ref_lamw)(void) { return LAMW; }

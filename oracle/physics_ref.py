@@ -1,0 +1,74 @@
+"""ctypes wrapper of oracle/libphysref.so (CPU reference physics).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg; never by the product package.  See physics_ref.c for what it restates.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libphysref.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class RefSim:
+    """AoS CPU simulator state for n envs (root[n,13], q/qd[n,12], warm-start lambdas)."""
+
+    def __init__(self, cfg, model, n, precision="f64", heightfield=None):
+        self.cfg, self.model, self.n = cfg, model, n
+        self.dt = np.float64 if precision == "f64" else np.float32
+        self.fn = getattr(lib(), "ref_step_" + precision)
+        self.lamw = lib().ref_lamw_f64()
+        self.root = np.zeros((n, 13), self.dt)
+        self.root[:, 6] = 1.0
+        self.q = np.zeros((n, 12), self.dt)
+        self.qd = np.zeros((n, 12), self.dt)
+        self.lam = np.zeros((n, self.lamw), self.dt)
+        self.mass0 = np.full(n, model.mass[0], self.dt)
+        self.fric = np.full(n, 1.0, self.dt)
+        self.torques = np.zeros((n, 12), self.dt)
+        self.contact = np.zeros((n, 13, 3), self.dt)
+        self.rigid = np.zeros((n, 13, 13), self.dt)
+        self.nonfinite = np.zeros(n, np.int32)
+        self.hf = None if heightfield is None else np.ascontiguousarray(heightfield, np.int16)
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, self.dt)
+        assert a.shape == (self.n, 12)
+        hf = None if self.hf is None else _p(self.hf)
+        self.fn(ctypes.byref(self.cfg), ctypes.byref(self.model), hf, ctypes.c_int(self.n), _p(self.root),
+                _p(self.q), _p(self.qd), _p(self.lam), _p(a), _p(self.mass0), _p(self.fric), _p(self.torques),
+                _p(self.contact), _p(self.rigid), _p(self.nonfinite))
+
+
+def dynamics(model, root, q, qd, mass0=None, gz=-9.81):
+    """(M[18,18], h[18]) at a state, float64."""
+    M = np.zeros((18, 18))
+    h = np.zeros(18)
+    root = np.ascontiguousarray(root, np.float64)
+    q = np.ascontiguousarray(q, np.float64)
+    qd = np.ascontiguousarray(qd, np.float64)
+    m0 = model.mass[0] if mass0 is None else mass0
+    lib().ref_dynamics_f64(ctypes.byref(model), _p(root), _p(q), _p(qd), ctypes.c_double(m0),
+                           ctypes.c_double(gz), _p(M), _p(h))
+    return M, h
