@@ -1,0 +1,238 @@
+"""Headline benchmark: env-steps/s (whole node) of the full PPO loop at 4096 envs per GPU.
+
+A "step" here is one PPO iteration of the reference's OnPolicyRunner.learn
+(humanoid/algo/ppo/on_policy_runner.py:110-170): T=24 x [policy act -> env.step (K_step: 10
+physics substeps + K_post: rewards/obs/reset) -> process_env_step], then GAE (K_gae) and the PPO
+update (2 epochs x 4 minibatches).  value = envs_per_gpu * T * n_gpus * K / max-over-ranks time,
+i.e. the reference's Perf/total_fps summed over the node.  Workload: BASELINE.json configs[1]
+(XBot-L, flat terrain, 4096 envs/GPU, 24-step rollout), synthetic data (random-init policy,
+no checkpoint), all physics/env inputs resident in HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run), envs sharded (4096 per rank, weak
+scaling), policy gradients all-reduced with RCCL (backend "nccl") once per minibatch.
+
+The roofline object is for the dominant kernel, K_step (FP32 VALU bound: state lives in
+registers/scratch across the 10 substeps, HBM traffic is ~1.5 KB/env-step); its launch time is
+measured with HIP events recorded on the stream the kernel runs on (torch's current stream,
+which the env passes to hg_step).  cpu_baseline times the oracle port (C reference physics,
+numpy env logic, torch-CPU PPO) on a bounded sample on the host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "humanoid-gym-with-comments_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) dense peak
+HBM_PEAK_GBS = 8000.0
+
+
+class KernelTimer:
+    """HIP-event pairs around kernel launches on the current stream."""
+
+    def __init__(self):
+        self.events = {}
+        self.enabled = False
+
+    def start(self, name):
+        if not self.enabled:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.events.setdefault(name, []).append([e, None])
+
+    def stop(self, name):
+        if not self.enabled:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.events[name][-1][1] = e
+
+    def mean_ms(self, name):
+        pairs = self.events.get(name, [])
+        return float(np.mean([a.elapsed_time(b) for a, b in pairs])) if pairs else float("nan")
+
+    def count(self, name):
+        return len(self.events.get(name, []))
+
+
+def physics_flops_per_env_step(rows, decimation=10):
+    """Analytic FLOP count of the K_step algorithm: per substep
+    kinematics 3.3k + bias forces 1.8k + inertia 1.5k + Cholesky 2.0k + solve 0.65k +
+    integration 0.1k, plus per constraint row: Jacobian 0.12k + M^-1 J^T solve 0.65k +
+    diagonal/warm start 0.07k + 6 PGS sweeps x 82.  Plus one end-of-step FK + quaternions (4.0k)."""
+    per_sub = 9350 + rows * (120 + 650 + 72 + 6 * 82)
+    return decimation * per_sub + 4000
+
+
+def active_rows(env):
+    from humanoid import _native as N
+    lam = env._view(N.T["CONTACT_LAMBDA"])
+    contacts = (lam[:, 0:48:3] > 0).sum(dim=1).float()
+    limits = (lam[:, 48:60] > 0).sum(dim=1).float()
+    return float((3 * contacts + limits).mean().item())
+
+
+def make_env(num_envs, device, seed):
+    from humanoid.envs import XBotLCfg
+    from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
+    from humanoid.utils.helpers import SimParams
+    cfg = XBotLCfg()
+    cfg.env.num_envs = num_envs
+    cfg.seed = seed
+    return XBotLFreeEnv(cfg, SimParams(), "hg_sim", device, True)
+
+
+def train_cfg(T):
+    from humanoid.envs import XBotLCfgPPO
+    from humanoid.utils.helpers import class_to_dict
+    t = XBotLCfgPPO()
+    t.runner.num_steps_per_env = T
+    return class_to_dict(t)
+
+
+def cpu_baseline(n_envs=256, T=24, threads=None):
+    """The oracle port on the host: C reference physics (f32, OpenMP over envs), numpy env logic
+    (oracle/pipeline_ref.py), torch-CPU policy + GAE + PPO update — one full PPO iteration on
+    n_envs envs.  Returns env-steps/s."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import physics_ref as P
+    import pipeline_ref as PR
+    import envlogic_ref as E
+    from humanoid import _native as N
+    from humanoid.envs import XBotLCfg
+    from humanoid.envs.custom.humanoid_env import build_hg_cfg
+    from humanoid.algo.ppo import ActorCritic, PPO
+    threads = threads or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    cfg = XBotLCfg()
+    model, js = N.load_model(armature=cfg.sim.hg.armature)
+    hc, _ = build_hg_cfg(cfg, n_envs, cfg.sim.dt, 5, js)
+    oc = PR.Cfg(hc)
+    side = int(np.ceil(np.sqrt(n_envs)))
+    origins = np.zeros((n_envs, 3), np.float32)
+    origins[:, 0] = 3.0 * (np.arange(n_envs) // side)
+    origins[:, 1] = 3.0 * (np.arange(n_envs) % side)
+    rng = np.random.default_rng(5)
+    mass = model.mass[0] + rng.uniform(-5, 5, n_envs)
+    fric = rng.uniform(0.1, 2.0, n_envs)
+    S, obs, priv = PR.initial_state(oc, origins, mass, fric)
+    sim = P.RefSim(hc, model, n_envs, "f32")
+    sim.mass0[:] = mass
+    sim.fric[:] = fric
+    torch.manual_seed(5)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128])
+    ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.994, lam=0.9,
+              learning_rate=1e-5, entropy_coef=0.001, schedule="adaptive", desired_kl=0.01, device="cpu")
+    ppo.init_storage(n_envs, T, [705], [219], [12])
+    ppo.storage.gae_fn = lambda r, d, v, lv, g, l: tuple(
+        torch.from_numpy(x)[..., None] for x in E.gae(r[..., 0].numpy(), d[..., 0].numpy(), v[..., 0].numpy(),
+                                                      lv[:, 0].numpy(), g, l))
+    t0 = time.time()
+    counter = 0
+    with torch.inference_mode():
+        for _ in range(T):
+            a = ppo.act(torch.from_numpy(obs), torch.from_numpy(priv)).numpy()
+            a_ref = PR.preprocess_actions(oc, a, S["actions"], counter)
+            S["actions"] = a_ref
+            sim.root[:], sim.q[:], sim.qd[:], sim.lam[:] = S["root_states"], S["dof_pos"], S["dof_vel"], S["lambda"]
+            sim.step(a_ref)
+            S.update(root_states=sim.root.copy(), dof_pos=sim.q.copy(), dof_vel=sim.qd.copy(), lambda_=None,
+                     torques=sim.torques.copy(), contact_forces=sim.contact.copy(), rigid_state=sim.rigid.copy())
+            S.pop("lambda_")
+            S["lambda"] = sim.lam.copy()
+            counter += 1
+            obs, priv, rew, reset, timeout, _ = PR.post(oc, S, counter, obs, priv)
+            infos = {"time_outs": torch.from_numpy(timeout)}
+            ppo.process_env_step(torch.from_numpy(rew), torch.from_numpy(reset), infos)
+        ppo.compute_returns(torch.from_numpy(priv))
+    ppo.update()
+    dt = time.time() - t0
+    return n_envs * T / dt, threads, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10, help="timed PPO iterations")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--T", type=int, default=24, help="rollout length (num_steps_per_env)")
+    ap.add_argument("--cpu-envs", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = f"cuda:{local}"
+    torch.manual_seed(5 + rank)
+    np.random.seed(5 + rank)
+    from humanoid.algo.ppo import OnPolicyRunner
+    env = make_env(args.envs, device, seed=5 + rank)
+    runner = OnPolicyRunner(env, train_cfg(args.T), log_dir=None, device=device)
+    timer = KernelTimer()
+    env.kernel_timer = timer
+    runner.learn(args.warmup, init_at_random_ep_len=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.enabled = True
+    t0 = time.time()
+    runner.learn(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.time() - t0
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    env_steps = args.envs * args.T * args.steps * world
+    value = env_steps / elapsed
+    rows = active_rows(env)
+    ms_step = timer.mean_ms("k_step")
+    flops = physics_flops_per_env_step(rows) * args.envs
+    achieved_tflops = flops / (ms_step * 1e-3) / 1e12
+    roofline = {"kernel": "k_step", "bound": "mfma", "pipe": "fp32-valu (f32 MFMA peak = f32 vector peak)",
+                "achieved": round(achieved_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 6), "traffic": None,
+                "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
+                "flops_per_launch": flops, "active_rows_per_env": round(rows, 2),
+                "k_post_avg_ms": round(timer.mean_ms("k_post"), 4)}
+    result = {
+        "metric": "env-steps/sec (whole node) at 4096 envs + PPO iters/sec, 1/2/4/8 MI355X",
+        "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ppo_iters_per_sec": round(args.steps / elapsed, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "XBot-L flat terrain, 4096 envs/GPU, PPO 24-step rollout (BASELINE configs[1])",
+                   "envs_per_gpu": args.envs, "num_steps_per_env": args.T, "parallelism": f"dp{world}",
+                   "ppo": "2 epochs x 4 minibatches, actor 705-512-256-128-12, critic 219-768-256-128-1"},
+        "roofline": roofline,
+        "collection_time_s": round(runner.last_iteration_stats.get("collection_time", float("nan")), 4),
+        "learn_time_s": round(runner.last_iteration_stats.get("learn_time", float("nan")), 4),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, threads, dt = cpu_baseline(args.cpu_envs, args.T)
+        result["cpu_baseline"] = {"value": round(v, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+                                  "sample": f"1 PPO iteration, {args.cpu_envs} envs x {args.T} steps, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -130,6 +130,7 @@ class XBotLFreeEnv(BaseTask):
         self.height_samples = None
         self.debug_viz = False
         self.init_done = False
+        self.kernel_timer = None  # optional: object with start(name)/stop(name) (bench.py HIP-event timer)
         self._parse_cfg(self.cfg)
         super().__init__(cfg, sim_params, physics_engine, sim_device, headless)
         self._init_buffers()
@@ -375,10 +376,18 @@ class XBotLFreeEnv(BaseTask):
         if a.shape != (self.num_envs, self.num_actions):
             raise ValueError(f"actions must be [{self.num_envs}, {self.num_actions}], got {tuple(a.shape)}")
         s = self._stream()
+        kt = self.kernel_timer
+        if kt is not None:
+            kt.start("k_step")
         N.check(self.hg.hg_step(self.sim, ctypes.c_void_p(a.data_ptr()), ctypes.c_uint64(self.common_step_counter), s),
                 self.sim)
+        if kt is not None:
+            kt.stop("k_step")
+            kt.start("k_post")
         self.common_step_counter += 1
         N.check(self.hg.hg_post(self.sim, ctypes.c_uint64(self.common_step_counter), s), self.sim)
+        if kt is not None:
+            kt.stop("k_post")
         self._parity ^= 1
         self._publish_extras()
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras

@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU session: parity tests then a short bench.  Stops at the first crash/timeout
+# (exit codes other than 0/1 from pytest), never retries.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${STEPS:-5}
+timeout -k 10 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -30 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -n "$SKIP_BENCH" ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+brc=$?
+echo "bench rc=$brc"
+grep -v "MLP\|Linear\|ELU\|Sequential\|^)" gpurun_out/bench.log | tail -20
+exit $brc

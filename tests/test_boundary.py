@@ -1,0 +1,68 @@
+"""The C-ABI library (CPU-side checks, no compute): it builds for gfx950, loads, exports every
+symbol include/hgsim.h declares, and the ctypes struct layouts match the C header."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from humanoid import _native as N
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "hgsim.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(hg_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+
+
+def test_header_lists_exports():
+    assert header_functions() == sorted(N.EXPORTS)
+
+
+def test_library_exports_all_symbols():
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("libhgsim.so not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    syms = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    missing = [s for s in N.EXPORTS if s not in syms]
+    assert not missing, missing
+
+
+def test_library_loads_without_gpu():
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("libhgsim.so not built")
+    L = N.load_library()
+    assert b"gfx950" in L.hg_version()
+    cfg = N.HgCfg()
+    assert L.hg_arena_bytes(ctypes.byref(cfg)) == 0          # num_envs = 0 -> invalid
+    cfg.num_envs, cfg.frame_stack, cfg.c_frame_stack = 4096, 15, 3
+    nbytes = L.hg_arena_bytes(ctypes.byref(cfg))
+    assert 4096 * (705 + 219) * 4 * 2 < nbytes < 64 << 20    # SoA state + double-buffered obs
+    out = ctypes.c_void_p()
+    rc = L.hg_create(ctypes.byref(cfg), None, None, 0, ctypes.byref(out))
+    assert rc != 0 and b"null" in L.hg_last_error(None)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    c = tmp_path / "sz.c"
+    c.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "hgsim.h"\nint main(){printf("%zu %zu %zu %zu %zu",'
+                 'sizeof(hg_model),sizeof(hg_cfg),offsetof(hg_cfg,heightfield),offsetof(hg_cfg,seed),sizeof(hg_desc));}')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(c), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(N.HgModel), ctypes.sizeof(N.HgCfg), N.HgCfg.heightfield.offset, N.HgCfg.seed.offset,
+            ctypes.sizeof(N.HgDesc)]
+    assert got == want
+
+
+def test_model_table():
+    m, js = N.load_model()
+    assert m.num_bodies == 13 and m.num_dof == 12 and m.num_contacts == 16 and m.num_foot_contacts == 8
+    assert abs(js["total_mass"] - 53.036) < 0.01
+    bodies = [b["name"] for b in js["bodies"]]
+    assert bodies.index("left_ankle_roll_link") == 6 and bodies.index("right_ankle_roll_link") == 12
+    assert bodies.index("left_knee_link") == 4 and bodies.index("right_knee_link") == 10
