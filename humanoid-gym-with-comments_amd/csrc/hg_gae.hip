@@ -4,8 +4,8 @@
 //
 // Pass 1 (k_gae_scan): one lane per env walks t = T-1..0 with the carry in a register; every
 // [t, :] row it touches is a contiguous 4*N-byte stream, so the wave's loads/stores coalesce.
-// The op order of the reference is kept and FMA contraction is disabled (explicit _rn
-// intrinsics), so returns match the reference bit-for-bit up to torch's own rounding.
+// The op order of the reference is kept and FMA contraction is disabled (clang fp contract(off);
+// plus -ffp-contract=off for this file), so returns match the reference bitwise.
 // Per-block (sum A, sum A^2) partials are reduced in fp64 and added to stats[0..1].
 // Pass 2 (k_gae_norm): A = (A - mean) / (std_unbiased + 1e-8), elementwise, float4-vectorised.
 // Roofline: HBM.  Algorithmic bytes: 17 B per (t, env) in pass 1 (r 4 + done 1 + V 4 + R 4 +
@@ -18,6 +18,7 @@ __global__ void __launch_bounds__(256) k_gae_scan(const float* __restrict__ rewa
                                                   const float* __restrict__ last_values, float* __restrict__ returns,
                                                   float* __restrict__ advantages, double* __restrict__ stats, int T,
                                                   int N, float gamma, float lam) {
+#pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
   if (e < N) {
@@ -28,13 +29,13 @@ __global__ void __launch_bounds__(256) k_gae_scan(const float* __restrict__ rewa
       const float v = values[i];
       const float nnt = 1.0f - (float)dones[i];
       // delta = r + nnt*gamma*next_v - v
-      const float g = __fmul_rn(nnt, gamma);
-      const float delta = __fsub_rn(__fadd_rn(rewards[i], __fmul_rn(g, next_v)), v);
+      const float g = nnt * gamma;
+      const float delta = (rewards[i] + g * next_v) - v;
       // adv = delta + nnt*gamma*lam*adv
-      adv = __fadd_rn(delta, __fmul_rn(__fmul_rn(g, lam), adv));
-      const float ret = __fadd_rn(adv, v);
+      adv = delta + (g * lam) * adv;
+      const float ret = adv + v;
       returns[i] = ret;
-      const float a = __fsub_rn(ret, v);  // advantages = returns - values
+      const float a = ret - v;  // advantages = returns - values
       advantages[i] = a;
       s1 += (double)a;
       s2 += (double)a * (double)a;
