@@ -1,5 +1,6 @@
 // hg_api.hip — host side of the hg_sim C ABI (include/hgsim.h): arena layout, tensor
 // descriptors, launches.  No host synchronisation on any step/post path.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -9,6 +10,7 @@
 #include "hg_common.h"
 
 extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
+extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
 extern "C" int hg_launch_post(const HgState* S, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
                               float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
                               float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
@@ -100,6 +102,7 @@ struct Sim {
   Layout L;
   HgState S;
   int parity;  // which obs/priv buffer holds the latest stack
+  int physics_version;  // 2 (lane-parallel, default) or 1 (lane-per-env reference kernel)
   std::string err;
 };
 
@@ -143,8 +146,9 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   if (model->num_bodies != HG_NB || model->num_dof != HG_ND)
     return fail(nullptr, HG_ERR_ARG, "model must have 13 bodies / 12 dofs (XBot-L profile)");
   if (model->num_contacts <= 0 || model->num_contacts > HG_NC) return fail(nullptr, HG_ERR_ARG, "bad contact count");
-  for (int b = 1; b < HG_NB; b++)
-    if (model->parent[b] < 0 || model->parent[b] >= b) return fail(nullptr, HG_ERR_ARG, "bodies must be topologically ordered");
+  for (int b = 1; b < HG_NB; b++)  // two 6-link leg chains off the base (XBot-L topology)
+    if (model->parent[b] != ((b == 1 || b == 7) ? 0 : b - 1))
+      return fail(nullptr, HG_ERR_ARG, "model topology must be base + two 6-link leg chains (bodies 1-6, 7-12)");
   if (cfg->decimation <= 0 || cfg->sim_dt <= 0.f || cfg->frame_stack <= 0 || cfg->c_frame_stack <= 0)
     return fail(nullptr, HG_ERR_ARG, "bad timing / stacking config");
   if (cfg->resample_interval <= 0 || cfg->push_interval <= 0) return fail(nullptr, HG_ERR_ARG, "bad intervals");
@@ -165,6 +169,10 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   s->arena = (char*)arena;
   s->bytes = arena_bytes;
   s->parity = 0;
+  {
+    const char* pv = getenv("HG_PHYSICS");
+    s->physics_version = (pv && strcmp(pv, "v1") == 0) ? 1 : 2;
+  }
   const int n = cfg->num_envs;
   HgState& S = s->S;
   S.n = n;
@@ -274,7 +282,9 @@ int hg_tensor(void* sim, int id, hg_desc* d) {
 int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream) {
   Sim* s = (Sim*)sim;
   if (!s || !actions) return fail(s, HG_ERR_ARG, "null argument");
-  if (hg_launch_step(&s->S, actions, step_counter, (hipStream_t)stream) != 0) return fail(s, HG_ERR_HIP, "k_step launch failed");
+  const int rc = s->physics_version == 1 ? hg_launch_step(&s->S, actions, step_counter, (hipStream_t)stream)
+                                         : hg_launch_step2(&s->S, actions, step_counter, (hipStream_t)stream);
+  if (rc != 0) return fail(s, HG_ERR_HIP, "k_step launch failed");
   return HG_OK;
 }
 
@@ -345,4 +355,4 @@ extern "C" int hg_set_root_state_indexed(void* sim, const int32_t* env_ids, int 
   return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_root launch failed");
 }
 
-extern "C" const char* hg_version(void) { return "hg_sim 0.1 (gfx950, physics v1: lane-per-env)"; }
+extern "C" const char* hg_version(void) { return "hg_sim 0.2 (gfx950, physics v2: 32 lanes/env, LDS-resident, Delassus PGS)"; }

@@ -278,6 +278,7 @@ __device__ bool substep(const hg_cfg* cfg, const hg_model* M, float* root, float
   const float mu = 0.5f * (fric + cfg->ground_friction);
   const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel, offc = cfg->contact_offset;
   if (!fixed) {
+    int nct = 0;
     for (int c = 0; c < M->num_contacts; c++) {
       const int b = M->contact_body[c];
       f3 x = k.o[b] + mat3_vec(k.R[b], ldm3(M->contact_pos, c));
@@ -285,10 +286,11 @@ __device__ bool substep(const hg_cfg* cfg, const hg_model* M, float* root, float
       f3 nrm;
       ground(cfg, x.x + root[0], x.y + root[1], &hg, &nrm);
       float phi = (x.z + root[2] - hg) * nrm.z;
-      if (!(phi < offc)) {
+      if (!(phi < offc) || nct >= 10) {  // at most 10 contacts (30 rows), candidate order
         lamst[c * 3 + 0] = lamst[c * 3 + 1] = lamst[c * 3 + 2] = 0.f;
         continue;
       }
+      nct++;
       f3 ref = mk(1, 0, 0);
       f3 t1 = ref - dot(ref, nrm) * nrm;
       t1 = rsqrtf(dot(t1, t1)) * t1;
@@ -317,6 +319,7 @@ __device__ bool substep(const hg_cfg* cfg, const hg_model* M, float* root, float
     if (glo < lim_margin) { sgn = 1.f; gap = glo; }
     else if (ghi < lim_margin) { sgn = -1.f; gap = ghi; }
     else { lamst[HG_NC * 3 + j] = 0.f; continue; }
+    if (nr >= 32) { lamst[HG_NC * 3 + j] = 0.f; continue; }  // at most 32 rows
     float* J = rw.J[nr];
     for (int i = 0; i < HG_NV; i++) J[i] = 0.f;
     J[6 + j] = sgn;

@@ -1,0 +1,643 @@
+// hg_physics2.hip — K_step v2: lane-parallel articulated dynamics for CDNA4 (gfx950).
+//
+// Same algorithm and results as hg_physics.hip (v1, one env per lane) and oracle/physics_ref.c,
+// re-mapped for the hardware:
+//   * 32 lanes per env, 2 envs per 64-lane wave, block = 1 wave; 4096 envs -> 2048 waves
+//     (8 per CU).  Every per-env working array lives in LDS (~11 KB/env), nothing spills.
+//   * Phases run lane-parallel: 12 joint rotations; the two 6-link leg chains (FK, RNEA forward
+//     and backward) on 2 lanes; 13 bodies' inertia/force terms; 12 mass-matrix columns;
+//     row-parallel Cholesky of M (18 lanes); explicit M^-1 by 18 parallel triangular solves;
+//     one constraint row per lane (<= 32 rows: sole/base contact normals+tangents, joint
+//     limits) with its Jacobian row held in the lane's registers; the Delassus matrix
+//     W = J M^-1 J^T one row per lane.
+//   * Projected Gauss-Seidel on W: lane r keeps row velocity v_r = J_r nu in a register; a row
+//     update reads v_r with v_readlane (no cross-lane reductions) and applies W[r][:] dlambda
+//     as one FMA per lane.  Gauss-Seidel order (normal, then the tangent pair, row by row) is
+//     the oracle's, so the PGS iterates are the same sequence as physics_ref.c.
+// Replaces humanoid_env.py:620-649 (+ refreshes :776-778), like v1.
+#include "hg_common.h"
+
+namespace {
+
+constexpr int RMAX = 32;
+
+struct __align__(16) EnvSh {
+  float root[16];
+  float q[12], qd[12], act[12], tau[12];
+  float nu[20];
+  float h[20];
+  float lamst[64];
+  float R[13][9];
+  float Lr[13][9];
+  float axp[13][3];  // joint axis in the parent-body frame (jrot * axis)
+  float o[13][3], a[13][3], c[13][3], w[13][3], v[13][3], al[13][3], ac[13][3], f[13][3], n[13][3];
+  float Iw[13][6];
+  float cm[13], cs[13][3], cJ[13][6];
+  union {
+    struct { float M[18][20]; float Minv[18][20]; float invd[20]; } fac;
+    float W[RMAX][RMAX];
+  } u;
+  float Y[RMAX][18];
+  float rD[RMAX], rInvD[RMAX], rTgt[RMAX], rLam[RMAX];
+  float rx[RMAX][3], rd[RMAX][3];   // row geometry: point (base-centred) and direction
+  int rKind[RMAX], rPt[RMAX], rBody[RMAX];
+  float cf[13][3];
+  float mass0, fric;
+  int nrows, bad;
+};
+
+__device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ void st3(float* p, f3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+__device__ __forceinline__ f3 mv3(const float* R, f3 v) {
+  return mk(R[0] * v.x + R[1] * v.y + R[2] * v.z, R[3] * v.x + R[4] * v.y + R[5] * v.z,
+            R[6] * v.x + R[7] * v.y + R[8] * v.z);
+}
+__device__ __forceinline__ void mm3(const float* A, const float* B, float* C) {
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) C[i * 3 + j] = A[i * 3] * B[j] + A[i * 3 + 1] * B[3 + j] + A[i * 3 + 2] * B[6 + j];
+}
+__device__ __forceinline__ f3 symv(const float* S, f3 v) {
+  return mk(S[0] * v.x + S[3] * v.y + S[4] * v.z, S[3] * v.x + S[1] * v.y + S[5] * v.z,
+            S[4] * v.x + S[5] * v.y + S[2] * v.z);
+}
+
+__device__ void ground(const hg_cfg* cfg, float x, float y, float* h, f3* n) {
+  if (cfg->terrain_type == 0 || cfg->heightfield == nullptr) { *h = 0; *n = mk(0, 0, 1); return; }
+  const float hs = cfg->hf_horizontal_scale, vs = cfg->hf_vertical_scale;
+  float fx = (x + cfg->hf_border) / hs, fy = (y + cfg->hf_border) / hs;
+  int i = (int)floorf(fx), j = (int)floorf(fy);
+  i = max(0, min(i, cfg->hf_rows - 2));
+  j = max(0, min(j, cfg->hf_cols - 2));
+  float u = fminf(fmaxf(fx - i, 0.f), 1.f), v = fminf(fmaxf(fy - j, 0.f), 1.f);
+  const int16_t* hf = cfg->heightfield;
+  const int C = cfg->hf_cols;
+  float h00 = vs * hf[i * C + j], h10 = vs * hf[(i + 1) * C + j];
+  float h01 = vs * hf[i * C + j + 1], h11 = vs * hf[(i + 1) * C + j + 1];
+  float dhdx, dhdy;
+  if (u + v <= 1) { *h = h00 + u * (h10 - h00) + v * (h01 - h00); dhdx = (h10 - h00) / hs; dhdy = (h01 - h00) / hs; }
+  else { *h = h11 + (1 - u) * (h01 - h11) + (1 - v) * (h10 - h11); dhdx = (h11 - h01) / hs; dhdy = (h11 - h10) / hs; }
+  float inv = rsqrtf(dhdx * dhdx + dhdy * dhdy + 1);
+  *n = mk(-dhdx * inv, -dhdy * inv, inv);
+}
+
+// ---- kinematics: local rotations (lanes 1..12) + base frame (lane 0); then leg chains (lanes 0,1)
+__device__ void kin_local(EnvSh& E, const hg_model* M, int l) {
+  if (l >= 1 && l <= 12) {
+    const int b = l;
+    float Rq[9];
+    f3 k = ld3(M->axis[b]);
+    float s, c;
+    sincosf(E.q[b - 1], &s, &c);
+    float vv = 1 - c;
+    Rq[0] = c + k.x * k.x * vv;       Rq[1] = k.x * k.y * vv - k.z * s; Rq[2] = k.x * k.z * vv + k.y * s;
+    Rq[3] = k.y * k.x * vv + k.z * s; Rq[4] = c + k.y * k.y * vv;       Rq[5] = k.y * k.z * vv - k.x * s;
+    Rq[6] = k.z * k.x * vv - k.y * s; Rq[7] = k.z * k.y * vv + k.x * s; Rq[8] = c + k.z * k.z * vv;
+    mm3(M->joint_rot[b], Rq, E.Lr[b]);
+    st3(E.axp[b], mv3(M->joint_rot[b], k));
+  } else if (l == 0) {
+    const float x = E.root[3], y = E.root[4], z = E.root[5], w = E.root[6];
+    float* R = E.R[0];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
+    st3(E.o[0], mk(0, 0, 0));
+    st3(E.v[0], mk(E.nu[0], E.nu[1], E.nu[2]));
+    st3(E.w[0], mk(E.nu[3], E.nu[4], E.nu[5]));
+  }
+}
+
+// leg chain: R, o, a, w, v (+ RNEA forward terms alpha, acc when `bias`)
+__device__ void kin_chain(EnvSh& E, const hg_model* M, int leg, float gz, bool bias) {
+  float Rp[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) Rp[i] = E.R[0][i];
+  f3 op = mk(0, 0, 0), vp = ld3(E.v[0]), wp = ld3(E.w[0]);
+  f3 alp = mk(0, 0, 0), acp = mk(0, 0, -gz);
+  for (int k = 0; k < 6; k++) {
+    const int b = 1 + 6 * leg + k;
+    float Rb[9];
+    mm3(Rp, E.Lr[b], Rb);
+    f3 ob = op + mv3(Rp, ld3(M->joint_pos[b]));
+    f3 ab = mv3(Rp, ld3(E.axp[b]));
+    const float qd = E.nu[5 + b];
+    f3 r = ob - op;
+    f3 wb = wp + qd * ab;
+    f3 vb = vp + cross(wp, r);
+#pragma unroll
+    for (int i = 0; i < 9; i++) E.R[b][i] = Rb[i];
+    st3(E.o[b], ob); st3(E.a[b], ab); st3(E.w[b], wb); st3(E.v[b], vb);
+    if (bias) {
+      f3 alb = alp + cross(wp, qd * ab);
+      f3 acb = acp + cross(alp, r) + cross(wp, cross(wp, r));
+      st3(E.al[b], alb); st3(E.ac[b], acb);
+      alp = alb; acp = acb;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) Rp[i] = Rb[i];
+    op = ob; vp = vb; wp = wb;
+  }
+}
+
+__device__ __forceinline__ void mat_to_quat(const float* m, float* q) {
+  float tr = m[0] + m[4] + m[8];
+  if (tr > 0) {
+    float s = sqrtf(tr + 1) * 2;
+    q[3] = 0.25f * s; q[0] = (m[7] - m[5]) / s; q[1] = (m[2] - m[6]) / s; q[2] = (m[3] - m[1]) / s;
+  } else if (m[0] > m[4] && m[0] > m[8]) {
+    float s = sqrtf(1 + m[0] - m[4] - m[8]) * 2;
+    q[3] = (m[7] - m[5]) / s; q[0] = 0.25f * s; q[1] = (m[1] + m[3]) / s; q[2] = (m[2] + m[6]) / s;
+  } else if (m[4] > m[8]) {
+    float s = sqrtf(1 + m[4] - m[0] - m[8]) * 2;
+    q[3] = (m[2] - m[6]) / s; q[0] = (m[1] + m[3]) / s; q[1] = 0.25f * s; q[2] = (m[5] + m[7]) / s;
+  } else {
+    float s = sqrtf(1 + m[8] - m[0] - m[4]) * 2;
+    q[3] = (m[3] - m[1]) / s; q[0] = (m[2] + m[6]) / s; q[1] = (m[5] + m[7]) / s; q[2] = 0.25f * s;
+  }
+  if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+}
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
+  __shared__ EnvSh shm[2];
+  const int half = threadIdx.x >> 5;
+  const int l = threadIdx.x & 31;
+  const int e_raw = blockIdx.x * 2 + half;
+  const bool valid = e_raw < S.n;
+  const int e = valid ? e_raw : S.n - 1;
+  EnvSh& E = shm[half];
+  const hg_cfg* cfg = S.cfg;
+  const hg_model* M = S.model;
+  const int np = S.np;
+  const float dt = cfg->sim_dt;
+  const bool fixed = cfg->fix_base_link != 0;
+  const float gz = cfg->gravity_z;
+
+  // ---------------- prologue: actions (humanoid_env.py:624-635) + state load
+  if (l < 12) {
+    const float delay = u01(rng4(cfg, e, step_counter, 0, RNG_ACT_DELAY).x);
+    float z4[4];
+    normals4(rng4(cfg, e, step_counter, l >> 2, RNG_ACT_NOISE), z4);
+    const float z = z4[l & 3];
+    float a = actions_in[(size_t)e * HG_ND + l];
+    const float prev = S.actions[l * np + e];
+    a = (1.0f - delay) * a + delay * prev;
+    a += cfg->dynamic_randomization * z * a;
+    a = fminf(fmaxf(a, -cfg->clip_actions), cfg->clip_actions);
+    E.act[l] = a;
+    if (valid) S.actions[l * np + e] = a;
+    E.q[l] = S.dof_pos[l * np + e];
+    E.qd[l] = S.dof_vel[l * np + e];
+  }
+  if (l < 13) E.root[l] = S.root[l * np + e];
+  for (int i = l; i < HG_LAMW; i += 32) E.lamst[i] = S.lambda[i * np + e];
+  if (l == 0) {
+    E.mass0 = S.body_mass[e];
+    E.fric = S.friction[e];
+    E.bad = 0;
+  }
+  __syncthreads();
+  const float scale0 = E.mass0 / M->mass[0];
+
+  for (int sub = 0; sub < cfg->decimation; sub++) {
+    // ---- A1: torques (_compute_torques, humanoid_env.py:910-925), generalized velocity
+    if (l < 12) {
+      float t = cfg->kp[l] * (E.act[l] * cfg->action_scale + cfg->default_dof_pos[l] - E.q[l]) - cfg->kd[l] * E.qd[l];
+      E.tau[l] = fminf(fmaxf(t, -cfg->torque_limit[l]), cfg->torque_limit[l]);
+      E.nu[6 + l] = E.qd[l];
+    }
+    if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
+    for (int i = l; i < 18 * 20; i += 32) (&E.u.fac.M[0][0])[i] = 0.f;
+    __syncthreads();
+    // ---- A2/A3: kinematics + RNEA forward
+    kin_local(E, M, l);
+    __syncthreads();
+    if (l < 2) kin_chain(E, M, l, gz, true);
+    if (l == 2) { st3(E.al[0], mk(0, 0, 0)); st3(E.ac[0], mk(0, 0, -gz)); }
+    __syncthreads();
+    // ---- A4: per-body inertia, RNEA forces, composite inertia seeds
+    if (l < 13) {
+      const int b = l;
+      f3 o = ld3(E.o[b]);
+      f3 cb = o + mv3(E.R[b], ld3(M->com[b]));
+      float Iw[6];
+      {
+        const float* I = M->inertia[b];
+        const float* Rm = E.R[b];
+        float Im[9] = {I[0], I[3], I[4], I[3], I[1], I[5], I[4], I[5], I[2]};
+        float T9[9];
+        mm3(Rm, Im, T9);
+        float W9[9];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+          for (int j = 0; j < 3; j++) W9[i * 3 + j] = T9[i * 3] * Rm[j * 3] + T9[i * 3 + 1] * Rm[j * 3 + 1] + T9[i * 3 + 2] * Rm[j * 3 + 2];
+        Iw[0] = W9[0]; Iw[1] = W9[4]; Iw[2] = W9[8]; Iw[3] = W9[1]; Iw[4] = W9[2]; Iw[5] = W9[5];
+      }
+      float mb = M->mass[b];
+      if (b == 0) {
+        mb = E.mass0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) Iw[i] *= scale0;
+      }
+      f3 wb = ld3(E.w[b]), alb = ld3(E.al[b]), acb = ld3(E.ac[b]);
+      f3 d = cb - o;
+      f3 acc = acb + cross(alb, d) + cross(wb, cross(wb, d));
+      f3 fb = mb * acc;
+      f3 nb = symv(Iw, alb) + cross(wb, symv(Iw, wb)) + cross(d, fb);
+      st3(E.c[b], cb); st3(E.f[b], fb); st3(E.n[b], nb);
+#pragma unroll
+      for (int i = 0; i < 6; i++) E.Iw[b][i] = Iw[i];
+      const float cc = dot(cb, cb);
+      E.cm[b] = mb;
+      st3(E.cs[b], mb * cb);
+      E.cJ[b][0] = Iw[0] + mb * (cc - cb.x * cb.x);
+      E.cJ[b][1] = Iw[1] + mb * (cc - cb.y * cb.y);
+      E.cJ[b][2] = Iw[2] + mb * (cc - cb.z * cb.z);
+      E.cJ[b][3] = Iw[3] - mb * cb.x * cb.y;
+      E.cJ[b][4] = Iw[4] - mb * cb.x * cb.z;
+      E.cJ[b][5] = Iw[5] - mb * cb.y * cb.z;
+    }
+    __syncthreads();
+    // ---- A5: backward leg chains (RNEA + composites), joint bias forces
+    if (l < 2) {
+      const int leg = l;
+      f3 fch = mk(0, 0, 0), nch = mk(0, 0, 0), csch = mk(0, 0, 0), och = mk(0, 0, 0);
+      float cmch = 0.f, cJch[6] = {0, 0, 0, 0, 0, 0};
+      for (int k = 5; k >= 0; k--) {
+        const int b = 1 + 6 * leg + k;
+        f3 ob = ld3(E.o[b]);
+        f3 fb = ld3(E.f[b]) + fch;
+        f3 nb = ld3(E.n[b]) + nch + cross(och - ob, fch);
+        float cmb = E.cm[b] + cmch;
+        f3 csb = ld3(E.cs[b]) + csch;
+        float cJb[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) cJb[i] = E.cJ[b][i] + cJch[i];
+        st3(E.f[b], fb); st3(E.n[b], nb);
+        E.cm[b] = cmb; st3(E.cs[b], csb);
+#pragma unroll
+        for (int i = 0; i < 6; i++) E.cJ[b][i] = cJb[i];
+        E.h[5 + b] = dot(ld3(E.a[b]), nb);
+        fch = fb; nch = nb; csch = csb; och = ob; cmch = cmb;
+#pragma unroll
+        for (int i = 0; i < 6; i++) cJch[i] = cJb[i];
+      }
+    }
+    __syncthreads();
+    // ---- A6/A7: base totals + base block (lane 0); joint columns of M (lanes 1..12)
+    if (l == 0) {
+      f3 f0 = ld3(E.f[0]) + ld3(E.f[1]) + ld3(E.f[7]);
+      f3 n0 = ld3(E.n[0]) + ld3(E.n[1]) + cross(ld3(E.o[1]), ld3(E.f[1])) + ld3(E.n[7]) + cross(ld3(E.o[7]), ld3(E.f[7]));
+      E.h[0] = f0.x; E.h[1] = f0.y; E.h[2] = f0.z; E.h[3] = n0.x; E.h[4] = n0.y; E.h[5] = n0.z;
+      const float m0 = E.cm[0] + E.cm[1] + E.cm[7];
+      f3 s = ld3(E.cs[0]) + ld3(E.cs[1]) + ld3(E.cs[7]);
+      float J0[6];
+#pragma unroll
+      for (int i = 0; i < 6; i++) J0[i] = E.cJ[0][i] + E.cJ[1][i] + E.cJ[7][i];
+      float (*A)[20] = E.u.fac.M;
+      A[0][0] = A[1][1] = A[2][2] = m0;
+      A[3][1] = -s.z; A[3][2] = s.y;
+      A[4][0] = s.z;  A[4][2] = -s.x;
+      A[5][0] = -s.y; A[5][1] = s.x;
+      A[3][3] = J0[0]; A[4][4] = J0[1]; A[5][5] = J0[2];
+      A[4][3] = J0[3]; A[5][3] = J0[4]; A[5][4] = J0[5];
+    } else if (l <= 12) {
+      const int b = l, col = 5 + b;
+      f3 a = ld3(E.a[b]), o = ld3(E.o[b]);
+      f3 cs = ld3(E.cs[b]);
+      f3 F = cross(a, cs - E.cm[b] * o);
+      f3 L = symv(E.cJ[b], a) - cross(cs, cross(a, o));
+      float (*A)[20] = E.u.fac.M;
+      A[col][0] = F.x; A[col][1] = F.y; A[col][2] = F.z;
+      A[col][3] = L.x; A[col][4] = L.y; A[col][5] = L.z;
+      const int first = b <= 6 ? 1 : 7;
+      for (int kb = b; kb >= first; kb--) A[col][5 + kb] = dot(ld3(E.a[kb]), L - cross(ld3(E.o[kb]), F));
+      A[col][col] += M->armature[b];
+    }
+    __syncthreads();
+    // ---- A8: Cholesky, rows in parallel (lane i owns row i)
+    const int off = fixed ? 6 : 0;
+    {
+      float (*A)[20] = E.u.fac.M;
+      for (int j = off; j < 18; j++) {
+        if (l == j) {
+          const float d = A[j][j];
+          if (!(d > 0.f)) E.bad = 1;
+          const float sd = sqrtf(fmaxf(d, 1e-20f));
+          A[j][j] = sd;
+          E.u.fac.invd[j] = 1.0f / sd;
+        }
+        __syncthreads();
+        if (l > j && l < 18) A[l][j] *= E.u.fac.invd[j];
+        __syncthreads();
+        if (l > j && l < 18) {
+          const float lij = A[l][j];
+          for (int k = j + 1; k <= l; k++) A[l][k] -= lij * A[k][j];
+        }
+        __syncthreads();
+      }
+    }
+    // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i; stored transposed = row i)
+    if (l < 18) {
+      float y[18];
+#pragma unroll
+      for (int k = 0; k < 18; k++) y[k] = 0.f;
+      if (l >= off) {
+        const float (*A)[20] = E.u.fac.M;
+#pragma unroll
+        for (int k = 0; k < 18; k++) {
+          if (k < off) continue;
+          float s = (k == l) ? 1.f : 0.f;
+#pragma unroll
+          for (int m = 0; m < k; m++) s -= A[k][m] * y[m];
+          y[k] = s * E.u.fac.invd[k];
+        }
+#pragma unroll
+        for (int k = 17; k >= 0; k--) {
+          if (k < off) continue;
+          const float xk = y[k] * E.u.fac.invd[k];
+          y[k] = xk;
+#pragma unroll
+          for (int m = 0; m < k; m++) y[m] -= A[k][m] * xk;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 18; k++) E.u.fac.Minv[k][l] = (k < off) ? 0.f : y[k];
+    }
+    __syncthreads();
+    // ---- A10: unconstrained velocity nu* = nu + dt M^-1 (tau - h)
+    float nu_star = 0.f;
+    if (l < 18) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 18; k++) acc += E.u.fac.Minv[l][k] * ((k >= 6 ? E.tau[k - 6] : 0.f) - E.h[k]);
+      nu_star = E.nu[l] + dt * acc;
+    }
+    __syncthreads();
+    if (l < 18) E.nu[l] = nu_star;
+    // ---- A11: contact / limit detection and row allocation
+    bool act_c = false, act_l = false;
+    f3 cx = mk(0, 0, 0), cn = mk(0, 0, 1);
+    float phi = 0.f, gapv = 0.f, sgnv = 1.f;
+    if (l < 16 && l < M->num_contacts && !fixed) {
+      const int b = M->contact_body[l];
+      cx = ld3(E.o[b]) + mv3(E.R[b], ld3(M->contact_pos[l]));
+      float hg;
+      ground(cfg, cx.x + E.root[0], cx.y + E.root[1], &hg, &cn);
+      phi = (cx.z + E.root[2] - hg) * cn.z;
+      act_c = phi < cfg->contact_offset;
+    } else if (l >= 16 && l < 28) {
+      const int j = l - 16;
+      const float glo = E.q[j] - M->lower[j + 1], ghi = M->upper[j + 1] - E.q[j];
+      if (glo < 0.01f) { act_l = true; gapv = glo; sgnv = 1.f; }
+      else if (ghi < 0.01f) { act_l = true; gapv = ghi; sgnv = -1.f; }
+    }
+    {
+      const uint64_t bal_c = __ballot(act_c), bal_l = __ballot(act_l);
+      const uint32_t mc = (uint32_t)(bal_c >> (32 * half)) & 0xFFFFu;
+      const uint32_t ml = ((uint32_t)(bal_l >> (32 * half)) >> 16) & 0xFFFu;
+      const int nc = min(__popc(mc), RMAX / 3);  // whole (normal, t1, t2) triples only
+      const int nrows = min(RMAX, 3 * nc + __popc(ml));
+      const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
+      if (l == 0) E.nrows = nrows;
+      if (l < 16) {
+        const int rank = __popc(mc & ((1u << l) - 1u));
+        if (act_c && rank < nc) {
+          const int start = 3 * rank;
+          f3 t1 = mk(1, 0, 0) - cn.x * cn;
+          t1 = rsqrtf(dot(t1, t1)) * t1;
+          f3 t2 = cross(cn, t1);
+          const float tgt = phi >= 0.f ? -phi / dt : fminf(-beta * phi / dt, vmax);
+          for (int d = 0; d < 3; d++) {
+            const int r = start + d;
+            f3 dir = d == 0 ? cn : (d == 1 ? t1 : t2);
+            st3(E.rx[r], cx); st3(E.rd[r], dir);
+            E.rKind[r] = d; E.rPt[r] = l; E.rBody[r] = M->contact_body[l];
+            E.rTgt[r] = d == 0 ? tgt : 0.f;
+            E.rLam[r] = E.lamst[l * 3 + d];
+          }
+        } else if (l < HG_NC) {
+          E.lamst[l * 3 + 0] = E.lamst[l * 3 + 1] = E.lamst[l * 3 + 2] = 0.f;
+        }
+      } else if (l < 28) {
+        const int j = l - 16;
+        const int r = 3 * nc + __popc(ml & ((1u << j) - 1u));
+        if (act_l && r < RMAX) {
+          E.rKind[r] = 3; E.rPt[r] = j; E.rBody[r] = -1;
+          E.rd[r][0] = sgnv;
+          E.rTgt[r] = gapv >= 0.f ? -gapv / dt : fminf(-beta * gapv / dt, vmax);
+          E.rLam[r] = E.lamst[HG_NC * 3 + j];
+        } else {
+          E.lamst[HG_NC * 3 + j] = 0.f;
+        }
+      }
+    }
+    __syncthreads();
+    const int nrows = E.nrows;
+    const int nrmax = max(shm[0].nrows, shm[1].nrows);
+    // ---- A12: Jacobian row (registers), Y = M^-1 J^T, D, initial row velocity
+    float J[18];
+#pragma unroll
+    for (int i = 0; i < 18; i++) J[i] = 0.f;
+    float vrow = 0.f, invD = 0.f;
+    const bool own = l < nrows;
+    const int kind = own ? E.rKind[l] : 2;
+    if (own) {
+      if (kind == 3) {
+        const int j = E.rPt[l];
+#pragma unroll
+        for (int jj = 0; jj < 12; jj++) J[6 + jj] = (jj == j) ? E.rd[l][0] : 0.f;
+      } else {
+        const f3 x = ld3(E.rx[l]), d = ld3(E.rd[l]);
+        const int b = E.rBody[l];
+        J[0] = d.x; J[1] = d.y; J[2] = d.z;
+        const f3 xd = cross(x, d);
+        J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
+        const int lo = b >= 7 ? 7 : 1;
+#pragma unroll
+        for (int k = 1; k <= 12; k++) {
+          const bool anc = b != 0 && k >= lo && k <= b && (k <= 6) == (b <= 6);
+          J[5 + k] = anc ? dot(d, cross(ld3(E.a[k]), x - ld3(E.o[k]))) : 0.f;
+        }
+      }
+      float Yr[18];
+#pragma unroll
+      for (int i = 0; i < 18; i++) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 18; k++) s += E.u.fac.Minv[i][k] * J[k];
+        Yr[i] = s;
+      }
+      float D = 0.f, v0 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 18; i++) { D += J[i] * Yr[i]; v0 += J[i] * E.nu[i]; E.Y[l][i] = Yr[i]; }
+      E.rD[l] = D;
+      invD = 1.0f / D;
+      E.rInvD[l] = invD;
+      vrow = v0;
+    }
+    __syncthreads();
+    // ---- A13: Delassus rows W[r][:] = J_r M^-1 J^T (lane r), warm-start row velocities
+    if (own) {
+      float acc = vrow;
+      for (int r2 = 0; r2 < nrows; r2++) {
+        float wv = 0.f;
+#pragma unroll
+        for (int i = 0; i < 18; i++) wv += J[i] * E.Y[r2][i];
+        E.u.W[r2][l] = wv;  // symmetric: W[l][r2] = W[r2][l]
+        acc += wv * E.rLam[r2];
+      }
+      vrow = acc;
+    }
+    __syncthreads();
+    // ---- A14: projected Gauss-Seidel (rows in order; normal, then its tangent pair)
+    {
+      const float mu = 0.5f * (E.fric + cfg->ground_friction);
+      float lam_n = 0.f;  // normal impulse of the contact whose tangent rows follow
+      for (int it = 0; it < cfg->pgs_iterations; it++) {
+        for (int r = 0; r < nrmax; r++) {
+          const bool live = r < nrows;
+          const int kr = live ? E.rKind[r] : 2;
+          const float v_a = readlane_f(vrow, r), v_b = readlane_f(vrow, 32 + r);
+          const float vr = half ? v_b : v_a;
+          float dl0 = 0.f, dl1 = 0.f;
+          if (kr == 0 || kr == 3) {
+            const float lam = E.rLam[r];
+            const float ln = fmaxf(lam + (E.rTgt[r] - vr) * E.rInvD[r], 0.f);
+            dl0 = ln - lam;
+            if (l == 0) E.rLam[r] = ln;
+            if (kr == 0) lam_n = ln;
+          } else if (kr == 1) {
+            const float v2a = readlane_f(vrow, r + 1), v2b = readlane_f(vrow, 32 + r + 1);
+            const float vr2 = half ? v2b : v2a;
+            const float la1 = E.rLam[r], la2 = E.rLam[r + 1];
+            float l1 = la1 - vr * E.rInvD[r], l2 = la2 - vr2 * E.rInvD[r + 1];
+            const float lim = mu * lam_n, nn = sqrtf(l1 * l1 + l2 * l2);
+            if (nn > lim) { const float s = lim / nn; l1 *= s; l2 *= s; }
+            dl0 = l1 - la1;
+            dl1 = l2 - la2;
+            if (l == 0) { E.rLam[r] = l1; E.rLam[r + 1] = l2; }
+          }
+          if (own && live) {
+            vrow += E.u.W[r][l] * dl0;
+            if (kr == 1) vrow += E.u.W[r + 1][l] * dl1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
+    float nu_new = 0.f;
+    if (l < 18) {
+      float s = E.nu[l];
+      for (int r = 0; r < nrows; r++) s += E.Y[r][l] * E.rLam[r];
+      nu_new = s;
+    }
+    for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
+    __syncthreads();
+    if (own) {
+      const float lam = E.rLam[l];
+      if (kind == 3) {
+        E.lamst[HG_NC * 3 + E.rPt[l]] = lam;
+      } else {
+        E.lamst[E.rPt[l] * 3 + kind] = lam;
+        const int b = E.rBody[l];
+        const float s = lam / dt;
+        atomicAdd(&E.cf[b][0], J[0] * s);
+        atomicAdd(&E.cf[b][1], J[1] * s);
+        atomicAdd(&E.cf[b][2], J[2] * s);
+      }
+    }
+    // ---- A16: integrate
+    const bool fin = (l >= 18) || isfinite(nu_new);
+    if ((uint32_t)(__ballot(!fin) >> (32 * half)) != 0u && l == 0) E.bad = 1;
+    __syncthreads();
+    if (l < 18) E.nu[l] = nu_new;
+    __syncthreads();
+    if (l < 12) {
+      E.qd[l] = E.nu[6 + l];
+      E.q[l] += dt * E.qd[l];
+    }
+    if (l == 0) {
+      if (!fixed) {
+        for (int i = 0; i < 3; i++) { E.root[7 + i] = E.nu[i]; E.root[10 + i] = E.nu[3 + i]; E.root[i] += dt * E.nu[i]; }
+        float* Q = E.root + 3;
+        const float wx = E.nu[3], wy = E.nu[4], wz = E.nu[5];
+        const float wn = sqrtf(wx * wx + wy * wy + wz * wz);
+        const float th = wn * dt;
+        if (th > 0.f) {
+          float sh, ch;
+          sincosf(0.5f * th, &sh, &ch);
+          const float s = sh / wn;
+          const float dq0 = wx * s, dq1 = wy * s, dq2 = wz * s, dq3 = ch;
+          const float x = dq3 * Q[0] + dq0 * Q[3] + dq1 * Q[2] - dq2 * Q[1];
+          const float y = dq3 * Q[1] - dq0 * Q[2] + dq1 * Q[3] + dq2 * Q[0];
+          const float z = dq3 * Q[2] + dq0 * Q[1] - dq1 * Q[0] + dq2 * Q[3];
+          const float w = dq3 * Q[3] - dq0 * Q[0] - dq1 * Q[1] - dq2 * Q[2];
+          const float inv = rsqrtf(x * x + y * y + z * z + w * w);
+          Q[0] = x * inv; Q[1] = y * inv; Q[2] = z * inv; Q[3] = w * inv;
+        }
+      } else {
+        for (int i = 7; i < 13; i++) E.root[i] = 0.f;
+      }
+    }
+    __syncthreads();
+    // a non-finite env keeps stepping (NaNs cannot hang the solver: every loop bound is
+    // uniform) and is replaced by the recovery state in the epilogue
+  }
+
+  // ---------------- epilogue: rigid-body states (refresh_rigid_body_state_tensor) + store
+  const bool bad = E.bad != 0;
+  if (l < 6) E.nu[l] = E.root[7 + l];
+  if (l < 12) E.nu[6 + l] = E.qd[l];
+  __syncthreads();
+  kin_local(E, M, l);
+  __syncthreads();
+  if (l < 2) kin_chain(E, M, l, gz, false);
+  __syncthreads();
+  if (!valid) return;
+  if (bad) {
+    // non-finite recovery: keep the pre-step state, push the base below ground so the
+    // termination check resets the env; count the event
+    if (l == 0) {
+      S.nonfinite[e] += 1;
+      S.root[2 * np + e] = -10.f;
+      S.contact[2 * np + e] = 1e3f;
+    }
+    if (l < 12) S.dof_vel[l * np + e] = 0.f;
+    return;
+  }
+  if (l < 13) {
+    const int b = l;
+    float qq[4];
+    mat_to_quat(E.R[b], qq);
+    float* o = S.rigid + (size_t)b * 13 * np + e;
+    o[0 * np] = E.o[b][0] + E.root[0];
+    o[1 * np] = E.o[b][1] + E.root[1];
+    o[2 * np] = E.o[b][2] + E.root[2];
+    o[3 * np] = qq[0]; o[4 * np] = qq[1]; o[5 * np] = qq[2]; o[6 * np] = qq[3];
+    o[7 * np] = E.v[b][0]; o[8 * np] = E.v[b][1]; o[9 * np] = E.v[b][2];
+    o[10 * np] = E.w[b][0]; o[11 * np] = E.w[b][1]; o[12 * np] = E.w[b][2];
+    S.root[b * np + e] = E.root[b];
+  }
+  if (l < 12) {
+    S.dof_pos[l * np + e] = E.q[l];
+    S.dof_vel[l * np + e] = E.qd[l];
+    S.torques[l * np + e] = E.tau[l];
+  }
+  for (int i = l; i < HG_LAMW; i += 32) S.lambda[i * np + e] = E.lamst[i];
+  for (int i = l; i < 13 * 3; i += 32) S.contact[i * np + e] = (&E.cf[0][0])[i];
+}
+
+extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream) {
+  const int grid = (S->n + 1) / 2;
+  hipLaunchKernelGGL(k_step2, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}

@@ -374,6 +374,7 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
   const real beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel, off_c = cfg->contact_offset;
   int body_of_row[MAX_ROWS];
   if (!fixed) {
+    int nct = 0;
     for (int c = 0; c < m->nc; c++) {
       int b = m->cbody[c];
       real x[3];
@@ -383,7 +384,9 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
       real hg, nrm[3];
       ground(cfg, hf, xw[0], xw[1], &hg, nrm);
       real phi = (xw[2] - hg) * nrm[2];
-      if (!(phi < off_c)) { for (int d = 0; d < 3; d++) lamst[c * 3 + d] = 0; continue; }
+      /* at most 10 active contacts (30 rows) in candidate order: feet first, then base */
+      if (!(phi < off_c) || nct >= 10) { for (int d = 0; d < 3; d++) lamst[c * 3 + d] = 0; continue; }
+      nct++;
       /* tangent basis */
       real t1[3], t2[3];
       real ref[3] = {1, 0, 0};
@@ -423,6 +426,7 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
     if (glo < lim_margin) { sgn = 1; gap = glo; }
     else if (ghi < lim_margin) { sgn = -1; gap = ghi; }
     else { lamst[NC_MAX * 3 + j] = 0; continue; }
+    if (nr >= 32) { lamst[NC_MAX * 3 + j] = 0; continue; }  /* at most 32 rows */
     Row* r = &rows[nr];
     r->kind = 3; r->pt = j;
     memset(r->J, 0, sizeof(r->J));

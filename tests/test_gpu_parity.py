@@ -22,6 +22,32 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
+def _make_env(n, version="v2", **over):
+    import os
+    from humanoid.envs import XBotLCfg
+    from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
+    from humanoid.utils.helpers import SimParams
+    os.environ["HG_PHYSICS"] = version
+    torch.manual_seed(5)
+    np.random.seed(5)
+    cfg = XBotLCfg()
+    cfg.env.num_envs = n
+    cfg.seed = 5
+    for k, v in over.items():
+        sec, name = k.split("__")
+        setattr(getattr(cfg, sec), name, v)
+    try:
+        return XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
+    finally:
+        os.environ.pop("HG_PHYSICS", None)
+
+
+@pytest.fixture(scope="module", params=["v2", "v1"])
+def physics_env(request):
+    _need_gpu()
+    return _make_env(N_ENVS, request.param)
+
+
 @pytest.fixture(scope="module")
 def env():
     _need_gpu()
@@ -169,9 +195,11 @@ def _step_only(env, actions, counter):
     torch.cuda.synchronize()
 
 
-def test_step_physics_parity(env):
-    """One K_step (prologue + 10 substeps + rigid states) vs the C reference simulator."""
+def test_step_physics_parity(physics_env):
+    """One K_step (prologue + 10 substeps + rigid states) vs the C reference simulator, for the
+    lane-parallel kernel (v2, default) and the lane-per-env kernel (v1)."""
     import pipeline_ref as PR
+    env = physics_env
     for _ in range(5):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
     S, _, _ = snapshot(env)
@@ -194,38 +222,30 @@ def test_step_physics_parity(env):
         assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
 
 
-def test_trajectory_1000_steps_fixed_base():
+@pytest.mark.parametrize("version", ["v2", "v1"])
+def test_trajectory_1000_steps_fixed_base(version):
     """SURVEY §8d parity trajectory, variant A (fix_base_link): joint angles / torques of the HIP
     path vs the f64 reference simulator over 1000 policy steps (10,000 substeps)."""
     _need_gpu()
-    err_q, err_tau = _run_trajectory(fixed=True, steps=1000)
+    err_q, err_tau = _run_trajectory(fixed=True, steps=1000, version=version)
     assert err_q.max() < 2e-3, err_q.max()
     assert err_tau.max() < 0.5, err_tau.max()
 
 
-def test_trajectory_floating_base():
+@pytest.mark.parametrize("version", ["v2", "v1"])
+def test_trajectory_floating_base(version):
     """Variant B (floating base on the plane): tight agreement over the first 100 steps; the
     contact dynamics then diverge chaotically (fp32 vs fp64), so the rest is reported."""
     _need_gpu()
-    err_q, err_tau = _run_trajectory(fixed=False, steps=300)
+    err_q, err_tau = _run_trajectory(fixed=False, steps=300, version=version)
     assert err_q[:100].max() < 5e-2, err_q[:100].max()
     print("floating-base |dq| max at steps 100/200/300:", err_q[99], err_q[199], err_q[299])
 
 
-def _run_trajectory(fixed, steps):
-    from humanoid.envs import XBotLCfg
-    from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
-    from humanoid.utils.helpers import SimParams
-    import physics_ref as P
+def _run_trajectory(fixed, steps, version="v2"):
     import pipeline_ref as PR
-    cfg = XBotLCfg()
-    cfg.env.num_envs = 16
-    cfg.asset.fix_base_link = fixed
-    cfg.domain_rand.dynamic_randomization = 0.0
-    cfg.domain_rand.push_robots = False
-    cfg.noise.add_noise = False
-    cfg.seed = 5
-    env = XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
+    env = _make_env(16, version, asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
+                    domain_rand__push_robots=False, noise__add_noise=False)
     S, _, _ = snapshot(env)
     oc = _oracle_cfg(env)
     r64 = _ref_sim(env, S, "f64")
