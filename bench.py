@@ -135,7 +135,7 @@ def cpu_baseline(n_envs=256, T=24, threads=None):
     ppo.init_storage(n_envs, T, [705], [219], [12])
     ppo.storage.gae_fn = lambda r, d, v, lv, g, l: tuple(
         torch.from_numpy(x)[..., None] for x in E.gae(r[..., 0].numpy(), d[..., 0].numpy(), v[..., 0].numpy(),
-                                                      lv[:, 0].numpy(), g, l))
+                                                      lv[:, 0].numpy(), g, l, normalize=False))
     t0 = time.time()
     counter = 0
     with torch.inference_mode():

@@ -83,8 +83,17 @@ class RolloutStorage:
 
     def compute_returns(self, last_values, gamma, lam):
         """GAE(gamma, lam) + advantage normalisation (rollout_storage.py:122-143)."""
+        T, Nn = self.num_transitions_per_env, self.num_envs
         if self.gae_fn is not None:
-            self.returns, self.advantages = self.gae_fn(self.rewards, self.dones, self.values, last_values, gamma, lam)
+            # test hook: gae_fn returns (returns, raw advantages); statistics and normalisation
+            # follow the same (distributed) path as the kernel
+            self.returns, raw = self.gae_fn(self.rewards, self.dones, self.values, last_values, gamma, lam)
+            a = raw.double()
+            self._stats = torch.stack([a.sum(), (a * a).sum()])
+            count = self._reduce_stats(T * Nn)
+            mean = self._stats[0] / count
+            std = ((self._stats[1] - self._stats[0] * mean) / (count - 1)).clamp_min(0).sqrt()
+            self.advantages = ((raw - mean.float()) / (std.float() + 1e-8)).float()
             return
         if self.rewards.device.type != "cuda":
             raise RuntimeError("RolloutStorage.compute_returns needs the HIP GAE kernel: storage must live on a "
@@ -92,17 +101,20 @@ class RolloutStorage:
         from humanoid import _native as N
         L = N.lib()
         lv = last_values.detach().reshape(-1).contiguous().float()
-        T, Nn = self.num_transitions_per_env, self.num_envs
         s = ctypes.c_void_p(torch.cuda.current_stream(self.rewards.device).cuda_stream)
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         N.check(L.hg_gae_scan(p(self.rewards), p(self.dones), p(self.values), p(lv), p(self.returns),
                               p(self.advantages), p(self._stats), T, Nn, ctypes.c_float(gamma), ctypes.c_float(lam), 1, s))
-        count = T * Nn
+        count = self._reduce_stats(T * Nn)
+        N.check(L.hg_gae_normalize(p(self.advantages), p(self._stats), ctypes.c_int64(count),
+                                   ctypes.c_int64(T * Nn), s))
+
+    def _reduce_stats(self, count):
+        """All-reduce (sum A, sum A^2) over the data-parallel group; returns the global count."""
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(self._stats)
             count *= dist.get_world_size()
-        N.check(L.hg_gae_normalize(p(self.advantages), p(self._stats), ctypes.c_int64(count),
-                                   ctypes.c_int64(T * Nn), s))
+        return count
 
     def get_statistics(self):
         done = self.dones

@@ -285,9 +285,10 @@ def stack(history, frame, reset=None):
 
 
 # ------------------------------------------------------------------------------------------ GAE
-def gae(rewards, dones, values, last_values, gamma, lam):
+def gae(rewards, dones, values, last_values, gamma, lam, normalize=True):
     """RolloutStorage.compute_returns (rollout_storage.py:122-143), float32 in the reference's
-    op order.  rewards/dones/values [T,N], last_values [N] -> (returns, normalised advantages)."""
+    op order.  rewards/dones/values [T,N], last_values [N] -> (returns, normalised advantages);
+    normalize=False returns the raw advantages (returns - values)."""
     T = rewards.shape[0]
     g, l = f32(gamma), f32(lam)
     adv = np.zeros(rewards.shape[1], f32)
@@ -299,6 +300,8 @@ def gae(rewards, dones, values, last_values, gamma, lam):
         adv = delta + ((nnt * g) * l) * adv
         ret[t] = adv + values[t]
     a = (ret - values).astype(f32)
+    if not normalize:
+        return ret, a
     a64 = a.astype(np.float64)
     mean = a64.mean()
     std = a64.std(ddof=1)

@@ -1,0 +1,192 @@
+"""Analytic known-answer tests for the CPU reference simulator (oracle/physics_ref.c).
+
+PhysX is unavailable, so physics parity against the reference is unpinned; these checks pin the
+oracle's mechanics to first principles instead: mass matrix symmetric positive
+definite and consistent with the bodies' kinetic energy, free fall, momentum conservation in
+flight, energy conservation without actuation, and static support ≈ m·g."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import physics_ref as P
+from humanoid import _native as N
+
+G = 9.81
+
+
+def quat_R(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+@pytest.fixture(scope="module")
+def model():
+    m, js = N.load_model(armature=0.0)
+    return m, js
+
+
+def make_cfg(n, gz=-9.81, kp=0.0, kd=0.0, fixed=False, pgs=6):
+    c = N.HgCfg()
+    c.num_envs, c.decimation, c.pgs_iterations, c.fix_base_link = n, 1, pgs, int(fixed)
+    c.sim_dt, c.gravity_z, c.contact_offset, c.max_depenetration_vel = 0.001, gz, 0.01, 1.0
+    c.baumgarte, c.ground_friction, c.action_scale = 0.2, 0.6, 0.25
+    for j in range(12):
+        c.kp[j], c.kd[j], c.torque_limit[j] = kp, kd, 1e6
+    return c
+
+
+def body_energy(m, js, rigid, mass0=None, gz=-9.81):
+    """Kinetic and potential energy from per-body states (independent of M)."""
+    ke = pe = 0.0
+    for b, bd in enumerate(js["bodies"]):
+        s = rigid[b]
+        R = quat_R(s[3:7])
+        mb = bd["mass"] if (b > 0 or mass0 is None) else mass0
+        r = R @ np.array(bd["com"])
+        c = s[0:3] + r
+        w = s[10:13]
+        vc = s[7:10] + np.cross(w, r)
+        I = np.array(bd["inertia"])
+        Ib = np.array([[I[0], I[3], I[4]], [I[3], I[1], I[5]], [I[4], I[5], I[2]]])
+        Iw = R @ Ib @ R.T
+        ke += 0.5 * mb * vc @ vc + 0.5 * w @ Iw @ w
+        pe += -mb * gz * c[2]
+    return ke, pe
+
+
+def momentum(js, rigid):
+    p = np.zeros(3)
+    L = np.zeros(3)
+    mtot = 0.0
+    cs = []
+    for b, bd in enumerate(js["bodies"]):
+        s = rigid[b]
+        R = quat_R(s[3:7])
+        r = R @ np.array(bd["com"])
+        c = s[0:3] + r
+        vc = s[7:10] + np.cross(s[10:13], r)
+        cs.append((bd["mass"], c, vc, R, s[10:13], bd["inertia"]))
+        p += bd["mass"] * vc
+        mtot += bd["mass"]
+    com = sum(m * c for m, c, *_ in cs) / mtot
+    for mb, c, vc, R, w, I in cs:
+        Ib = np.array([[I[0], I[3], I[4]], [I[3], I[1], I[5]], [I[4], I[5], I[2]]])
+        L += mb * np.cross(c - com, vc) + R @ Ib @ R.T @ w
+    return p, L
+
+
+def random_state(rng, n, z=2.0):
+    root = np.zeros((n, 13))
+    q = rng.normal(size=(n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    root[:, 2] = z
+    root[:, 3:7] = q
+    root[:, 7:13] = rng.normal(size=(n, 6)) * 0.5
+    return root, rng.uniform(-0.4, 0.4, (n, 12)), rng.normal(size=(n, 12))
+
+
+def test_mass_matrix_spd(model):
+    m, js = model
+    rng = np.random.default_rng(0)
+    root, q, qd = random_state(rng, 5)
+    for e in range(5):
+        M, h = P.dynamics(m, root[e], q[e], qd[e])
+        assert np.abs(M - M.T).max() < 1e-12
+        assert np.linalg.eigvalsh(M).min() > 0
+        np.testing.assert_allclose(M[0, 0], js["total_mass"], rtol=1e-6)   # base linear block = m I
+
+
+def test_kinetic_energy_matches_bodies(model):
+    """0.5 nu^T M nu equals the sum of body kinetic energies computed from the rigid states."""
+    m, js = model
+    rng = np.random.default_rng(1)
+    n = 4
+    cfg = make_cfg(n, gz=0.0)
+    cfg.sim_dt = 1e-9   # effectively freeze the state; rigid states reflect the initial state
+    sim = P.RefSim(cfg, m, n)
+    root, q, qd = random_state(rng, n, z=5.0)
+    sim.root[:], sim.q[:], sim.qd[:] = root, q, qd
+    sim.step(np.zeros((n, 12)))
+    for e in range(n):
+        M, _ = P.dynamics(m, sim.root[e], sim.q[e], sim.qd[e], gz=0.0)
+        nu = np.concatenate([sim.root[e, 7:13], sim.qd[e]])
+        ke, _ = body_energy(m, js, sim.rigid[e])
+        np.testing.assert_allclose(0.5 * nu @ M @ nu, ke, rtol=1e-7)
+
+
+def test_free_fall(model):
+    m, js = model
+    n = 2
+    cfg = make_cfg(n)
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 10.0
+    for k in range(100):
+        sim.step(np.zeros((n, 12)))
+    t = 100 * 0.001
+    np.testing.assert_allclose(sim.root[:, 9], -G * t, rtol=1e-6)  # g is a float32 config value
+    np.testing.assert_allclose(sim.root[:, 2], 10.0 - G * 0.001 ** 2 * 100 * 101 / 2, rtol=1e-7)
+    assert np.abs(sim.q).max() < 1e-9 and np.abs(sim.root[:, 10:13]).max() < 1e-9
+
+
+def test_momentum_conservation_in_flight(model):
+    m, js = model
+    rng = np.random.default_rng(2)
+    n = 4
+    cfg = make_cfg(n, gz=0.0)
+    sim = P.RefSim(cfg, m, n)
+    root, q, qd = random_state(rng, n, z=10.0)
+    sim.root[:], sim.q[:], sim.qd[:] = root, q, qd * 0.5
+    sim.step(np.zeros((n, 12)))
+    p0 = [momentum(js, sim.rigid[e]) for e in range(n)]
+    for _ in range(200):
+        sim.step(np.zeros((n, 12)))
+    for e in range(n):
+        p1, L1 = momentum(js, sim.rigid[e])
+        np.testing.assert_allclose(p1, p0[e][0], rtol=1e-3, atol=1e-3)   # no external force; O(dt) integrator drift
+        np.testing.assert_allclose(L1, p0[e][1], rtol=5e-3, atol=5e-3)   # semi-implicit Euler drift
+
+
+def test_energy_conservation_fixed_base(model):
+    """Unactuated fixed-base swing under gravity with joint limits removed (no constraint
+    impulses): total energy is conserved up to the integrator's O(dt) error."""
+    m, js = model
+    free = N.HgModel.from_buffer_copy(m)
+    for b in range(1, 13):
+        free.lower[b], free.upper[b] = -100.0, 100.0
+    rng = np.random.default_rng(3)
+    n = 3
+    cfg = make_cfg(n, fixed=True)
+    sim = P.RefSim(cfg, free, n)
+    sim.root[:, 2] = 3.0
+    sim.q[:] = rng.uniform(-0.5, 0.5, (n, 12))
+    sim.step(np.zeros((n, 12)))
+    e0 = np.array([sum(body_energy(m, js, sim.rigid[e])) for e in range(n)])
+    swing = np.zeros(n)
+    for _ in range(500):
+        sim.step(np.zeros((n, 12)))
+        for e in range(n):
+            swing[e] = max(swing[e], body_energy(m, js, sim.rigid[e])[0])
+    e1 = np.array([sum(body_energy(m, js, sim.rigid[e])) for e in range(n)])
+    assert (swing > 0.5).all()                      # it really swings
+    assert (np.abs(e1 - e0) < 0.03 * swing).all(), (e1 - e0, swing)   # semi-implicit Euler: bounded O(dt) error
+
+
+def test_static_support_equals_weight():
+    m, js = N.load_model(armature=0.01)   # the product's armature (explicit kd=10 on the bare foot is unstable)
+    n = 2
+    cfg = make_cfg(n, kp=0.0)
+    for j in range(12):
+        cfg.kp[j] = [200, 200, 350, 350, 15, 15][j % 6]
+        cfg.kd[j] = 10.0
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 0.90
+    sim.fric[:] = 1.0
+    for _ in range(300):
+        sim.step(np.zeros((n, 12)))
+    fz = sim.contact[:, 6, 2] + sim.contact[:, 12, 2] + sim.contact[:, 0, 2]
+    np.testing.assert_allclose(fz, js["total_mass"] * G, rtol=0.05)
+    sole_z = sim.rigid[:, 6, 2]
+    assert (sole_z > 0.03).all()          # no deep penetration (sole is 0.056 below the foot frame)
