@@ -17,6 +17,24 @@
 // Replaces humanoid_env.py:620-649 (+ refreshes :776-778), like v1.
 #include "hg_common.h"
 
+#ifdef HG_STAMPS
+// diagnostic build only (libhgsim_stamps.so): per-phase cycle accumulators, lane 0 of each block
+__device__ unsigned long long g_hg_stamps[32];
+#define STAMP_DECL unsigned long long st_acc[20] = {0}; unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(k) do { __builtin_amdgcn_s_waitcnt(0xC07F); unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+  st_acc[k] += _t - st_prev; st_prev = _t; } while (0)
+#define STAMP_FLUSH() do { if (threadIdx.x == 0) for (int _k = 0; _k < 20; _k++) atomicAdd(&g_hg_stamps[_k], st_acc[_k]); } while (0)
+extern "C" int hg_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hg_stamps), sizeof(unsigned long long) * 32) != hipSuccess) return 1;
+  if (reset) { unsigned long long z[32] = {0}; hipMemcpyToSymbol(HIP_SYMBOL(g_hg_stamps), z, sizeof(z)); }
+  return 0;
+}
+#else
+#define STAMP_DECL
+#define STAMP(k) do {} while (0)
+#define STAMP_FLUSH() do {} while (0)
+#endif
+
 namespace {
 
 constexpr int RMAX = 32;
@@ -179,6 +197,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
   const bool fixed = cfg->fix_base_link != 0;
   const float gz = cfg->gravity_z;
 
+  STAMP_DECL
   // ---------------- prologue: actions (humanoid_env.py:624-635) + state load
   if (l < 12) {
     const float delay = u01(rng4(cfg, e, step_counter, 0, RNG_ACT_DELAY).x);
@@ -206,6 +225,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
   const float scale0 = E.mass0 / M->mass[0];
 
   for (int sub = 0; sub < cfg->decimation; sub++) {
+    STAMP(0);
     // ---- A1: torques (_compute_torques, humanoid_env.py:910-925), generalized velocity
     if (l < 12) {
       float t = cfg->kp[l] * (E.act[l] * cfg->action_scale + cfg->default_dof_pos[l] - E.q[l]) - cfg->kd[l] * E.qd[l];
@@ -215,12 +235,14 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
     if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
     for (int i = l; i < 18 * 20; i += 32) (&E.u.fac.M[0][0])[i] = 0.f;
     __syncthreads();
+    STAMP(1);
     // ---- A2/A3: kinematics + RNEA forward
     kin_local(E, M, l);
     __syncthreads();
     if (l < 2) kin_chain(E, M, l, gz, true);
     if (l == 2) { st3(E.al[0], mk(0, 0, 0)); st3(E.ac[0], mk(0, 0, -gz)); }
     __syncthreads();
+    STAMP(2);
     // ---- A4: per-body inertia, RNEA forces, composite inertia seeds
     if (l < 13) {
       const int b = l;
@@ -265,6 +287,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       E.cJ[b][5] = Iw[5] - mb * cb.y * cb.z;
     }
     __syncthreads();
+    STAMP(3);
     // ---- A5: backward leg chains (RNEA + composites), joint bias forces
     if (l < 2) {
       const int leg = l;
@@ -291,6 +314,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       }
     }
     __syncthreads();
+    STAMP(4);
     // ---- A6/A7: base totals + base block (lane 0); joint columns of M (lanes 1..12)
     if (l == 0) {
       f3 f0 = ld3(E.f[0]) + ld3(E.f[1]) + ld3(E.f[7]);
@@ -322,6 +346,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       A[col][col] += M->armature[b];
     }
     __syncthreads();
+    STAMP(5);
     // ---- A8: Cholesky, rows in parallel (lane i owns row i)
     const int off = fixed ? 6 : 0;
     {
@@ -344,6 +369,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
         __syncthreads();
       }
     }
+    STAMP(6);
     // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i; stored transposed = row i)
     if (l < 18) {
       float y[18];
@@ -372,6 +398,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       for (int k = 0; k < 18; k++) E.u.fac.Minv[k][l] = (k < off) ? 0.f : y[k];
     }
     __syncthreads();
+    STAMP(7);
     // ---- A10: unconstrained velocity nu* = nu + dt M^-1 (tau - h)
     float nu_star = 0.f;
     if (l < 18) {
@@ -382,6 +409,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
     }
     __syncthreads();
     if (l < 18) E.nu[l] = nu_star;
+    STAMP(8);
     // ---- A11: contact / limit detection and row allocation
     bool act_c = false, act_l = false;
     f3 cx = mk(0, 0, 0), cn = mk(0, 0, 1);
@@ -442,6 +470,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
     __syncthreads();
     const int nrows = E.nrows;
     const int nrmax = max(shm[0].nrows, shm[1].nrows);
+    STAMP(9);
     // ---- A12: Jacobian row (registers), Y = M^-1 J^T, D, initial row velocity
     float J[18];
 #pragma unroll
@@ -484,6 +513,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       vrow = v0;
     }
     __syncthreads();
+    STAMP(10);
     // ---- A13: Delassus rows W[r][:] = J_r M^-1 J^T (lane r), warm-start row velocities
     if (own) {
       float acc = vrow;
@@ -497,6 +527,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       vrow = acc;
     }
     __syncthreads();
+    STAMP(11);
     // ---- A14: projected Gauss-Seidel (rows in order; normal, then its tangent pair)
     {
       const float mu = 0.5f * (E.fric + cfg->ground_friction);
@@ -533,6 +564,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       }
     }
     __syncthreads();
+    STAMP(12);
     // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
     float nu_new = 0.f;
     if (l < 18) {
@@ -555,6 +587,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
         atomicAdd(&E.cf[b][2], J[2] * s);
       }
     }
+    STAMP(13);
     // ---- A16: integrate
     const bool fin = (l >= 18) || isfinite(nu_new);
     if ((uint32_t)(__ballot(!fin) >> (32 * half)) != 0u && l == 0) E.bad = 1;
@@ -589,6 +622,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       }
     }
     __syncthreads();
+    STAMP(14);
     // a non-finite env keeps stepping (NaNs cannot hang the solver: every loop bound is
     // uniform) and is replaced by the recovery state in the epilogue
   }
@@ -602,6 +636,8 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
   __syncthreads();
   if (l < 2) kin_chain(E, M, l, gz, false);
   __syncthreads();
+  STAMP(15);
+  STAMP_FLUSH();
   if (!valid) return;
   if (bad) {
     // non-finite recovery: keep the pre-step state, push the base below ground so the

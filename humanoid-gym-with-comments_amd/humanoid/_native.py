@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "csrc", "libhgsim.so")
+LIB_PATH = os.environ.get("HG_LIB") or os.path.join(PKG_ROOT, "csrc", "libhgsim.so")  # HG_LIB: diagnostic builds
 MODEL_PATH = os.path.join(PKG_ROOT, "model", "xbotl_model.json")
 
 HG_MAX_BODIES = 16
