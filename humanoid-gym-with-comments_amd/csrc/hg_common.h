@@ -21,8 +21,8 @@ struct HgState {
   float* root;        // [13][np]
   float* dof_pos;     // [12][np]
   float* dof_vel;     // [12][np]
-  float* contact;     // [13*3][np]
-  float* rigid;       // [13*13][np]
+  float* contact;     // [n][13][3]  AoS (reference layout, coalesced per-env stores from K_step)
+  float* rigid;       // [n][13][13] AoS
   float* torques;     // [12][np]
   float* actions;     // [12][np]
   float* last_actions;
@@ -57,6 +57,9 @@ struct HgState {
   const hg_cfg* cfg;      // device copy
   const hg_model* model;  // device copy
 };
+
+#define HG_CF(S, e, b, i) ((S).contact[(size_t)(e) * (HG_NB * 3) + (b) * 3 + (i)])
+#define HG_RS(S, e, b, f) ((S).rigid[(size_t)(e) * (HG_NB * 13) + (b) * 13 + (f)])
 
 // ------------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. SC'11).  Keyed by the run seed; counter = (a, b, c, purpose).

@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(256) k_post(HgState S, uint64_t counter, int m
       S.root[10 * np + e] = t0; S.root[11 * np + e] = t1; S.root[12 * np + e] = t2;
     }
     // ---- check_termination
-    f3 fb = mk(S.contact[0 * np + e], S.contact[1 * np + e], S.contact[2 * np + e]);
+    f3 fb = mk(HG_CF(S, e, 0, 0), HG_CF(S, e, 0, 1), HG_CF(S, e, 0, 2));
     float fbn = sqrtf(dot(fb, fb));
     bool timeout = ep > (int64_t)cfg->max_episode_length;
     do_reset = (fbn > 1.0f) || timeout;
@@ -187,8 +187,8 @@ __global__ void __launch_bounds__(256) k_post(HgState S, uint64_t counter, int m
     Gait g = gait(cfg, ep);
     const int f0 = cfg->feet_body[0], f1 = cfg->feet_body[1];
     const int k0 = cfg->knee_body[0], k1 = cfg->knee_body[1];
-    auto rig = [&](int b, int f) { return S.rigid[((size_t)b * 13 + f) * np + e]; };
-    auto cfz = [&](int b, int i) { return S.contact[((size_t)b * 3 + i) * np + e]; };
+    auto rig = [&](int b, int f) { return HG_RS(S, e, b, f); };
+    auto cfz = [&](int b, int i) { return HG_CF(S, e, b, i); };
     bool contact[2] = {cfz(f0, 2) > 5.f, cfz(f1, 2) > 5.f};
     float term[HG_NUM_REWARDS];
     // 0 action_smoothness
@@ -365,8 +365,8 @@ __global__ void __launch_bounds__(256) k_post(HgState S, uint64_t counter, int m
       for (int j = 0; j < HG_ND; j++) ref[j] = 0.f;
     for (int j = 0; j < HG_ND; j++) S.ref_dof_pos[j * np + e] = ref[j];
     const int f0 = cfg->feet_body[0], f1 = cfg->feet_body[1];
-    float cm0 = S.contact[((size_t)f0 * 3 + 2) * np + e] > 5.f ? 1.f : 0.f;
-    float cm1 = S.contact[((size_t)f1 * 3 + 2) * np + e] > 5.f ? 1.f : 0.f;
+    float cm0 = HG_CF(S, e, f0, 2) > 5.f ? 1.f : 0.f;
+    float cm1 = HG_CF(S, e, f1, 2) > 5.f ? 1.f : 0.f;
     float c0 = S.commands[0 * np + e] * cfg->obs_lin_vel, c1 = S.commands[1 * np + e] * cfg->obs_lin_vel;
     float c2 = S.commands[2 * np + e] * cfg->obs_ang_vel;
     float* P = frame_priv + (size_t)e * HG_PRIV1;

@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(64) k_step(HgState S, const float* __restrict_
     S.torques[j * np + e] = tau[j];
   }
   for (int i = 0; i < HG_LAMW; i++) S.lambda[i * np + e] = lam[i];
-  for (int i = 0; i < HG_NB * 3; i++) S.contact[i * np + e] = cf[i];
+  for (int i = 0; i < HG_NB * 3; i++) S.contact[(size_t)e * (HG_NB * 3) + i] = cf[i];
   // ---- rigid body states (refresh_rigid_body_state_tensor)
   {
     float nu[HG_NV];
@@ -492,13 +492,13 @@ __global__ void __launch_bounds__(64) k_step(HgState S, const float* __restrict_
     for (int b = 0; b < HG_NB; b++) {
       float qq[4];
       mat_to_quat(k.R[b], qq);
-      float* o = S.rigid + (size_t)b * 13 * np + e;
-      o[0 * np] = k.o[b].x + root[0];
-      o[1 * np] = k.o[b].y + root[1];
-      o[2 * np] = k.o[b].z + root[2];
-      o[3 * np] = qq[0]; o[4 * np] = qq[1]; o[5 * np] = qq[2]; o[6 * np] = qq[3];
-      o[7 * np] = k.v[b].x; o[8 * np] = k.v[b].y; o[9 * np] = k.v[b].z;
-      o[10 * np] = k.w[b].x; o[11 * np] = k.w[b].y; o[12 * np] = k.w[b].z;
+      float* o = &HG_RS(S, e, b, 0);
+      o[0] = k.o[b].x + root[0];
+      o[1] = k.o[b].y + root[1];
+      o[2] = k.o[b].z + root[2];
+      o[3] = qq[0]; o[4] = qq[1]; o[5] = qq[2]; o[6] = qq[3];
+      o[7] = k.v[b].x; o[8] = k.v[b].y; o[9] = k.v[b].z;
+      o[10] = k.w[b].x; o[11] = k.w[b].y; o[12] = k.w[b].z;
     }
   }
 }

@@ -10,9 +10,10 @@
 //     one constraint row per lane (<= 32 rows: sole/base contact normals+tangents, joint
 //     limits) with its Jacobian row held in the lane's registers; the Delassus matrix
 //     W = J M^-1 J^T one row per lane.
-//   * Projected Gauss-Seidel on W: lane r keeps row velocity v_r = J_r nu in a register; a row
-//     update reads v_r with v_readlane (no cross-lane reductions) and applies W[r][:] dlambda
-//     as one FMA per lane.  Gauss-Seidel order (normal, then the tangent pair, row by row) is
+//   * Projected Gauss-Seidel entirely in registers: lane r keeps the row velocity v_r = J_r nu
+//     and its Delassus row W[r][0..31]; every lane of an env keeps a copy of the 32 impulses;
+//     a row update reads v_r with v_readlane (no cross-lane reductions) and applies
+//     W[:][r] dlambda as one FMA per lane; the row loop is unrolled so all indices are static.  Gauss-Seidel order (normal, then the tangent pair, row by row) is
 //     the oracle's, so the PGS iterates are the same sequence as physics_ref.c.
 // Replaces humanoid_env.py:620-649 (+ refreshes :776-778), like v1.
 #include "hg_common.h"
@@ -39,6 +40,11 @@ namespace {
 
 constexpr int RMAX = 32;
 
+struct RowC {  // per-row constants of the PGS, one 16-byte broadcast read
+  float tgt, invD, invD2;  // target velocity, 1/W_rr, 1/W_(r+1)(r+1) (tangent pair partner)
+  int kind;                // 0 normal, 1 tangent-1 (pair head), 2 tangent-2, 3 joint limit
+};
+
 struct __align__(16) EnvSh {
   float root[16];
   float q[12], qd[12], act[12], tau[12];
@@ -46,20 +52,21 @@ struct __align__(16) EnvSh {
   float h[20];
   float lamst[64];
   float R[13][9];
-  float Lr[13][9];
   float axp[13][3];  // joint axis in the parent-body frame (jrot * axis)
-  float o[13][3], a[13][3], c[13][3], w[13][3], v[13][3], al[13][3], ac[13][3], f[13][3], n[13][3];
-  float Iw[13][6];
+  float o[13][3], a[13][3], w[13][3], v[13][3];
   float cm[13], cs[13][3], cJ[13][6];
   union {
-    struct { float M[18][20]; float Minv[18][20]; float invd[20]; } fac;
-    float W[RMAX][RMAX];
+    struct { float Lr[13][9]; float al[13][3], ac[13][3], f[13][3], n[13][3]; } kin;  // A2..A5 scratch
+    struct { float M[18][20]; float Minv[18][20]; float invd[20]; } fac;                 // A6..A12
+    struct { float rigid[13 * 13]; float cf[13 * 3]; } out;                              // epilogue staging
   } u;
   float Y[RMAX][18];
-  float rD[RMAX], rInvD[RMAX], rTgt[RMAX], rLam[RMAX];
+  RowC rc[RMAX];
+  float rLam[RMAX];
   float rx[RMAX][3], rd[RMAX][3];   // row geometry: point (base-centred) and direction
-  int rKind[RMAX], rPt[RMAX], rBody[RMAX];
+  int rPt[RMAX], rBody[RMAX];
   float cf[13][3];
+  float base_f[6], base_cm, base_cs[3], base_cJ[6];
   float mass0, fric;
   int nrows, bad;
 };
@@ -112,7 +119,7 @@ __device__ void kin_local(EnvSh& E, const hg_model* M, int l) {
     Rq[0] = c + k.x * k.x * vv;       Rq[1] = k.x * k.y * vv - k.z * s; Rq[2] = k.x * k.z * vv + k.y * s;
     Rq[3] = k.y * k.x * vv + k.z * s; Rq[4] = c + k.y * k.y * vv;       Rq[5] = k.y * k.z * vv - k.x * s;
     Rq[6] = k.z * k.x * vv - k.y * s; Rq[7] = k.z * k.y * vv + k.x * s; Rq[8] = c + k.z * k.z * vv;
-    mm3(M->joint_rot[b], Rq, E.Lr[b]);
+    mm3(M->joint_rot[b], Rq, E.u.kin.Lr[b]);
     st3(E.axp[b], mv3(M->joint_rot[b], k));
   } else if (l == 0) {
     const float x = E.root[3], y = E.root[4], z = E.root[5], w = E.root[6];
@@ -136,7 +143,7 @@ __device__ void kin_chain(EnvSh& E, const hg_model* M, int leg, float gz, bool b
   for (int k = 0; k < 6; k++) {
     const int b = 1 + 6 * leg + k;
     float Rb[9];
-    mm3(Rp, E.Lr[b], Rb);
+    mm3(Rp, E.u.kin.Lr[b], Rb);
     f3 ob = op + mv3(Rp, ld3(M->joint_pos[b]));
     f3 ab = mv3(Rp, ld3(E.axp[b]));
     const float qd = E.nu[5 + b];
@@ -149,7 +156,7 @@ __device__ void kin_chain(EnvSh& E, const hg_model* M, int leg, float gz, bool b
     if (bias) {
       f3 alb = alp + cross(wp, qd * ab);
       f3 acb = acp + cross(alp, r) + cross(wp, cross(wp, r));
-      st3(E.al[b], alb); st3(E.ac[b], acb);
+      st3(E.u.kin.al[b], alb); st3(E.u.kin.ac[b], acb);
       alp = alb; acp = acb;
     }
 #pragma unroll
@@ -182,7 +189,7 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 
 }  // namespace
 
-__global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_step2(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
   __shared__ EnvSh shm[2];
   const int half = threadIdx.x >> 5;
   const int l = threadIdx.x & 31;
@@ -196,8 +203,8 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
   const float dt = cfg->sim_dt;
   const bool fixed = cfg->fix_base_link != 0;
   const float gz = cfg->gravity_z;
-
   STAMP_DECL
+
   // ---------------- prologue: actions (humanoid_env.py:624-635) + state load
   if (l < 12) {
     const float delay = u01(rng4(cfg, e, step_counter, 0, RNG_ACT_DELAY).x);
@@ -223,6 +230,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
   }
   __syncthreads();
   const float scale0 = E.mass0 / M->mass[0];
+  const int off = fixed ? 6 : 0;
 
   for (int sub = 0; sub < cfg->decimation; sub++) {
     STAMP(0);
@@ -233,14 +241,13 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       E.nu[6 + l] = E.qd[l];
     }
     if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
-    for (int i = l; i < 18 * 20; i += 32) (&E.u.fac.M[0][0])[i] = 0.f;
     __syncthreads();
     STAMP(1);
     // ---- A2/A3: kinematics + RNEA forward
     kin_local(E, M, l);
     __syncthreads();
     if (l < 2) kin_chain(E, M, l, gz, true);
-    if (l == 2) { st3(E.al[0], mk(0, 0, 0)); st3(E.ac[0], mk(0, 0, -gz)); }
+    if (l == 2) { st3(E.u.kin.al[0], mk(0, 0, 0)); st3(E.u.kin.ac[0], mk(0, 0, -gz)); }
     __syncthreads();
     STAMP(2);
     // ---- A4: per-body inertia, RNEA forces, composite inertia seeds
@@ -268,14 +275,12 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
 #pragma unroll
         for (int i = 0; i < 6; i++) Iw[i] *= scale0;
       }
-      f3 wb = ld3(E.w[b]), alb = ld3(E.al[b]), acb = ld3(E.ac[b]);
+      f3 wb = ld3(E.w[b]), alb = ld3(E.u.kin.al[b]), acb = ld3(E.u.kin.ac[b]);
       f3 d = cb - o;
       f3 acc = acb + cross(alb, d) + cross(wb, cross(wb, d));
       f3 fb = mb * acc;
       f3 nb = symv(Iw, alb) + cross(wb, symv(Iw, wb)) + cross(d, fb);
-      st3(E.c[b], cb); st3(E.f[b], fb); st3(E.n[b], nb);
-#pragma unroll
-      for (int i = 0; i < 6; i++) E.Iw[b][i] = Iw[i];
+      st3(E.u.kin.f[b], fb); st3(E.u.kin.n[b], nb);
       const float cc = dot(cb, cb);
       E.cm[b] = mb;
       st3(E.cs[b], mb * cb);
@@ -296,14 +301,14 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       for (int k = 5; k >= 0; k--) {
         const int b = 1 + 6 * leg + k;
         f3 ob = ld3(E.o[b]);
-        f3 fb = ld3(E.f[b]) + fch;
-        f3 nb = ld3(E.n[b]) + nch + cross(och - ob, fch);
+        f3 fb = ld3(E.u.kin.f[b]) + fch;
+        f3 nb = ld3(E.u.kin.n[b]) + nch + cross(och - ob, fch);
         float cmb = E.cm[b] + cmch;
         f3 csb = ld3(E.cs[b]) + csch;
         float cJb[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) cJb[i] = E.cJ[b][i] + cJch[i];
-        st3(E.f[b], fb); st3(E.n[b], nb);
+        st3(E.u.kin.f[b], fb); st3(E.u.kin.n[b], nb);
         E.cm[b] = cmb; st3(E.cs[b], csb);
 #pragma unroll
         for (int i = 0; i < 6; i++) E.cJ[b][i] = cJb[i];
@@ -314,17 +319,27 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       }
     }
     __syncthreads();
-    STAMP(4);
-    // ---- A6/A7: base totals + base block (lane 0); joint columns of M (lanes 1..12)
+    // base totals (lane 0) — read the kinematics scratch before M overwrites it
     if (l == 0) {
-      f3 f0 = ld3(E.f[0]) + ld3(E.f[1]) + ld3(E.f[7]);
-      f3 n0 = ld3(E.n[0]) + ld3(E.n[1]) + cross(ld3(E.o[1]), ld3(E.f[1])) + ld3(E.n[7]) + cross(ld3(E.o[7]), ld3(E.f[7]));
+      f3 f0 = ld3(E.u.kin.f[0]) + ld3(E.u.kin.f[1]) + ld3(E.u.kin.f[7]);
+      f3 n0 = ld3(E.u.kin.n[0]) + ld3(E.u.kin.n[1]) + cross(ld3(E.o[1]), ld3(E.u.kin.f[1])) + ld3(E.u.kin.n[7]) +
+              cross(ld3(E.o[7]), ld3(E.u.kin.f[7]));
       E.h[0] = f0.x; E.h[1] = f0.y; E.h[2] = f0.z; E.h[3] = n0.x; E.h[4] = n0.y; E.h[5] = n0.z;
-      const float m0 = E.cm[0] + E.cm[1] + E.cm[7];
+      E.base_cm = E.cm[0] + E.cm[1] + E.cm[7];
       f3 s = ld3(E.cs[0]) + ld3(E.cs[1]) + ld3(E.cs[7]);
-      float J0[6];
+      st3(E.base_cs, s);
 #pragma unroll
-      for (int i = 0; i < 6; i++) J0[i] = E.cJ[0][i] + E.cJ[1][i] + E.cJ[7][i];
+      for (int i = 0; i < 6; i++) E.base_cJ[i] = E.cJ[0][i] + E.cJ[1][i] + E.cJ[7][i];
+    }
+    __syncthreads();
+    for (int i = l; i < 18 * 20; i += 32) (&E.u.fac.M[0][0])[i] = 0.f;
+    __syncthreads();
+    STAMP(4);
+    // ---- A6/A7: base block (lane 0); joint columns of M (lanes 1..12)
+    if (l == 0) {
+      const float m0 = E.base_cm;
+      f3 s = ld3(E.base_cs);
+      const float* J0 = E.base_cJ;
       float (*A)[20] = E.u.fac.M;
       A[0][0] = A[1][1] = A[2][2] = m0;
       A[3][1] = -s.z; A[3][2] = s.y;
@@ -348,7 +363,6 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
     __syncthreads();
     STAMP(5);
     // ---- A8: Cholesky, rows in parallel (lane i owns row i)
-    const int off = fixed ? 6 : 0;
     {
       float (*A)[20] = E.u.fac.M;
       for (int j = off; j < 18; j++) {
@@ -370,7 +384,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       }
     }
     STAMP(6);
-    // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i; stored transposed = row i)
+    // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i)
     if (l < 18) {
       float y[18];
 #pragma unroll
@@ -384,6 +398,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
 #pragma unroll
           for (int m = 0; m < k; m++) s -= A[k][m] * y[m];
           y[k] = s * E.u.fac.invd[k];
+          __builtin_amdgcn_sched_barrier(0);  // keep the row's LDS loads next to their use
         }
 #pragma unroll
         for (int k = 17; k >= 0; k--) {
@@ -392,6 +407,7 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
           y[k] = xk;
 #pragma unroll
           for (int m = 0; m < k; m++) y[m] -= A[k][m] * xk;
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
 #pragma unroll
@@ -410,28 +426,28 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
     __syncthreads();
     if (l < 18) E.nu[l] = nu_star;
     STAMP(8);
-    // ---- A11: contact / limit detection and row allocation
-    bool act_c = false, act_l = false;
-    f3 cx = mk(0, 0, 0), cn = mk(0, 0, 1);
-    float phi = 0.f, gapv = 0.f, sgnv = 1.f;
-    if (l < 16 && l < M->num_contacts && !fixed) {
-      const int b = M->contact_body[l];
-      cx = ld3(E.o[b]) + mv3(E.R[b], ld3(M->contact_pos[l]));
-      float hg;
-      ground(cfg, cx.x + E.root[0], cx.y + E.root[1], &hg, &cn);
-      phi = (cx.z + E.root[2] - hg) * cn.z;
-      act_c = phi < cfg->contact_offset;
-    } else if (l >= 16 && l < 28) {
-      const int j = l - 16;
-      const float glo = E.q[j] - M->lower[j + 1], ghi = M->upper[j + 1] - E.q[j];
-      if (glo < 0.01f) { act_l = true; gapv = glo; sgnv = 1.f; }
-      else if (ghi < 0.01f) { act_l = true; gapv = ghi; sgnv = -1.f; }
-    }
+    // ---- A11: contact / limit detection and row allocation (whole contact triples first)
     {
+      bool act_c = false, act_l = false;
+      f3 cx = mk(0, 0, 0), cn = mk(0, 0, 1);
+      float phi = 0.f, gapv = 0.f, sgnv = 1.f;
+      if (l < 16 && l < M->num_contacts && !fixed) {
+        const int b = M->contact_body[l];
+        cx = ld3(E.o[b]) + mv3(E.R[b], ld3(M->contact_pos[l]));
+        float hg;
+        ground(cfg, cx.x + E.root[0], cx.y + E.root[1], &hg, &cn);
+        phi = (cx.z + E.root[2] - hg) * cn.z;
+        act_c = phi < cfg->contact_offset;
+      } else if (l >= 16 && l < 28) {
+        const int j = l - 16;
+        const float glo = E.q[j] - M->lower[j + 1], ghi = M->upper[j + 1] - E.q[j];
+        if (glo < 0.01f) { act_l = true; gapv = glo; sgnv = 1.f; }
+        else if (ghi < 0.01f) { act_l = true; gapv = ghi; sgnv = -1.f; }
+      }
       const uint64_t bal_c = __ballot(act_c), bal_l = __ballot(act_l);
       const uint32_t mc = (uint32_t)(bal_c >> (32 * half)) & 0xFFFFu;
       const uint32_t ml = ((uint32_t)(bal_l >> (32 * half)) >> 16) & 0xFFFu;
-      const int nc = min(__popc(mc), RMAX / 3);  // whole (normal, t1, t2) triples only
+      const int nc = min(__popc(mc), RMAX / 3);
       const int nrows = min(RMAX, 3 * nc + __popc(ml));
       const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
       if (l == 0) E.nrows = nrows;
@@ -447,8 +463,8 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
             const int r = start + d;
             f3 dir = d == 0 ? cn : (d == 1 ? t1 : t2);
             st3(E.rx[r], cx); st3(E.rd[r], dir);
-            E.rKind[r] = d; E.rPt[r] = l; E.rBody[r] = M->contact_body[l];
-            E.rTgt[r] = d == 0 ? tgt : 0.f;
+            E.rc[r].kind = d; E.rc[r].tgt = d == 0 ? tgt : 0.f;
+            E.rPt[r] = l; E.rBody[r] = M->contact_body[l];
             E.rLam[r] = E.lamst[l * 3 + d];
           }
         } else if (l < HG_NC) {
@@ -458,9 +474,9 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
         const int j = l - 16;
         const int r = 3 * nc + __popc(ml & ((1u << j) - 1u));
         if (act_l && r < RMAX) {
-          E.rKind[r] = 3; E.rPt[r] = j; E.rBody[r] = -1;
+          E.rc[r].kind = 3; E.rc[r].tgt = gapv >= 0.f ? -gapv / dt : fminf(-beta * gapv / dt, vmax);
+          E.rPt[r] = j; E.rBody[r] = -1;
           E.rd[r][0] = sgnv;
-          E.rTgt[r] = gapv >= 0.f ? -gapv / dt : fminf(-beta * gapv / dt, vmax);
           E.rLam[r] = E.lamst[HG_NC * 3 + j];
         } else {
           E.lamst[HG_NC * 3 + j] = 0.f;
@@ -468,17 +484,17 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       }
     }
     __syncthreads();
+    STAMP(9);
     const int nrows = E.nrows;
     const int nrmax = max(shm[0].nrows, shm[1].nrows);
-    STAMP(9);
-    // ---- A12: Jacobian row (registers), Y = M^-1 J^T, D, initial row velocity
+    // ---- A12: Jacobian row (registers), Y = M^-1 J^T, 1/D, J nu*
     float J[18];
 #pragma unroll
     for (int i = 0; i < 18; i++) J[i] = 0.f;
-    float vrow = 0.f, invD = 0.f;
+    float vrow = 0.f;
     const bool own = l < nrows;
-    const int kind = own ? E.rKind[l] : 2;
     if (own) {
+      const int kind = E.rc[l].kind;
       if (kind == 3) {
         const int j = E.rPt[l];
 #pragma unroll
@@ -507,93 +523,96 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
       float D = 0.f, v0 = 0.f;
 #pragma unroll
       for (int i = 0; i < 18; i++) { D += J[i] * Yr[i]; v0 += J[i] * E.nu[i]; E.Y[l][i] = Yr[i]; }
-      E.rD[l] = D;
-      invD = 1.0f / D;
-      E.rInvD[l] = invD;
+      E.rc[l].invD = 1.0f / D;
       vrow = v0;
     }
     __syncthreads();
+    if (own && E.rc[l].kind == 1) E.rc[l].invD2 = E.rc[l + 1].invD;
     STAMP(10);
-    // ---- A13: Delassus rows W[r][:] = J_r M^-1 J^T (lane r), warm-start row velocities
-    if (own) {
-      float acc = vrow;
-      for (int r2 = 0; r2 < nrows; r2++) {
-        float wv = 0.f;
+    // ---- A13: Delassus row W[l][:] = J_l M^-1 J^T in registers; warm-start row velocities
+    // lane r of an env owns row r: its impulse mylam, its velocity vrow = J_r nu, its W row
+    float wrow[RMAX];
+    float mylam = own ? E.rLam[l] : 0.f;
+#pragma unroll
+    for (int r2 = 0; r2 < RMAX; r2++) {
+      float wv = 0.f;
+      if (own && r2 < nrows) {
 #pragma unroll
         for (int i = 0; i < 18; i++) wv += J[i] * E.Y[r2][i];
-        E.u.W[r2][l] = wv;  // symmetric: W[l][r2] = W[r2][l]
-        acc += wv * E.rLam[r2];
       }
-      vrow = acc;
+      wrow[r2] = wv;
+      if (r2 < nrows) vrow += wv * E.rLam[r2];
     }
-    __syncthreads();
     STAMP(11);
-    // ---- A14: projected Gauss-Seidel (rows in order; normal, then its tangent pair)
+    // ---- A14: projected Gauss-Seidel, rows in order (normal, then its tangent pair).  Row state
+    // (v_r, lambda_r) lives in lane r and is read with v_readlane; the update is uniform over the
+    // env's 32 lanes; no LDS traffic besides the read-only 16-byte row constants
     {
       const float mu = 0.5f * (E.fric + cfg->ground_friction);
-      float lam_n = 0.f;  // normal impulse of the contact whose tangent rows follow
+      const int hb = 32 * half;
+#define RL(x, r) (half ? readlane_f((x), 32 + (r)) : readlane_f((x), (r)))
       for (int it = 0; it < cfg->pgs_iterations; it++) {
-        for (int r = 0; r < nrmax; r++) {
-          const bool live = r < nrows;
-          const int kr = live ? E.rKind[r] : 2;
-          const float v_a = readlane_f(vrow, r), v_b = readlane_f(vrow, 32 + r);
-          const float vr = half ? v_b : v_a;
-          float dl0 = 0.f, dl1 = 0.f;
-          if (kr == 0 || kr == 3) {
-            const float lam = E.rLam[r];
-            const float ln = fmaxf(lam + (E.rTgt[r] - vr) * E.rInvD[r], 0.f);
-            dl0 = ln - lam;
-            if (l == 0) E.rLam[r] = ln;
-            if (kr == 0) lam_n = ln;
-          } else if (kr == 1) {
-            const float v2a = readlane_f(vrow, r + 1), v2b = readlane_f(vrow, 32 + r + 1);
-            const float vr2 = half ? v2b : v2a;
-            const float la1 = E.rLam[r], la2 = E.rLam[r + 1];
-            float l1 = la1 - vr * E.rInvD[r], l2 = la2 - vr2 * E.rInvD[r + 1];
-            const float lim = mu * lam_n, nn = sqrtf(l1 * l1 + l2 * l2);
-            if (nn > lim) { const float s = lim / nn; l1 *= s; l2 *= s; }
-            dl0 = l1 - la1;
-            dl1 = l2 - la2;
-            if (l == 0) { E.rLam[r] = l1; E.rLam[r + 1] = l2; }
-          }
-          if (own && live) {
-            vrow += E.u.W[r][l] * dl0;
-            if (kr == 1) vrow += E.u.W[r + 1][l] * dl1;
+#pragma unroll
+        for (int r = 0; r < RMAX; r++) {
+          if (r < nrmax) {
+            const bool live = r < nrows;
+            const RowC c = E.rc[r];
+            const int kr = live ? c.kind : 2;
+            const float vr = RL(vrow, r), lr = RL(mylam, r);
+            float dl0 = 0.f, dl1 = 0.f;
+            if (kr == 0 || kr == 3) {
+              const float ln = fmaxf(lr + (c.tgt - vr) * c.invD, 0.f);
+              dl0 = ln - lr;
+              if (l == r) mylam = ln;
+            } else if (kr == 1 && r + 1 < RMAX) {
+              const float vr2 = RL(vrow, r + 1), lr2 = RL(mylam, r + 1);
+              const float lnrm = r >= 1 ? RL(mylam, r - 1) : 0.f;
+              float l1 = lr - vr * c.invD, l2 = lr2 - vr2 * c.invD2;
+              const float lim = mu * lnrm, nn = sqrtf(l1 * l1 + l2 * l2);
+              if (nn > lim) { const float sc = lim / nn; l1 *= sc; l2 *= sc; }
+              dl0 = l1 - lr;
+              dl1 = l2 - lr2;
+              if (l == r) mylam = l1;
+              if (l == r + 1) mylam = l2;
+            }
+            if (r + 1 < RMAX) vrow += wrow[r] * dl0 + wrow[r + 1] * dl1;
+            else vrow += wrow[r] * dl0;
           }
         }
       }
+      (void)hb;
     }
-    __syncthreads();
     STAMP(12);
     // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
+    if (own) E.rLam[l] = mylam;
+    for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
+    __syncthreads();
     float nu_new = 0.f;
     if (l < 18) {
       float s = E.nu[l];
       for (int r = 0; r < nrows; r++) s += E.Y[r][l] * E.rLam[r];
       nu_new = s;
     }
-    for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
-    __syncthreads();
     if (own) {
-      const float lam = E.rLam[l];
+      const int kind = E.rc[l].kind;
       if (kind == 3) {
-        E.lamst[HG_NC * 3 + E.rPt[l]] = lam;
+        E.lamst[HG_NC * 3 + E.rPt[l]] = mylam;
       } else {
-        E.lamst[E.rPt[l] * 3 + kind] = lam;
+        E.lamst[E.rPt[l] * 3 + kind] = mylam;
         const int b = E.rBody[l];
-        const float s = lam / dt;
-        atomicAdd(&E.cf[b][0], J[0] * s);
-        atomicAdd(&E.cf[b][1], J[1] * s);
-        atomicAdd(&E.cf[b][2], J[2] * s);
+        const float s = mylam / dt;
+        atomicAdd(&E.cf[b][0], E.rd[l][0] * s);
+        atomicAdd(&E.cf[b][1], E.rd[l][1] * s);
+        atomicAdd(&E.cf[b][2], E.rd[l][2] * s);
       }
     }
-    STAMP(13);
-    // ---- A16: integrate
     const bool fin = (l >= 18) || isfinite(nu_new);
     if ((uint32_t)(__ballot(!fin) >> (32 * half)) != 0u && l == 0) E.bad = 1;
     __syncthreads();
     if (l < 18) E.nu[l] = nu_new;
     __syncthreads();
+    STAMP(13);
+    // ---- A16: integrate (semi-implicit Euler; exact quaternion exponential)
     if (l < 12) {
       E.qd[l] = E.nu[6 + l];
       E.q[l] += dt * E.qd[l];
@@ -636,6 +655,22 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
   __syncthreads();
   if (l < 2) kin_chain(E, M, l, gz, false);
   __syncthreads();
+  // stage the [13][13] rigid states and [13][3] contact forces in LDS, then store each env's
+  // rows as one contiguous run (AoS, the reference's tensor layout)
+  if (l < 13) {
+    const int b = l;
+    float qq[4];
+    mat_to_quat(E.R[b], qq);
+    float* o = E.u.out.rigid + b * 13;
+    o[0] = E.o[b][0] + E.root[0];
+    o[1] = E.o[b][1] + E.root[1];
+    o[2] = E.o[b][2] + E.root[2];
+    o[3] = qq[0]; o[4] = qq[1]; o[5] = qq[2]; o[6] = qq[3];
+    o[7] = E.v[b][0]; o[8] = E.v[b][1]; o[9] = E.v[b][2];
+    o[10] = E.w[b][0]; o[11] = E.w[b][1]; o[12] = E.w[b][2];
+  }
+  for (int i = l; i < 13 * 3; i += 32) E.u.out.cf[i] = (&E.cf[0][0])[i];
+  __syncthreads();
   STAMP(15);
   STAMP_FLUSH();
   if (!valid) return;
@@ -645,31 +680,22 @@ __global__ void __launch_bounds__(64) k_step2(HgState S, const float* __restrict
     if (l == 0) {
       S.nonfinite[e] += 1;
       S.root[2 * np + e] = -10.f;
-      S.contact[2 * np + e] = 1e3f;
+      HG_CF(S, e, 0, 2) = 1e3f;
     }
     if (l < 12) S.dof_vel[l * np + e] = 0.f;
     return;
   }
-  if (l < 13) {
-    const int b = l;
-    float qq[4];
-    mat_to_quat(E.R[b], qq);
-    float* o = S.rigid + (size_t)b * 13 * np + e;
-    o[0 * np] = E.o[b][0] + E.root[0];
-    o[1 * np] = E.o[b][1] + E.root[1];
-    o[2 * np] = E.o[b][2] + E.root[2];
-    o[3 * np] = qq[0]; o[4 * np] = qq[1]; o[5 * np] = qq[2]; o[6 * np] = qq[3];
-    o[7 * np] = E.v[b][0]; o[8 * np] = E.v[b][1]; o[9 * np] = E.v[b][2];
-    o[10 * np] = E.w[b][0]; o[11 * np] = E.w[b][1]; o[12 * np] = E.w[b][2];
-    S.root[b * np + e] = E.root[b];
-  }
+  float* rs = &HG_RS(S, e, 0, 0);
+  for (int i = l; i < 13 * 13; i += 32) rs[i] = E.u.out.rigid[i];
+  float* cfo = &HG_CF(S, e, 0, 0);
+  for (int i = l; i < 13 * 3; i += 32) cfo[i] = E.u.out.cf[i];
+  if (l < 13) S.root[l * np + e] = E.root[l];
   if (l < 12) {
     S.dof_pos[l * np + e] = E.q[l];
     S.dof_vel[l * np + e] = E.qd[l];
     S.torques[l * np + e] = E.tau[l];
   }
   for (int i = l; i < HG_LAMW; i += 32) S.lambda[i * np + e] = E.lamst[i];
-  for (int i = l; i < 13 * 3; i += 32) S.contact[i * np + e] = (&E.cf[0][0])[i];
 }
 
 extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream) {
