@@ -186,6 +186,10 @@ __device__ __forceinline__ void mat_to_quat(const float* m, float* q) {
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
+// value of lane r of this lane's env (lanes 0..31 or 32..63): both reads are scalar, the pick
+// is one v_cndmask (no divergent branch around the convergent readlane)
+#define RL(x, r) hsel(half, readlane_f((x), (r)), readlane_f((x), 32 + (r)))
+__device__ __forceinline__ float hsel(int half, float lo, float hi) { return half ? hi : lo; }
 
 }  // namespace
 
@@ -451,6 +455,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       const int nrows = min(RMAX, 3 * nc + __popc(ml));
       const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
       if (l == 0) E.nrows = nrows;
+      if (l >= nrows) { E.rc[l].kind = 2; E.rc[l].tgt = 0.f; E.rc[l].invD = 0.f; E.rc[l].invD2 = 0.f; }
       if (l < 16) {
         const int rank = __popc(mc & ((1u << l) - 1u));
         if (act_c && rank < nc) {
@@ -486,7 +491,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     STAMP(9);
     const int nrows = E.nrows;
-    const int nrmax = max(shm[0].nrows, shm[1].nrows);
+    const int nrmax = __builtin_amdgcn_readfirstlane(max(shm[0].nrows, shm[1].nrows));
     // ---- A12: Jacobian row (registers), Y = M^-1 J^T, 1/D, J nu*
     float J[18];
 #pragma unroll
@@ -528,6 +533,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     if (own && E.rc[l].kind == 1) E.rc[l].invD2 = E.rc[l + 1].invD;
+    __syncthreads();
     STAMP(10);
     // ---- A13: Delassus row W[l][:] = J_l M^-1 J^T in registers; warm-start row velocities
     // lane r of an env owns row r: its impulse mylam, its velocity vrow = J_r nu, its W row
@@ -546,41 +552,40 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     STAMP(11);
     // ---- A14: projected Gauss-Seidel, rows in order (normal, then its tangent pair).  Row state
     // (v_r, lambda_r) lives in lane r and is read with v_readlane; the update is uniform over the
-    // env's 32 lanes; no LDS traffic besides the read-only 16-byte row constants
+    // env's 32 lanes and branch-free (both halves of the wave run it whatever their row kinds):
+    //   normal / limit row:  lambda <- max(lambda + (tgt - v) / D, 0)
+    //   tangent pair (r, r+1): unconstrained 2-D step, projected onto the disc mu * lambda_n,
+    //   lambda_n being the normal impulse updated one row earlier
+    //   kind 2 / unused rows: no-op (rc.kind = 2 for rows >= nrows)
     {
       const float mu = 0.5f * (E.fric + cfg->ground_friction);
-      const int hb = 32 * half;
-#define RL(x, r) (half ? readlane_f((x), 32 + (r)) : readlane_f((x), (r)))
-      for (int it = 0; it < cfg->pgs_iterations; it++) {
+      const int npgs = cfg->pgs_iterations;
+      for (int it = 0; it < npgs; it++) {
+        float prev_ln = 0.f;
 #pragma unroll
         for (int r = 0; r < RMAX; r++) {
           if (r < nrmax) {
-            const bool live = r < nrows;
-            const RowC c = E.rc[r];
-            const int kr = live ? c.kind : 2;
-            const float vr = RL(vrow, r), lr = RL(mylam, r);
-            float dl0 = 0.f, dl1 = 0.f;
-            if (kr == 0 || kr == 3) {
-              const float ln = fmaxf(lr + (c.tgt - vr) * c.invD, 0.f);
-              dl0 = ln - lr;
-              if (l == r) mylam = ln;
-            } else if (kr == 1 && r + 1 < RMAX) {
-              const float vr2 = RL(vrow, r + 1), lr2 = RL(mylam, r + 1);
-              const float lnrm = r >= 1 ? RL(mylam, r - 1) : 0.f;
-              float l1 = lr - vr * c.invD, l2 = lr2 - vr2 * c.invD2;
-              const float lim = mu * lnrm, nn = sqrtf(l1 * l1 + l2 * l2);
-              if (nn > lim) { const float sc = lim / nn; l1 *= sc; l2 *= sc; }
-              dl0 = l1 - lr;
-              dl1 = l2 - lr2;
-              if (l == r) mylam = l1;
-              if (l == r + 1) mylam = l2;
-            }
-            if (r + 1 < RMAX) vrow += wrow[r] * dl0 + wrow[r + 1] * dl1;
-            else vrow += wrow[r] * dl0;
+          const RowC c = E.rc[r];
+          const float vr = RL(vrow, r), lr = RL(mylam, r);
+          const bool isF = c.kind == 1, isN = c.kind == 0 || c.kind == 3;
+          const float ln = fmaxf(lr + (c.tgt - vr) * c.invD, 0.f);
+          float dl0 = isN ? ln - lr : 0.f, dl1 = 0.f;
+          if (r + 1 < RMAX) {
+            const float vr2 = RL(vrow, r + 1), lr2 = RL(mylam, r + 1);
+            float l1 = lr - vr * c.invD, l2 = lr2 - vr2 * c.invD2;
+            const float lim = mu * prev_ln, nn2 = l1 * l1 + l2 * l2;
+            const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+            dl0 = isF ? l1 * sc - lr : dl0;
+            dl1 = isF ? l2 * sc - lr2 : 0.f;
+            vrow += wrow[r] * dl0 + wrow[r + 1] * dl1;
+          } else {
+            vrow += wrow[r] * dl0;
+          }
+          mylam += (l == r ? dl0 : 0.f) + (l == r + 1 ? dl1 : 0.f);
+          prev_ln = isN ? ln : prev_ln;
           }
         }
       }
-      (void)hb;
     }
     STAMP(12);
     // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
