@@ -31,8 +31,11 @@ class _DiagGaussian:
         return self.scale
 
     def sample(self):
+        # torch.normal(loc, scale) computes normal_(0, 1) * scale + loc after checking
+        # scale >= 0 with a host round trip (two device syncs per call); this is the same
+        # arithmetic on the same generator stream without the check
         with torch.no_grad():
-            return torch.normal(self.loc, self.scale)
+            return torch.randn_like(self.loc).mul_(self.scale).add_(self.loc)
 
     def log_prob(self, value):
         var = self.scale ** 2

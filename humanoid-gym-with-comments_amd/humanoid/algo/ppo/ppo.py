@@ -9,6 +9,12 @@ Data parallel (new): when torch.distributed is initialised with wor
 live in ONE flat buffer that is all-reduced (SUM / world) before clip_grad_norm_, and kl_mean is
 all-reduced so the adaptive learning rate stays identical on every rank.  With world_size 1 the
 path is the reference's.
+
+Sync-free update on a ROCm device: the adaptive learning rate is a float64 device scalar updated
+with the reference's rule (torch.where instead of Python branches on kl_mean.item()) and fed to
+the fused Adam kernel as a tensor; the three loss means are accumulated on the device and read
+once per update.  The host therefore never waits for the GPU inside the minibatch loop.  On the
+CPU the reference's host-side arithmetic is kept verbatim (this is what the golden tests pin).
 """
 import torch
 import torch.distributed as dist
@@ -34,9 +40,9 @@ class PPO:
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu", sym_loss=False,
                  obs_permutation=None, act_permutation=None, frame_stack=0, sym_coef=1.0, base_lin_vel_coef=1.0):
         self.device = device
+        self._lr = float(learning_rate)
         self.desired_kl = desired_kl
         self.schedule = schedule
-        self.learning_rate = learning_rate
         self.actor_critic = actor_critic
         self.actor_critic.to(self.device)
         self.storage = None
@@ -53,7 +59,16 @@ class PPO:
             for p in self._params:
                 p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
                 off += p.numel()
-        self.optimizer = optim.Adam(self._params, lr=learning_rate)
+        self._on_device = torch.device(device).type == "cuda"
+        if self._on_device:
+            # float64 master (the reference's Python-float arithmetic) + the float32 copy the fused
+            # Adam kernel reads
+            self._lr_t = torch.tensor(float(learning_rate), dtype=torch.float64, device=device)
+            self._lr_f32 = self._lr_t.float()
+            self.optimizer = optim.Adam(self._params, lr=self._lr_f32, fused=True)
+        else:
+            self._lr_t = None
+            self.optimizer = optim.Adam(self._params, lr=learning_rate)
         self.transition = RolloutStorage.Transition()
         self.clip_param = clip_param
         self.num_learning_epochs = num_learning_epochs
@@ -81,6 +96,23 @@ class PPO:
             self.obs_perm_mat = torch.zeros(len(stack), len(stack), device=device)
             for i, perm in enumerate(stack):
                 self.obs_perm_mat[int(abs(perm))][i] = 1.0 if perm >= 0 else -1.0
+
+    @property
+    def learning_rate(self):
+        """Current learning rate as a Python float (reads the device scalar: logging only)."""
+        if self._lr_t is not None:
+            return float(self._lr_t.item())
+        return self._lr
+
+    @learning_rate.setter
+    def learning_rate(self, value):
+        self._lr = float(value)
+        if getattr(self, "_lr_t", None) is not None:
+            self._lr_t.fill_(self._lr)
+            self._lr_f32.fill_(self._lr)
+        elif hasattr(self, "optimizer"):
+            for g in self.optimizer.param_groups:
+                g["lr"] = self._lr
 
     def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
@@ -126,19 +158,32 @@ class PPO:
             if self.world_size > 1:
                 dist.all_reduce(kl_mean)
                 kl_mean /= self.world_size
+            if self._lr_t is not None:
+                # the reference's rule in float64 on the device (kl promoted exactly as
+                # Python promotes kl_mean.item())
+                k = kl_mean.double()
+                lr = self._lr_t
+                down = torch.clamp_min(lr / 1.5, 1e-5)
+                up = torch.clamp_max(lr * 1.5, 1e-2)
+                new = torch.where(k > self.desired_kl * 2.0, down,
+                                  torch.where((k < self.desired_kl / 2.0) & (k > 0.0), up, lr))
+                self._lr_t.copy_(new)
+                self._lr_f32.copy_(new)
+                return
             kl_mean = kl_mean.item()
         if kl_mean > self.desired_kl * 2.0:
-            self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+            self._lr = max(1e-5, self._lr / 1.5)
         elif kl_mean < self.desired_kl / 2.0 and kl_mean > 0.0:
-            self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+            self._lr = min(1e-2, self._lr * 1.5)
         for g in self.optimizer.param_groups:
-            g["lr"] = self.learning_rate
+            g["lr"] = self._lr
 
     def update(self):
         mean_value_loss = 0.0
         mean_surrogate_loss = 0.0
         mean_base_lin_vel_loss = 0.0
         sym_loss = 0
+        sums = None
         ac = self.actor_critic
         gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
@@ -181,10 +226,16 @@ class PPO:
                 loss.backward()
             nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
             self.optimizer.step()
-            mean_value_loss += value_loss.item()
-            mean_surrogate_loss += surrogate_loss.item()
-            mean_base_lin_vel_loss += base_lin_vel_loss.item()
+            if self._on_device:
+                acc = torch.stack([value_loss.detach(), surrogate_loss.detach(), base_lin_vel_loss.detach()])
+                sums = acc if sums is None else sums + acc
+            else:
+                mean_value_loss += value_loss.item()
+                mean_surrogate_loss += surrogate_loss.item()
+                mean_base_lin_vel_loss += base_lin_vel_loss.item()
         num_updates = self.num_learning_epochs * self.num_mini_batches
+        if sums is not None:
+            mean_value_loss, mean_surrogate_loss, mean_base_lin_vel_loss = sums.tolist()  # one host read
         mean_value_loss /= num_updates
         mean_surrogate_loss /= num_updates
         mean_base_lin_vel_loss /= num_updates

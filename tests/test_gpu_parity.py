@@ -298,3 +298,37 @@ def test_runner_one_iteration():
     st = runner.last_iteration_stats
     assert np.isfinite(st["value_loss"]) and np.isfinite(st["surrogate_loss"])
     assert torch.isfinite(env.obs_buf).all()
+
+
+def test_ppo_update_sync_free_matches_golden(golden, monkeypatch):
+    """The device-resident update (fused Adam with a float64 device learning rate, adaptive-KL
+    rule evaluated with torch.where, losses read once) against the reference golden update.
+    Minibatch order is drawn on the CPU generator exactly as in the golden run."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    from test_ppo_golden import SMALL, sd
+    g = golden("ppo_update.npz")
+    torch.manual_seed(0)
+    ac = ActorCritic(**SMALL)
+    ac.load_state_dict(sd(g, "init/"))
+    ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.994, lam=0.9,
+              value_loss_coef=1.0, entropy_coef=0.001, learning_rate=1e-5, max_grad_norm=1.0,
+              use_clipped_value_loss=True, schedule="adaptive", desired_kl=0.01, device="cuda:0")
+    assert ppo._lr_t is not None and ppo._lr_t.is_cuda
+    ppo.init_storage(8, 24, [141], [73], [12])
+    st = ppo.storage
+    for k in ("observations", "privileged_observations", "actions", "rewards", "dones", "values", "actions_log_prob",
+              "mu", "sigma", "returns", "advantages"):
+        getattr(st, k).copy_(torch.from_numpy(g["st/" + k]))
+    st.step = 24
+    real = torch.randperm
+    monkeypatch.setattr(torch, "randperm", lambda n, **kw: real(n).to(kw.get("device", "cpu")))
+    torch.manual_seed(1234)
+    vloss, sloss, sym, lvloss = ppo.update()
+    np.testing.assert_allclose(vloss, g["value_loss"], rtol=1e-4)
+    np.testing.assert_allclose(sloss, g["surrogate_loss"], rtol=1e-3, atol=1e-6)
+    np.testing.assert_allclose(lvloss, g["lin_vel_loss"], rtol=1e-4)
+    np.testing.assert_allclose(ppo.learning_rate, g["learning_rate"], rtol=1e-12)
+    final = sd(g, "final/")
+    for k, v in ac.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), final[k].numpy(), rtol=1e-4, atol=2e-6, err_msg=k)
