@@ -168,6 +168,7 @@ def main():
     ap.add_argument("--T", type=int, default=24, help="rollout length (num_steps_per_env)")
     ap.add_argument("--cpu-envs", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gemm-table", action="store_true", help="hipBLASLt default GEMM heuristics")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -180,6 +181,8 @@ def main():
     torch.manual_seed(5 + rank)
     np.random.seed(5 + rank)
     from humanoid.algo.ppo import OnPolicyRunner
+    from humanoid.utils.blas_tuning import use_tuned_gemms
+    tuned = use_tuned_gemms() if not args.no_gemm_table else False
     env = make_env(args.envs, device, seed=5 + rank)
     runner = OnPolicyRunner(env, train_cfg(args.T), log_dir=None, device=device)
     timer = KernelTimer()
@@ -219,7 +222,8 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": "XBot-L flat terrain, 4096 envs/GPU, PPO 24-step rollout (BASELINE configs[1])",
                    "envs_per_gpu": args.envs, "num_steps_per_env": args.T, "parallelism": f"dp{world}",
-                   "ppo": "2 epochs x 4 minibatches, actor 705-512-256-128-12, critic 219-768-256-128-1"},
+                   "ppo": "2 epochs x 4 minibatches, actor 705-512-256-128-12, critic 219-768-256-128-1",
+                   "gemm_table": "tuning/tunableop_mi355x_f32.csv" if tuned else None},
         "roofline": roofline,
         "collection_time_s": round(runner.last_iteration_stats.get("collection_time", float("nan")), 4),
         "learn_time_s": round(runner.last_iteration_stats.get("learn_time", float("nan")), 4),

@@ -48,24 +48,30 @@ class PPO:
         self.storage = None
         self.world_size = _world()
         self._params = list(self.actor_critic.parameters())
+        self._on_device = torch.device(device).type == "cuda"
+        self.use_graphs = self._on_device
+        self._graphs = None
+        self._graph_warm = False
+        self._flat_grad = None
         if self.world_size > 1:
             with torch.no_grad():
                 for p in self._params:
                     dist.broadcast(p.data, src=0)
-            # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack copies
+        if self.world_size > 1 or self._on_device:
+            # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack
+            # copies; fixed gradient addresses for the captured update graph
             numel = sum(p.numel() for p in self._params)
             self._flat_grad = torch.zeros(numel, device=self._params[0].device, dtype=torch.float32)
             off = 0
             for p in self._params:
                 p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
                 off += p.numel()
-        self._on_device = torch.device(device).type == "cuda"
         if self._on_device:
             # float64 master (the reference's Python-float arithmetic) + the float32 copy the fused
             # Adam kernel reads
             self._lr_t = torch.tensor(float(learning_rate), dtype=torch.float64, device=device)
             self._lr_f32 = self._lr_t.float()
-            self.optimizer = optim.Adam(self._params, lr=self._lr_f32, fused=True)
+            self.optimizer = optim.Adam(self._params, lr=self._lr_f32, fused=True, capturable=True)
         else:
             self._lr_t = None
             self.optimizer = optim.Adam(self._params, lr=learning_rate)
@@ -126,7 +132,9 @@ class PPO:
 
     def act(self, obs, critic_obs):
         t = self.transition
-        t.actions = self.actor_critic.act(obs)[0].detach()
+        # actor_critic.act() would also run the lin-vel MLP, whose output the rollout discards
+        self.actor_critic.update_distribution(obs)
+        t.actions = self.actor_critic.distribution.sample().detach()
         t.values = self.actor_critic.evaluate(critic_obs).detach()
         t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
         t.action_mean = self.actor_critic.action_mean.detach()
@@ -149,28 +157,36 @@ class PPO:
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         self.storage.compute_returns(last_values, self.gamma, self.lam)
 
-    def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
+    def _kl_mean(self, mu, sigma, old_mu, old_sigma):
         with torch.inference_mode():
             kl = torch.sum(torch.log(sigma / old_sigma + 1.0e-5)
                            + (torch.square(old_sigma) + torch.square(old_mu - mu)) / (2.0 * torch.square(sigma))
                            - 0.5, axis=-1)
-            kl_mean = torch.mean(kl)
-            if self.world_size > 1:
+            return torch.mean(kl)
+
+    def _lr_rule_device(self, kl_mean):
+        """The reference's adaptive rule (ppo.py:168-176) in float64 on the device (kl promoted
+        exactly as Python promotes kl_mean.item())."""
+        with torch.inference_mode():
+            k = kl_mean.double()
+            lr = self._lr_t
+            down = torch.clamp_min(lr / 1.5, 1e-5)
+            up = torch.clamp_max(lr * 1.5, 1e-2)
+            new = torch.where(k > self.desired_kl * 2.0, down,
+                              torch.where((k < self.desired_kl / 2.0) & (k > 0.0), up, lr))
+            self._lr_t.copy_(new)
+            self._lr_f32.copy_(new)
+
+    def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
+        kl_mean = self._kl_mean(mu, sigma, old_mu, old_sigma)
+        if self.world_size > 1:
+            with torch.inference_mode():
                 dist.all_reduce(kl_mean)
                 kl_mean /= self.world_size
-            if self._lr_t is not None:
-                # the reference's rule in float64 on the device (kl promoted exactly as
-                # Python promotes kl_mean.item())
-                k = kl_mean.double()
-                lr = self._lr_t
-                down = torch.clamp_min(lr / 1.5, 1e-5)
-                up = torch.clamp_max(lr * 1.5, 1e-2)
-                new = torch.where(k > self.desired_kl * 2.0, down,
-                                  torch.where((k < self.desired_kl / 2.0) & (k > 0.0), up, lr))
-                self._lr_t.copy_(new)
-                self._lr_f32.copy_(new)
-                return
-            kl_mean = kl_mean.item()
+        if self._lr_t is not None:
+            self._lr_rule_device(kl_mean)
+            return
+        kl_mean = kl_mean.item()
         if kl_mean > self.desired_kl * 2.0:
             self._lr = max(1e-5, self._lr / 1.5)
         elif kl_mean < self.desired_kl / 2.0 and kl_mean > 0.0:
@@ -178,7 +194,50 @@ class PPO:
         for g in self.optimizer.param_groups:
             g["lr"] = self._lr
 
+    @property
+    def _adaptive(self):
+        return self.desired_kl is not None and self.schedule == "adaptive"
+
+    def _losses(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b):
+        """Minibatch loss (ppo.py:155-214).  The reference calls actor_critic.act() here and
+        discards the sampled action; only the distribution and the lin-vel estimate are used, so
+        the sample is not drawn."""
+        ac = self.actor_critic
+        ac.update_distribution(obs_b)
+        est_lin_vel = ac.base_get_lin_vel(obs_b)
+        logp_b = ac.get_actions_log_prob(actions_b)
+        value_b = ac.evaluate(critic_b)
+        mu_b = ac.action_mean
+        entropy_b = ac.entropy
+        # clipped surrogate
+        ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+        adv = torch.squeeze(adv_b)
+        surrogate = -adv * ratio
+        surrogate_clipped = -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
+        surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+        # value loss
+        if self.use_clipped_value_loss:
+            value_clipped = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
+            value_losses = (value_b - returns_b).pow(2)
+            value_losses_clipped = (value_clipped - returns_b).pow(2)
+            value_loss = torch.max(value_losses, value_losses_clipped).mean()
+        else:
+            value_loss = (returns_b - value_b).pow(2).mean()
+        sym_loss = 0
+        if self.sym_loss:
+            mirror_act = ac.actor(torch.matmul(obs_b, self.obs_perm_mat))
+            sym_loss = (mu_b - torch.matmul(mirror_act, self.act_perm_mat)).pow(2).mean()
+        base_lin_vel_loss = F.mse_loss(est_lin_vel, lin_vel_b)
+        loss = (surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean()
+                + self.sym_coef * sym_loss + self.base_lin_vel_coef * base_lin_vel_loss)
+        return loss, value_loss, surrogate_loss, base_lin_vel_loss, sym_loss
+
     def update(self):
+        if self._on_device and self.use_graphs:
+            return self._update_graphed()
+        return self._update_eager()
+
+    def _update_eager(self):
         mean_value_loss = 0.0
         mean_surrogate_loss = 0.0
         mean_base_lin_vel_loss = 0.0
@@ -188,39 +247,16 @@ class PPO:
         gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
              old_sigma_b, hid_b, masks_b) in gen:
-            _, est_lin_vel = ac.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
-            logp_b = ac.get_actions_log_prob(actions_b)
-            value_b = ac.evaluate(critic_b, masks=masks_b, hidden_states=hid_b[1])
-            mu_b = ac.action_mean
-            sigma_b = ac.action_std
-            entropy_b = ac.entropy
-            if self.desired_kl is not None and self.schedule == "adaptive":
-                self._adapt_lr(mu_b, sigma_b, old_mu_b, old_sigma_b)
-            # clipped surrogate
-            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
-            adv = torch.squeeze(adv_b)
-            surrogate = -adv * ratio
-            surrogate_clipped = -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
-            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
-            # value loss
-            if self.use_clipped_value_loss:
-                value_clipped = target_values_b + (value_b - target_values_b).clamp(-self.clip_param, self.clip_param)
-                value_losses = (value_b - returns_b).pow(2)
-                value_losses_clipped = (value_clipped - returns_b).pow(2)
-                value_loss = torch.max(value_losses, value_losses_clipped).mean()
-            else:
-                value_loss = (returns_b - value_b).pow(2).mean()
-            if self.sym_loss:
-                mirror_act = ac.actor(torch.matmul(obs_b, self.obs_perm_mat))
-                sym_loss = (mu_b - torch.matmul(mirror_act, self.act_perm_mat)).pow(2).mean()
-            base_lin_vel_loss = F.mse_loss(est_lin_vel, lin_vel_b)
-            loss = (surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean()
-                    + self.sym_coef * sym_loss + self.base_lin_vel_coef * base_lin_vel_loss)
-            if self.world_size > 1:
+            loss, value_loss, surrogate_loss, base_lin_vel_loss, sym_loss = self._losses(
+                obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b)
+            if self._adaptive:
+                self._adapt_lr(ac.action_mean, ac.action_std, old_mu_b, old_sigma_b)
+            if self._flat_grad is not None:
                 self._flat_grad.zero_()
                 loss.backward()
-                dist.all_reduce(self._flat_grad)
-                self._flat_grad /= self.world_size
+                if self.world_size > 1:
+                    dist.all_reduce(self._flat_grad)
+                    self._flat_grad /= self.world_size
             else:
                 self.optimizer.zero_grad()
                 loss.backward()
@@ -241,3 +277,86 @@ class PPO:
         mean_base_lin_vel_loss /= num_updates
         self.storage.clear()
         return mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss
+
+    # ------------------------------------------------------------------------------------------
+    # HIP-graph update: the minibatch step is captured once as two graphs and replayed
+    #   A: gather the minibatch rows (static index buffer) -> losses -> backward into the flat
+    #      gradient buffer; KL mean; loss sums
+    #   (world_size > 1: all-reduce of the flat gradients and of the KL mean, eager RCCL calls)
+    #   B: adaptive learning rate, global-norm clip, fused Adam
+    # The first update() runs eagerly on a side stream (the warm-up graph capture needs); the
+    # graphs are captured at the start of the second one.  Minibatch order: one randperm per
+    # update, as the reference's generator (rollout_storage.py:153-191).
+    # ------------------------------------------------------------------------------------------
+    def _storage_key(self):
+        st = self.storage
+        return (st.observations.data_ptr(), st.num_envs, st.num_transitions_per_env)
+
+    def _capture(self, mb):
+        st = self.storage
+        dev = st.observations.device
+        obs = st.observations.flatten(0, 1)
+        critic = st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else obs
+        flat = {"obs": obs, "critic": critic, "lin_vel": critic[:, 53:56],
+                "actions": st.actions.flatten(0, 1), "values": st.values.flatten(0, 1),
+                "returns": st.returns.flatten(0, 1), "logp": st.actions_log_prob.flatten(0, 1),
+                "adv": st.advantages.flatten(0, 1), "mu": st.mu.flatten(0, 1), "sigma": st.sigma.flatten(0, 1)}
+        self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
+        self._sums = torch.zeros(3, dtype=torch.float32, device=dev)
+        self._kl = torch.zeros((), dtype=torch.float32, device=dev)
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.graph(ga):
+            self._flat_grad.zero_()
+            i = self._idx
+            b = {k: v[i] for k, v in flat.items()}
+            loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
+                b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"], b["logp"])
+            if self._adaptive:
+                ac = self.actor_critic
+                self._kl.copy_(self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"]))
+            self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
+            loss.backward()
+        with torch.cuda.graph(gb, pool=ga.pool()):
+            if self.world_size > 1:
+                self._flat_grad.div_(self.world_size)
+                self._kl.div_(self.world_size)
+            if self._adaptive:
+                self._lr_rule_device(self._kl)
+            nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
+            self.optimizer.step()
+        self._graphs = (ga, gb, mb, self._storage_key())
+
+    def _update_graphed(self):
+        st = self.storage
+        nmb = self.num_mini_batches
+        batch = st.num_envs * st.num_transitions_per_env
+        mb = batch // nmb
+        if self.sym_loss or (self._graphs is None and not self._graph_warm):
+            # warm-up (and the symmetry-loss configuration, which stays eager)
+            cur = torch.cuda.current_stream()
+            side = torch.cuda.Stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                out = self._update_eager()
+            cur.wait_stream(side)
+            self._graph_warm = True
+            return out
+        if self._graphs is None or self._graphs[2] != mb or self._graphs[3] != self._storage_key():
+            self._capture(mb)
+        ga, gb = self._graphs[0], self._graphs[1]
+        indices = torch.randperm(nmb * mb, requires_grad=False, device=st.observations.device)
+        self._sums.zero_()
+        for _ in range(self.num_learning_epochs):
+            for i in range(nmb):
+                self._idx.copy_(indices[i * mb:(i + 1) * mb])
+                ga.replay()
+                if self.world_size > 1:
+                    dist.all_reduce(self._flat_grad)
+                    if self._adaptive:
+                        dist.all_reduce(self._kl)
+                gb.replay()
+        num_updates = self.num_learning_epochs * nmb
+        v, s, lv = (self._sums / num_updates).tolist()  # the one host read of the update
+        st.clear()
+        return v, s, 0, lv

@@ -332,3 +332,42 @@ def test_ppo_update_sync_free_matches_golden(golden, monkeypatch):
     final = sd(g, "final/")
     for k, v in ac.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), final[k].numpy(), rtol=1e-4, atol=2e-6, err_msg=k)
+
+
+def test_ppo_graphed_update_matches_eager():
+    """Three updates replayed from the captured HIP graphs == three eager updates (same data,
+    same minibatch permutations)."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    from test_ppo_golden import SMALL
+    torch.manual_seed(3)
+    init = ActorCritic(**SMALL).state_dict()
+    data = {}
+    g = torch.Generator().manual_seed(11)
+    shapes = {"observations": (24, 64, 141), "privileged_observations": (24, 64, 73), "actions": (24, 64, 12),
+              "rewards": (24, 64, 1), "values": (24, 64, 1), "actions_log_prob": (24, 64, 1), "mu": (24, 64, 12),
+              "sigma": (24, 64, 12), "returns": (24, 64, 1), "advantages": (24, 64, 1)}
+    for k, sh in shapes.items():
+        data[k] = torch.randn(*sh, generator=g)
+    data["sigma"] = data["sigma"].abs() + 0.5
+    runs = []
+    for graphs in (False, True):
+        ac = ActorCritic(**SMALL)
+        ac.load_state_dict(init)
+        ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=4, learning_rate=1e-3, entropy_coef=0.001,
+                  schedule="adaptive", desired_kl=0.01, device="cuda:0")
+        ppo.use_graphs = graphs
+        ppo.init_storage(64, 24, [141], [73], [12])
+        losses = []
+        for it in range(3):
+            for k, v in data.items():
+                getattr(ppo.storage, k).copy_(v)
+            torch.cuda.manual_seed(100 + it)
+            losses.append(ppo.update())
+        runs.append(({k: v.detach().cpu() for k, v in ac.state_dict().items()}, losses, ppo.learning_rate))
+    (sd0, l0, lr0), (sd1, l1, lr1) = runs
+    assert lr0 == lr1
+    np.testing.assert_allclose(np.array(l1)[:, [0, 1, 3]].astype(float), np.array(l0)[:, [0, 1, 3]].astype(float),
+                               rtol=1e-5, atol=1e-7)
+    for k in sd0:
+        np.testing.assert_allclose(sd1[k].numpy(), sd0[k].numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
