@@ -366,27 +366,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     STAMP(5);
-    // ---- A8: Cholesky, rows in parallel (lane i owns row i)
+    // ---- A8: Cholesky in registers: lane i holds row i of M (lower part); column j's entries
+    // L[k][j] reach the other rows by v_readlane (no LDS round trips, no barriers).  Entries
+    // right of a lane's diagonal are never read.
     {
-      float (*A)[20] = E.u.fac.M;
-      for (int j = off; j < 18; j++) {
-        if (l == j) {
-          const float d = A[j][j];
-          if (!(d > 0.f)) E.bad = 1;
+      float a[18];
+#pragma unroll
+      for (int k = 0; k < 18; k++) a[k] = (l < 18) ? E.u.fac.M[l < 18 ? l : 0][k] : 0.f;
+      float myinv = 0.f;
+      bool nonpd = false;
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        if (j >= off) {
+          const float d = RL(a[j], j);
+          nonpd |= !(d > 0.f);
           const float sd = sqrtf(fmaxf(d, 1e-20f));
-          A[j][j] = sd;
-          E.u.fac.invd[j] = 1.0f / sd;
+          const float inv = 1.0f / sd;
+          a[j] = (l == j) ? sd : (l > j ? a[j] * inv : a[j]);
+          myinv = (l == j) ? inv : myinv;
+#pragma unroll
+          for (int k = j + 1; k < 18; k++) a[k] -= a[j] * RL(a[j], k);
         }
-        __syncthreads();
-        if (l > j && l < 18) A[l][j] *= E.u.fac.invd[j];
-        __syncthreads();
-        if (l > j && l < 18) {
-          const float lij = A[l][j];
-          for (int k = j + 1; k <= l; k++) A[l][k] -= lij * A[k][j];
-        }
-        __syncthreads();
       }
+      if (l < 18) {
+#pragma unroll
+        for (int k = 0; k < 18; k++) E.u.fac.M[l][k] = a[k];
+        E.u.fac.invd[l] = myinv;
+      }
+      if (l == 0 && nonpd) E.bad = 1;
     }
+    __syncthreads();
     STAMP(6);
     // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i)
     if (l < 18) {
@@ -491,7 +500,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     STAMP(9);
     const int nrows = E.nrows;
-    const int nrmax = __builtin_amdgcn_readfirstlane(max(shm[0].nrows, shm[1].nrows));
     // ---- A12: Jacobian row (registers), Y = M^-1 J^T, 1/D, J nu*
     float J[18];
 #pragma unroll
@@ -533,6 +541,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     if (own && E.rc[l].kind == 1) E.rc[l].invD2 = E.rc[l + 1].invD;
+    // rows that are a no-op in BOTH envs of the wave (tangent partner rows, unused rows) are
+    // skipped by a scalar branch: with contacts allocated first as triples they line up
+    const uint64_t live_b = __ballot(own && E.rc[l].kind != 2);
+    const uint32_t live_rows = __builtin_amdgcn_readfirstlane((uint32_t)live_b | (uint32_t)(live_b >> 32));
     __syncthreads();
     STAMP(10);
     // ---- A13: Delassus row W[l][:] = J_l M^-1 J^T in registers; warm-start row velocities
@@ -564,7 +576,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         float prev_ln = 0.f;
 #pragma unroll
         for (int r = 0; r < RMAX; r++) {
-          if (r < nrmax) {
+          if (live_rows & (1u << r)) {
           const RowC c = E.rc[r];
           const float vr = RL(vrow, r), lr = RL(mylam, r);
           const bool isF = c.kind == 1, isN = c.kind == 0 || c.kind == 3;

@@ -138,7 +138,9 @@ class XBotLCfg(BaseConfig):
             contact_collection = 2
 
         class hg:
-            pgs_iterations = 6         # projected Gauss-Seidel sweeps per substep
+            # projected Gauss-Seidel sweeps per substep; None = the reference's solver budget,
+            # physx.num_position_iterations + physx.num_velocity_iterations (4 + 1)
+            pgs_iterations = None
             baumgarte = 0.2            # fraction of penetration corrected per substep
             armature = 0.01            # kg m^2 per leg joint (XBot-L.xml:37-39)
 

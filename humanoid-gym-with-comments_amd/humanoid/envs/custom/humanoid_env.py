@@ -38,7 +38,11 @@ def build_hg_cfg(cfg, num_envs, sim_dt, seed, model_js, heightfield=None, hf_sha
     c = N.HgCfg()
     c.num_envs = num_envs
     c.decimation = cfg.control.decimation
-    c.pgs_iterations = cfg.sim.hg.pgs_iterations
+    it = getattr(cfg.sim.hg, "pgs_iterations", None)
+    if it is None:
+        px = cfg.sim.physx
+        it = int(px.num_position_iterations) + int(getattr(px, "num_velocity_iterations", 0))
+    c.pgs_iterations = max(1, int(it))
     c.fix_base_link = int(cfg.asset.fix_base_link)
     c.sim_dt = sim_dt
     c.gravity_z = cfg.sim.gravity[2]
