@@ -189,6 +189,13 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 // value of lane r of this lane's env (lanes 0..31 or 32..63): both reads are scalar, the pick
 // is one v_cndmask (no divergent branch around the convergent readlane)
 #define RL(x, r) hsel(half, readlane_f((x), (r)), readlane_f((x), 32 + (r)))
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// v_permlane32_swap: x' = (x.lo | z.lo), z' = (x.hi | z.hi)
+__device__ __forceinline__ void swap32(float x, float z, float& xo, float& zo) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(z), false, false);
+  xo = __uint_as_float(r[0]);
+  zo = __uint_as_float(r[1]);
+}
 __device__ __forceinline__ float hsel(int half, float lo, float hi) { return half ? hi : lo; }
 
 }  // namespace
@@ -525,17 +532,58 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           J[5 + k] = anc ? dot(d, cross(ld3(E.a[k]), x - ld3(E.o[k]))) : 0.f;
         }
       }
-      float Yr[18];
+    }
+    // ---- Y = M^-1 J^T and W = J Y on the matrix cores (v_mfma_f32_32x32x2_f32), one 32x32
+    // product per env.  MFMA operand i/kk = lane%32 / lane/32, so the wave's two envs are
+    // interleaved with v_permlane32_swap: swap(X, Z) -> (X.lo|Z.lo, X.hi|Z.hi).
+    //   Y_h (dof x row): 9 k-pairs (2p, 2p+1); A = M^-1_h (rows >= 18 zero) read from LDS,
+    //   B = J_h^T.  D layout: lane (kk, n), vgpr v holds Y_h[8(v/4) + 4kk + v%4][n].
+    //   W_h = J_h Y_h: contraction pairs follow that layout, k = 8(q/4) + q%4 (+4 for kk = 1),
+    //   so Y's accumulators are the B operands as they stand.
+    f32x16 dy0 = {0}, dy1 = {0};
 #pragma unroll
-      for (int i = 0; i < 18; i++) {
-        float s = 0.f;
+    for (int p = 0; p < 9; p++) {
+      const float am0 = (l < 18) ? shm[0].u.fac.Minv[l < 18 ? l : 0][2 * p + half] : 0.f;
+      const float am1 = (l < 18) ? shm[1].u.fac.Minv[l < 18 ? l : 0][2 * p + half] : 0.f;
+      float b0, b1;
+      swap32(J[2 * p], J[2 * p + 1], b0, b1);
+      dy0 = __builtin_amdgcn_mfma_f32_32x32x2f32(am0, b0, dy0, 0, 0, 0);
+      dy1 = __builtin_amdgcn_mfma_f32_32x32x2f32(am1, b1, dy1, 0, 0, 0);
+    }
+    f32x16 dw0 = {0}, dw1 = {0};
 #pragma unroll
-        for (int k = 0; k < 18; k++) s += E.u.fac.Minv[i][k] * J[k];
-        Yr[i] = s;
-      }
-      float D = 0.f, v0 = 0.f;
+    for (int q = 0; q < 10; q++) {
+      const int klo = 8 * (q / 4) + q % 4, khi = klo + 4;
+      float a0, a1;
+      swap32(J[klo], khi < 18 ? J[khi < 18 ? khi : 0] : 0.f, a0, a1);
+      dw0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, dy0[q], dw0, 0, 0, 0);
+      dw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, dy1[q], dw1, 0, 0, 0);
+    }
+    // Y rows to LDS for the velocity update (A15): this lane holds Y_h[i][l] for its 10 dofs
 #pragma unroll
-      for (int i = 0; i < 18; i++) { D += J[i] * Yr[i]; v0 += J[i] * E.nu[i]; E.Y[l][i] = Yr[i]; }
+    for (int v = 0; v < 10; v++) {
+      const int i = 8 * (v / 4) + 4 * half + v % 4;
+      if (i < 18) { shm[0].Y[l][i] = dy0[v]; shm[1].Y[l][i] = dy1[v]; }
+    }
+    // gather each env's W column l into its own lanes: wA[v] = W[8(v/4) + v%4][l],
+    // wB[v] = W[8(v/4) + 4 + v%4][l]  (W symmetric: column l == row l)
+    float wA[16], wB[16];
+#pragma unroll
+    for (int v = 0; v < 16; v++) swap32(dw0[v], dw1[v], wA[v], wB[v]);
+    float wrow[RMAX];
+#pragma unroll
+    for (int m = 0; m < RMAX; m++) wrow[m] = (m % 8 < 4) ? wA[4 * (m / 8) + m % 8] : wB[4 * (m / 8) + m % 8 - 4];
+    float mylam = own ? E.rLam[l] : 0.f;
+    if (own) {
+      float D = 0.f;
+#pragma unroll
+      for (int m = 0; m < RMAX; m++) D = (l == m) ? wrow[m] : D;
+      float v0 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 18; i++) v0 += J[i] * E.nu[i];
+#pragma unroll
+      for (int m = 0; m < RMAX; m++)
+        if (m < nrows) v0 += wrow[m] * E.rLam[m];
       E.rc[l].invD = 1.0f / D;
       vrow = v0;
     }
@@ -547,20 +595,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const uint32_t live_rows = __builtin_amdgcn_readfirstlane((uint32_t)live_b | (uint32_t)(live_b >> 32));
     __syncthreads();
     STAMP(10);
-    // ---- A13: Delassus row W[l][:] = J_l M^-1 J^T in registers; warm-start row velocities
-    // lane r of an env owns row r: its impulse mylam, its velocity vrow = J_r nu, its W row
-    float wrow[RMAX];
-    float mylam = own ? E.rLam[l] : 0.f;
-#pragma unroll
-    for (int r2 = 0; r2 < RMAX; r2++) {
-      float wv = 0.f;
-      if (own && r2 < nrows) {
-#pragma unroll
-        for (int i = 0; i < 18; i++) wv += J[i] * E.Y[r2][i];
-      }
-      wrow[r2] = wv;
-      if (r2 < nrows) vrow += wv * E.rLam[r2];
-    }
     STAMP(11);
     // ---- A14: projected Gauss-Seidel, rows in order (normal, then its tangent pair).  Row state
     // (v_r, lambda_r) lives in lane r and is read with v_readlane; the update is uniform over the
