@@ -80,13 +80,15 @@ def active_rows(env):
     return float((3 * contacts + limits).mean().item())
 
 
-def make_env(num_envs, device, seed):
+def make_env(num_envs, device, seed, terrain="plane"):
     from humanoid.envs import XBotLCfg
     from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
     from humanoid.utils.helpers import SimParams
     cfg = XBotLCfg()
     cfg.env.num_envs = num_envs
     cfg.seed = seed
+    cfg.terrain.mesh_type = terrain
+    cfg.terrain.seed = 5  # identical heightfield on every rank
     return XBotLFreeEnv(cfg, SimParams(), "hg_sim", device, True)
 
 
@@ -169,6 +171,8 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-table", action="store_true", help="hipBLASLt default GEMM heuristics")
+    ap.add_argument("--terrain", default="plane", choices=["plane", "heightfield"],
+                    help="plane = config 2; heightfield = config 3 (2100x2100 generated terrain)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,7 +187,7 @@ def main():
     from humanoid.algo.ppo import OnPolicyRunner
     from humanoid.utils.blas_tuning import use_tuned_gemms
     tuned = use_tuned_gemms() if not args.no_gemm_table else False
-    env = make_env(args.envs, device, seed=5 + rank)
+    env = make_env(args.envs, device, seed=5 + rank, terrain=args.terrain)
     runner = OnPolicyRunner(env, train_cfg(args.T), log_dir=None, device=device)
     timer = KernelTimer()
     env.kernel_timer = timer
@@ -220,7 +224,9 @@ def main():
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ppo_iters_per_sec": round(args.steps / elapsed, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "XBot-L flat terrain, 4096 envs/GPU, PPO 24-step rollout (BASELINE configs[1])",
+        "config": {"workload": ("XBot-L flat terrain, 4096 envs/GPU, PPO 24-step rollout (BASELINE configs[1])"
+                                if args.terrain == "plane" else
+                                "XBot-L heightfield terrain 2100x2100, 4096 envs/GPU, PPO 24-step rollout (config 3)"),
                    "envs_per_gpu": args.envs, "num_steps_per_env": args.T, "parallelism": f"dp{world}",
                    "ppo": "2 epochs x 4 minibatches, actor 705-512-256-128-12, critic 219-768-256-128-1",
                    "gemm_table": "tuning/tunableop_mi355x_f32.csv" if tuned else None},

@@ -92,8 +92,9 @@ __device__ void ground(const hg_cfg* cfg, float x, float y, float* h, f3* n) {
   float h00 = vs * hf[i * C + j], h10 = vs * hf[(i + 1) * C + j];
   float h01 = vs * hf[i * C + j + 1], h11 = vs * hf[(i + 1) * C + j + 1];
   float dhdx, dhdy;
-  if (u + v <= 1) { *h = h00 + u * (h10 - h00) + v * (h01 - h00); dhdx = (h10 - h00) / hs; dhdy = (h01 - h00) / hs; }
-  else { *h = h11 + (1 - u) * (h01 - h11) + (1 - v) * (h10 - h11); dhdx = (h11 - h01) / hs; dhdy = (h11 - h10) / hs; }
+  // cells split along the (i,j)-(i+1,j+1) diagonal, as convert_heightfield_to_trimesh tessellates
+  if (u >= v) { *h = h00 + u * (h10 - h00) + v * (h11 - h10); dhdx = (h10 - h00) / hs; dhdy = (h11 - h10) / hs; }
+  else { *h = h00 + v * (h01 - h00) + u * (h11 - h01); dhdx = (h11 - h01) / hs; dhdy = (h01 - h00) / hs; }
   float inv = rsqrtf(dhdx * dhdx + dhdy * dhdy + 1);
   *n = mk(-dhdx * inv, -dhdy * inv, inv);
 }

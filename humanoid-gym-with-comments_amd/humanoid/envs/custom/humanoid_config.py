@@ -59,7 +59,8 @@ class XBotLCfg(BaseConfig):
         thickness = 0.01
 
     class terrain:
-        mesh_type = "plane"               # 'plane' | 'heightfield'
+        mesh_type = "plane"               # 'plane' | 'heightfield' | 'trimesh'
+        seed = None                       # heightfield generator seed (None: the run seed)
         horizontal_scale = 0.1
         vertical_scale = 0.005
         border_size = 25

@@ -183,14 +183,26 @@ class XBotLFreeEnv(BaseTask):
         self.custom_origins = False
         if mesh == "plane":
             pass
-        elif mesh == "heightfield":
+        elif mesh in ("heightfield", "trimesh"):
+            # 'trimesh' collides against the same triangulated heightfield (cells split along the
+            # (i,j)-(i+1,j+1) diagonal, the tessellation of convert_heightfield_to_trimesh).
+            # Every data-parallel rank must build the identical map: the generator runs on a
+            # private numpy stream seeded by terrain.seed (default: the run seed), then the global
+            # numpy state is restored.
             from humanoid.utils.terrain import HumanoidTerrain
-            self.terrain = HumanoidTerrain(self.cfg.terrain, self.num_envs)
+            tseed = getattr(self.cfg.terrain, "seed", None)
+            tseed = int(getattr(self.cfg, "seed", 5)) if tseed is None else int(tseed)
+            saved = np.random.get_state()
+            np.random.seed(tseed)
+            try:
+                self.terrain = HumanoidTerrain(self.cfg.terrain, self.num_envs)
+            finally:
+                np.random.set_state(saved)
             self.height_samples = torch.tensor(self.terrain.heightsamples, dtype=torch.int16, device=self.device)
             hf_ptr, hf_shape = self.height_samples.data_ptr(), tuple(self.height_samples.shape)
             self.custom_origins = True
         elif mesh is not None:
-            raise ValueError("Terrain mesh type not recognised. Allowed types are [None, plane, heightfield]")
+            raise ValueError("Terrain mesh type not recognised. Allowed types are [None, plane, heightfield, trimesh]")
         seed = int(getattr(self.cfg, "seed", 5))
         self._hgcfg, self._aux = build_hg_cfg(self.cfg, self.num_envs, self.sim_dt, seed, js, hf_ptr, hf_shape)
         nbytes = self.hg.hg_arena_bytes(ctypes.byref(self._hgcfg))

@@ -156,8 +156,9 @@ static void ground(const hg_cfg* cfg, const int16_t* hf, real x, real y, real* h
   real h00 = vs * hf[i * cfg->hf_cols + j], h10 = vs * hf[(i + 1) * cfg->hf_cols + j];
   real h01 = vs * hf[i * cfg->hf_cols + j + 1], h11 = vs * hf[(i + 1) * cfg->hf_cols + j + 1];
   real dhdx, dhdy;
-  if (u + v <= 1) { *h = h00 + u * (h10 - h00) + v * (h01 - h00); dhdx = (h10 - h00) / hs; dhdy = (h01 - h00) / hs; }
-  else { *h = h11 + (1 - u) * (h01 - h11) + (1 - v) * (h10 - h11); dhdx = (h11 - h01) / hs; dhdy = (h11 - h10) / hs; }
+  // cells split along the (i,j)-(i+1,j+1) diagonal, as convert_heightfield_to_trimesh tessellates
+  if (u >= v) { *h = h00 + u * (h10 - h00) + v * (h11 - h10); dhdx = (h10 - h00) / hs; dhdy = (h11 - h10) / hs; }
+  else { *h = h00 + v * (h01 - h00) + u * (h11 - h01); dhdx = (h11 - h01) / hs; dhdy = (h01 - h00) / hs; }
   real inv = 1 / sqrt(dhdx * dhdx + dhdy * dhdy + 1);
   n[0] = -dhdx * inv; n[1] = -dhdy * inv; n[2] = inv;
 }

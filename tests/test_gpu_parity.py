@@ -144,6 +144,15 @@ def _post_once(env, counter):
 def test_post_parity(env):
     """K_post (rewards, commands, push, termination, masked reset, obs + noise, stacking) vs
     the numpy pipeline on the identical GPU state, with forced resets/timeouts/resample/push."""
+    _post_parity(env)
+
+
+def test_post_parity_heightfield(terrain_env):
+    """Same on the heightfield terrain: resets land at the sub-terrain origins +- 1 m."""
+    _post_parity(terrain_env)
+
+
+def _post_parity(env):
     import pipeline_ref as PR
     for _ in range(3):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.5)
@@ -176,8 +185,8 @@ def test_post_parity(env):
 
 def _ref_sim(env, S, precision):
     import physics_ref as P
-    from humanoid import _native as N
-    sim = P.RefSim(env._hgcfg, env._model, env.num_envs, precision)
+    hf = env.height_samples.cpu().numpy() if getattr(env, "height_samples", None) is not None else None
+    sim = P.RefSim(env._hgcfg, env._model, env.num_envs, precision, heightfield=hf)
     sim.root[:] = S["root_states"]
     sim.q[:] = S["dof_pos"]
     sim.qd[:] = S["dof_vel"]
@@ -371,3 +380,35 @@ def test_ppo_graphed_update_matches_eager():
                                rtol=1e-5, atol=1e-7)
     for k in sd0:
         np.testing.assert_allclose(sd1[k].numpy(), sd0[k].numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.fixture(scope="module")
+def terrain_env():
+    _need_gpu()
+    return _make_env(N_ENVS, "v2", terrain__mesh_type="heightfield")
+
+
+def test_step_physics_parity_heightfield(terrain_env):
+    """K_step on the generated heightfield (config 3 terrain) vs the C reference simulator
+    colliding against the same int16 samples."""
+    env = terrain_env
+    assert env._hgcfg.terrain_type == 1 and tuple(env.height_samples.shape) == (2100, 2100)
+    for _ in range(30):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    S, _, _ = snapshot(env)
+    import pipeline_ref as PR
+    cfg = _oracle_cfg(env)
+    actions = torch.randn(env.num_envs, 12, device="cuda:0") * 0.5
+    a_ref = PR.preprocess_actions(cfg, actions.cpu().numpy(), S["actions"], 91)
+    _step_only(env, actions, 91)
+    g = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    r64, r32 = _ref_sim(env, S, "f64"), _ref_sim(env, S, "f32")
+    r64.step(a_ref)
+    r32.step(a_ref)
+    for name, gpu, a64, a32 in (("q", g(env.dof_pos), r64.q, r32.q), ("qd", g(env.dof_vel), r64.qd, r32.qd),
+                                ("root", g(env.root_states), r64.root, r32.root)):
+        tol = 20 * np.abs(a32 - a64) + 1e-3 * (1 + np.abs(a64))
+        bad = np.abs(gpu - a64) > tol
+        assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
+    # the robots stand on terrain: base heights follow the sub-terrain origins, not z = 0
+    assert np.isfinite(g(env.root_states)).all()
