@@ -50,7 +50,8 @@ int soa_rows(int id) {
     case HG_T_LAST_ROOT_VEL: return 6;
     case HG_T_COMMANDS: return 4;
     case HG_T_REW_BUF: case HG_T_RESET_BUF: case HG_T_TIME_OUT_BUF: case HG_T_EPISODE_LENGTH:
-    case HG_T_ENV_FRICTION: case HG_T_BODY_MASS: case HG_T_NONFINITE: return 1;
+    case HG_T_ENV_FRICTION: case HG_T_BODY_MASS: case HG_T_NONFINITE: case HG_T_TERRAIN_LEVEL:
+    case HG_T_TERRAIN_TYPE: return 1;
     case HG_T_EPISODE_SUMS: return HG_NUM_REWARDS;
     case HG_T_FEET_AIR_TIME: case HG_T_LAST_CONTACTS: case HG_T_FEET_HEIGHT: case HG_T_LAST_FEET_Z: return 2;
     case HG_T_PUSH_FORCE: case HG_T_PUSH_TORQUE: case HG_T_BASE_LIN_VEL: case HG_T_BASE_ANG_VEL:
@@ -63,7 +64,7 @@ int dtype_of(int id) {
   switch (id) {
     case HG_T_RESET_BUF: case HG_T_TIME_OUT_BUF: case HG_T_LAST_CONTACTS: return 2;
     case HG_T_EPISODE_LENGTH: return 1;
-    case HG_T_NONFINITE: return 3;
+    case HG_T_NONFINITE: case HG_T_TERRAIN_LEVEL: case HG_T_TERRAIN_TYPE: return 3;
     default: return 0;
   }
 }
@@ -154,6 +155,8 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   if (cfg->resample_interval <= 0 || cfg->push_interval <= 0) return fail(nullptr, HG_ERR_ARG, "bad intervals");
   if (cfg->terrain_type != 0 && (!cfg->heightfield || cfg->hf_rows < 2 || cfg->hf_cols < 2))
     return fail(nullptr, HG_ERR_ARG, "heightfield terrain needs a device heightfield");
+  if (cfg->curriculum && (!cfg->terrain_origins || cfg->terrain_rows < 1 || cfg->terrain_cols < 1))
+    return fail(nullptr, HG_ERR_ARG, "terrain curriculum needs the device terrain_origins table");
   Sim* s = new Sim();
   s->cfg = *cfg;
   s->model = *model;
@@ -214,6 +217,8 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   S.ep_stats = (float*)P(HG_T_EP_STATS);
   S.lambda = (float*)P(HG_T_CONTACT_LAMBDA);
   S.nonfinite = (int32_t*)P(HG_T_NONFINITE);
+  S.terrain_level = (int32_t*)P(HG_T_TERRAIN_LEVEL);
+  S.terrain_type = (int32_t*)P(HG_T_TERRAIN_TYPE);
   S.cfg = (const hg_cfg*)(s->arena + s->L.cfg);
   S.model = (const hg_model*)(s->arena + s->L.model);
   // zero the arena, upload cfg/model, initial state (synchronous: creation is not on the hot path)
@@ -353,6 +358,39 @@ extern "C" int hg_set_root_state_indexed(void* sim, const int32_t* env_ids, int 
   if (n == 0) return HG_OK;
   hipLaunchKernelGGL(k_set_root, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, s->S, env_ids, n, root);
   return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_root launch failed");
+}
+
+// ---- measured heights: one thread per (env, point)
+__global__ void k_heights(HgState S, const float* __restrict__ pts, int P, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)S.n * P) return;
+  const int e = (int)(t / P), k = (int)(t % P);
+  const hg_cfg* cfg = S.cfg;
+  if (cfg->terrain_type == 0 || cfg->heightfield == nullptr) { out[t] = 0.f; return; }
+  // quat_apply_yaw (utils/math.py:39-43): keep (z, w), normalise, rotate
+  const float qz = S.root[5 * S.np + e], qw = S.root[6 * S.np + e];
+  const float nrm = fmaxf(sqrtf(qz * qz + qw * qw), 1e-9f);
+  const f3 p = quat_apply(0.f, 0.f, qz / nrm, qw / nrm, mk(pts[2 * k], pts[2 * k + 1], 0.f));
+  const float x = p.x + S.root[0 * S.np + e] + cfg->hf_border;
+  const float y = p.y + S.root[1 * S.np + e] + cfg->hf_border;
+  long long px = (long long)(x / cfg->hf_horizontal_scale), py = (long long)(y / cfg->hf_horizontal_scale);
+  px = px < 0 ? 0 : (px > cfg->hf_rows - 2 ? cfg->hf_rows - 2 : px);
+  py = py < 0 ? 0 : (py > cfg->hf_cols - 2 ? cfg->hf_cols - 2 : py);
+  const int16_t* hf = cfg->heightfield;
+  const int C = cfg->hf_cols;
+  int h = hf[px * C + py];
+  h = min(h, (int)hf[(px + 1) * C + py]);
+  h = min(h, (int)hf[px * C + py + 1]);
+  out[t] = (float)h * cfg->hf_vertical_scale;
+}
+
+extern "C" int hg_measure_heights(void* sim, const float* points_xy, int num_points, float* out, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s || !points_xy || !out || num_points <= 0) return HG_ERR_ARG;
+  const int64_t total = (int64_t)s->S.n * num_points;
+  hipLaunchKernelGGL(k_heights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, s->S,
+                     points_xy, num_points, out);
+  return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_heights launch failed");
 }
 
 extern "C" const char* hg_version(void) { return "hg_sim 0.2 (gfx950, physics v2: 32 lanes/env, LDS-resident, Delassus PGS)"; }

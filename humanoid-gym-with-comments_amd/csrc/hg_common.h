@@ -54,6 +54,8 @@ struct HgState {
   float* ep_stats;        // [24] (+ accumulators [24] after)
   float* lambda;          // [60][np]
   int32_t* nonfinite;     // [np]
+  int32_t* terrain_level; // [np]
+  int32_t* terrain_type;  // [np]
   const hg_cfg* cfg;      // device copy
   const hg_model* model;  // device copy
 };
@@ -83,7 +85,7 @@ __host__ __device__ inline u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 
 enum HgRngPurpose : uint32_t {
   RNG_ACT_DELAY = 1, RNG_ACT_NOISE = 2, RNG_OBS_NOISE = 3, RNG_CMD = 4, RNG_PUSH = 5,
-  RNG_RESET_DOF = 6, RNG_RESET_ROOT = 7,
+  RNG_RESET_DOF = 6, RNG_RESET_ROOT = 7, RNG_TERRAIN = 8,
 };
 
 // uniform in [0,1): 24 high bits

@@ -77,6 +77,26 @@ __device__ void resample_commands(const hg_cfg* cfg, HgState& S, int e, uint64_t
 // reset_idx for one env (humanoid_env.py:1109-1163); episode stats accumulate into ep_stats[24..]
 __device__ void reset_env(const hg_cfg* cfg, HgState& S, int e, uint64_t step, int nrew) {
   const int np = S.np;
+  // _update_terrain_curriculum (humanoid_env.py:1075-1095), before the root reset reads the
+  // origin; skipped for the construction-time reset (step 0, the reference's init_done gate)
+  if (cfg->curriculum && step != 0) {
+    const float dx = S.root[0 * np + e] - S.env_origins[0 * np + e];
+    const float dy = S.root[1 * np + e] - S.env_origins[1 * np + e];
+    const float dist = sqrtf(dx * dx + dy * dy);
+    const float c0 = S.commands[0 * np + e], c1 = S.commands[1 * np + e];
+    const bool up = dist > cfg->terrain_env_length / 2;
+    const bool down = (dist < sqrtf(c0 * c0 + c1 * c1) * cfg->max_episode_length_s * 0.5f) && !up;
+    int lvl = S.terrain_level[e] + (up ? 1 : 0) - (down ? 1 : 0);
+    const int maxl = cfg->terrain_rows;
+    if (lvl >= maxl) {  // torch.randint_like(levels, max_terrain_level)
+      lvl = min((int)(u01(rng4(cfg, e, step, 0, RNG_TERRAIN).x) * (float)maxl), maxl - 1);
+    } else {
+      lvl = max(lvl, 0);
+    }
+    S.terrain_level[e] = lvl;
+    const float* o = cfg->terrain_origins + ((size_t)lvl * cfg->terrain_cols + S.terrain_type[e]) * 3;
+    for (int i = 0; i < 3; i++) S.env_origins[i * np + e] = o[i];
+  }
   // _reset_dofs
   for (int b = 0; b < 3; b++) {
     u4 r = rng4(cfg, e, step, b, RNG_RESET_DOF);

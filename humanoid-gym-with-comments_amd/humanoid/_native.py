@@ -63,6 +63,8 @@ class HgCfg(ctypes.Structure):
         ("reward_scale", f32 * HG_NUM_REWARDS),
         ("feet_body", i32 * 2), ("knee_body", i32 * 2), ("ref_idx", i32 * 6), ("yaw_roll_idx", i32 * 4),
         ("seed", ctypes.c_uint64),
+        ("curriculum", i32), ("terrain_rows", i32), ("terrain_cols", i32), ("terrain_env_length", f32),
+        ("max_episode_length_s", f32), ("_pad0", i32), ("terrain_origins", ctypes.c_void_p),
     ]
 
 
@@ -78,14 +80,14 @@ TENSOR_IDS = [
     "PRIV_BUF", "REW_BUF", "RESET_BUF", "TIME_OUT_BUF", "EPISODE_LENGTH", "EPISODE_SUMS",
     "FEET_AIR_TIME", "LAST_CONTACTS", "FEET_HEIGHT", "LAST_FEET_Z", "ENV_FRICTION", "BODY_MASS",
     "PUSH_FORCE", "PUSH_TORQUE", "BASE_LIN_VEL", "BASE_ANG_VEL", "PROJ_GRAVITY", "BASE_EULER",
-    "REF_DOF_POS", "ENV_ORIGINS", "EP_STATS", "CONTACT_LAMBDA", "NONFINITE",
+    "REF_DOF_POS", "ENV_ORIGINS", "EP_STATS", "CONTACT_LAMBDA", "NONFINITE", "TERRAIN_LEVEL", "TERRAIN_TYPE",
 ]
 T = {name: i for i, name in enumerate(TENSOR_IDS)}
 
 # every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
            "hg_post", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
-           "hg_gae_scan", "hg_gae_normalize", "hg_version"]
+           "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_version"]
 
 _LIB = None
 
@@ -120,6 +122,8 @@ def load_library(path=LIB_PATH):
     L.hg_set_dof_state_indexed.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp]
     L.hg_set_root_state_indexed.restype = ctypes.c_int
     L.hg_set_root_state_indexed.argtypes = [vp, vp, ctypes.c_int, vp, vp]
+    L.hg_measure_heights.restype = ctypes.c_int
+    L.hg_measure_heights.argtypes = [vp, vp, ctypes.c_int, vp, vp]
     L.hg_gae_scan.restype = ctypes.c_int
     L.hg_gae_scan.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                               ctypes.c_float, ctypes.c_int, vp]

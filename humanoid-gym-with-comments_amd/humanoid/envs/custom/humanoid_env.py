@@ -33,7 +33,8 @@ assert REWARD_NAMES == sorted(REWARD_NAMES)
 _TORCH_DTYPES = {0: torch.float32, 1: torch.int64, 2: torch.uint8, 3: torch.int32}
 
 
-def build_hg_cfg(cfg, num_envs, sim_dt, seed, model_js, heightfield=None, hf_shape=(0, 0)):
+def build_hg_cfg(cfg, num_envs, sim_dt, seed, model_js, heightfield=None, hf_shape=(0, 0), terrain_origins=None,
+                 terrain_shape=(0, 0)):
     """XBotLCfg -> hg_cfg (include/hgsim.h).  Returns (hg_cfg, aux dict)."""
     c = N.HgCfg()
     c.num_envs = num_envs
@@ -120,6 +121,12 @@ def build_hg_cfg(cfg, num_envs, sim_dt, seed, model_js, heightfield=None, hf_sha
     for k, n in enumerate(["left_leg_roll_joint", "left_leg_yaw_joint", "right_leg_roll_joint", "right_leg_yaw_joint"]):
         c.yaw_roll_idx[k] = idx[n]
     c.seed = seed & 0xFFFFFFFFFFFFFFFF
+    c.max_episode_length_s = cfg.env.episode_length_s
+    c.terrain_env_length = cfg.terrain.terrain_length
+    if terrain_origins is not None and cfg.terrain.curriculum:
+        c.curriculum = 1
+        c.terrain_rows, c.terrain_cols = terrain_shape
+        c.terrain_origins = terrain_origins
     aux = dict(feet=feet, knees=knees, dof_names=dofs, body_names=bodies, kp=kp, kd=kd, torque_limits=tl,
                default_dof_pos=dd, limits=limits, velocity=velocity, scales=scales)
     return c, aux
@@ -204,7 +211,12 @@ class XBotLFreeEnv(BaseTask):
         elif mesh is not None:
             raise ValueError("Terrain mesh type not recognised. Allowed types are [None, plane, heightfield, trimesh]")
         seed = int(getattr(self.cfg, "seed", 5))
-        self._hgcfg, self._aux = build_hg_cfg(self.cfg, self.num_envs, self.sim_dt, seed, js, hf_ptr, hf_shape)
+        to_ptr, to_shape = None, (0, 0)
+        if self.custom_origins:
+            self.terrain_origins = torch.from_numpy(self.terrain.env_origins).to(self.device).to(torch.float).contiguous()
+            to_ptr, to_shape = self.terrain_origins.data_ptr(), tuple(self.terrain_origins.shape[:2])
+        self._hgcfg, self._aux = build_hg_cfg(self.cfg, self.num_envs, self.sim_dt, seed, js, hf_ptr, hf_shape,
+                                              to_ptr, to_shape)
         nbytes = self.hg.hg_arena_bytes(ctypes.byref(self._hgcfg))
         self._arena = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
         off = (-self._arena.data_ptr()) % 256
@@ -282,12 +294,14 @@ class XBotLFreeEnv(BaseTask):
             max_init_level = self.cfg.terrain.max_init_terrain_level
             if not self.cfg.terrain.curriculum:
                 max_init_level = self.cfg.terrain.num_rows - 1
-            self.terrain_levels = torch.randint(0, max_init_level + 1, (self.num_envs,), device=self.device)
-            self.terrain_types = torch.div(torch.arange(self.num_envs, device=self.device),
-                                           (self.num_envs / self.cfg.terrain.num_cols), rounding_mode="floor").to(torch.long)
+            # levels/types live in the arena (int32): K_post's reset applies the curriculum
+            self.terrain_levels = self._view(N.T["TERRAIN_LEVEL"])
+            self.terrain_types = self._view(N.T["TERRAIN_TYPE"])
+            self.terrain_levels[:] = torch.randint(0, max_init_level + 1, (self.num_envs,), device=self.device).to(torch.int32)
+            self.terrain_types[:] = torch.div(torch.arange(self.num_envs, device=self.device),
+                                              (self.num_envs / self.cfg.terrain.num_cols), rounding_mode="floor").to(torch.int32)
             self.max_terrain_level = self.cfg.terrain.num_rows
-            self.terrain_origins = torch.from_numpy(self.terrain.env_origins).to(self.device).to(torch.float)
-            self.env_origins[:] = self.terrain_origins[self.terrain_levels, self.terrain_types]
+            self.env_origins[:] = self.terrain_origins[self.terrain_levels.long(), self.terrain_types.long()]
         else:
             num_cols = np.floor(np.sqrt(self.num_envs))
             num_rows = np.ceil(self.num_envs / num_cols)
@@ -330,8 +344,40 @@ class XBotLFreeEnv(BaseTask):
         self.base_init_state = torch.tensor(self.cfg.init_state.pos + self.cfg.init_state.rot + self.cfg.init_state.lin_vel
                                             + self.cfg.init_state.ang_vel, device=self.device)
         self.measured_heights = 0
+        if self.cfg.terrain.measure_heights:
+            self.height_points = self._init_height_points()
+            self._height_xy = self.height_points[0, :, :2].contiguous()
+            self.measured_heights = torch.zeros(self.num_envs, self.num_height_points, device=self.device)
         self.course_gain = 1.0   # read by OnPolicyRunner.learn (on_policy_runner.py:160-162)
         self.course_ratio = 1.0
+
+    def _init_height_points(self):
+        """Base-frame sample grid (humanoid_env.py:314-328): [N, P, 3], x-major meshgrid."""
+        y = torch.tensor(self.cfg.terrain.measured_points_y, device=self.device)
+        x = torch.tensor(self.cfg.terrain.measured_points_x, device=self.device)
+        grid_x, grid_y = torch.meshgrid(x, y, indexing="ij")
+        self.num_height_points = grid_x.numel()
+        points = torch.zeros(self.num_envs, self.num_height_points, 3, device=self.device)
+        points[:, :, 0] = grid_x.flatten()
+        points[:, :, 1] = grid_y.flatten()
+        return points
+
+    def _get_heights(self, env_ids=None):
+        """Terrain heights under the sample grid (humanoid_env.py:949-985) by the HIP kernel
+        hg_measure_heights: [N, P] (or [len(env_ids), P])."""
+        mesh = self.cfg.terrain.mesh_type
+        if mesh == "none":
+            raise NameError("Can't measure height with terrain mesh type 'none'")
+        if not hasattr(self, "height_points"):
+            self.height_points = self._init_height_points()
+            self._height_xy = self.height_points[0, :, :2].contiguous()
+        out = torch.empty(self.num_envs, self.num_height_points, device=self.device)
+        N.check(self.hg.hg_measure_heights(self.sim, ctypes.c_void_p(self._height_xy.data_ptr()),
+                                           self.num_height_points, ctypes.c_void_p(out.data_ptr()), self._stream()),
+                self.sim)
+        if env_ids is not None and len(env_ids) > 0:
+            return out[torch.as_tensor(env_ids, device=self.device, dtype=torch.long)]
+        return out
 
     # ------------------------------------------------------------------ buffers with reference semantics
     @property
@@ -401,6 +447,11 @@ class XBotLFreeEnv(BaseTask):
             kt.stop("k_step")
             kt.start("k_post")
         self.common_step_counter += 1
+        if self.cfg.terrain.measure_heights:
+            # _post_physics_step_callback (:1012-1013): after physics, before termination/reset
+            N.check(self.hg.hg_measure_heights(self.sim, ctypes.c_void_p(self._height_xy.data_ptr()),
+                                               self.num_height_points, ctypes.c_void_p(self.measured_heights.data_ptr()),
+                                               s), self.sim)
         N.check(self.hg.hg_post(self.sim, ctypes.c_uint64(self.common_step_counter), s), self.sim)
         if kt is not None:
             kt.stop("k_post")

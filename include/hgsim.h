@@ -103,6 +103,15 @@ typedef struct hg_cfg {
   int32_t ref_idx[6];                   /* left pitch,knee,ankle ; right pitch,knee,ankle dofs */
   int32_t yaw_roll_idx[4];              /* default_joint_pos reward dof indices */
   uint64_t seed;
+  /* terrain curriculum (_update_terrain_curriculum, humanoid_env.py:1075-1095); reset_idx
+   * applies it before the root reset when curriculum != 0 and the step counter is non-zero
+   * (the reference's init_done gate) */
+  int32_t curriculum;
+  int32_t terrain_rows, terrain_cols;   /* levels x types of terrain_origins */
+  float terrain_env_length;             /* move up when the robot walked > length / 2 */
+  float max_episode_length_s;           /* move down when it walked < |cmd_xy| * T_ep / 2 */
+  int32_t _pad0;
+  const float* terrain_origins;         /* device [rows, cols, 3], caller-owned */
 } hg_cfg;
 
 typedef struct hg_desc {
@@ -138,6 +147,8 @@ enum hg_tensor_id {
   HG_T_EP_STATS,         /* [22 + 2] episode reward means of the last resetting step, n_reset, any */
   HG_T_CONTACT_LAMBDA,   /* solver warm-start impulses [C*3 + D, N] */
   HG_T_NONFINITE,        /* [N] int32 count of non-finite recoveries */
+  HG_T_TERRAIN_LEVEL,    /* [N] int32 curriculum level (row of terrain_origins) */
+  HG_T_TERRAIN_TYPE,     /* [N] int32 terrain type (column of terrain_origins) */
   HG_T_COUNT
 };
 
@@ -170,6 +181,14 @@ int hg_reset_masked(void* sim, const uint8_t* mask, uint64_t counter, void* stre
 int hg_set_dof_state_indexed(void* sim, const int32_t* env_ids, int n, const float* dof_pos,
                              const float* dof_vel, void* stream);
 int hg_set_root_state_indexed(void* sim, const int32_t* env_ids, int n, const float* root, void* stream);
+
+/* ---- measured heights (replaces _get_heights, humanoid_env.py:949-985) ----
+ * points_xy: device f32 [P,2] sample points in the base frame (the _init_height_points grid,
+ * :314-328); out: device f32 [N,P].  Each point is yaw-rotated (quat_apply_yaw), offset by the
+ * base position, quantised to the heightfield grid ((p + border) / horizontal_scale, truncated,
+ * clipped to [0, rows-2] x [0, cols-2]) and reads min(h[i][j], h[i+1][j], h[i][j+1]) *
+ * vertical_scale.  Zeros on a plane (terrain_type 0), as the reference. */
+int hg_measure_heights(void* sim, const float* points_xy, int num_points, float* out, void* stream);
 
 /* ---- rollout storage: fused GAE (replaces RolloutStorage.compute_returns,
  * humanoid/algo/ppo/rollout_storage.py:122-143) ---- */

@@ -71,6 +71,21 @@ def reset_envs(cfg, S, rid, counter):
     c = cfg.c
     if len(rid) == 0:
         return
+    if c.curriculum and counter != 0:
+        # _update_terrain_curriculum (humanoid_env.py:1075-1095); S["terrain_origins"] is the
+        # host copy of the [rows, cols, 3] table
+        d = S["root_states"][rid, :2] - S["env_origins"][rid, :2]
+        dist = np.sqrt((d * d).sum(1, dtype=f32), dtype=f32)
+        cmd = S["commands"][rid, :2]
+        cn = np.sqrt((cmd * cmd).sum(1, dtype=f32), dtype=f32)
+        up = dist > f32(c.terrain_env_length) / f32(2)
+        down = (dist < cn * f32(c.max_episode_length_s) * f32(0.5)) & ~up
+        lvl = S["terrain_levels"][rid].astype(np.int64) + up.astype(np.int64) - down.astype(np.int64)
+        maxl = int(c.terrain_rows)
+        rnd = np.minimum((R.u01(R.rng4(cfg.seed, rid, counter, 0, R.TERRAIN)[0]) * f32(maxl)).astype(np.int64), maxl - 1)
+        lvl = np.where(lvl >= maxl, rnd, np.maximum(lvl, 0))
+        S["terrain_levels"][rid] = lvl
+        S["env_origins"][rid] = S["terrain_origins"][lvl, S["terrain_types"][rid]]
     u = np.concatenate([np.stack(R.rng4(cfg.seed, rid, counter, b, R.RESET_DOF), 1) for b in range(3)], 1)
     S["dof_pos"][rid] = cfg.default[None, :] + f32(0.2) * R.u01(u) + f32(-0.1)
     S["dof_vel"][rid] = 0

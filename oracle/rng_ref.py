@@ -12,7 +12,7 @@ M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
 W0, W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
 MASK = np.uint64(0xFFFFFFFF)
 
-ACT_DELAY, ACT_NOISE, OBS_NOISE, CMD, PUSH, RESET_DOF, RESET_ROOT = 1, 2, 3, 4, 5, 6, 7
+ACT_DELAY, ACT_NOISE, OBS_NOISE, CMD, PUSH, RESET_DOF, RESET_ROOT, TERRAIN = 1, 2, 3, 4, 5, 6, 7, 8
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):

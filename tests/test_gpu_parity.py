@@ -77,6 +77,10 @@ def snapshot(env):
              lambda_=g(env._view(__import__("humanoid._native", fromlist=["T"]).T["CONTACT_LAMBDA"])),
              base_lin_vel=g(env.base_lin_vel), base_ang_vel=g(env.base_ang_vel))
     S["lambda"] = S.pop("lambda_")
+    if getattr(env, "custom_origins", False):
+        S["terrain_levels"] = g(env.terrain_levels).astype(np.int64)
+        S["terrain_types"] = g(env.terrain_types).astype(np.int64)
+        S["terrain_origins"] = g(env.terrain_origins)
     from humanoid.envs.custom.humanoid_env import REWARD_NAMES
     S["episode_sums"] = {n: g(env._sums[k]) for k, n in enumerate(REWARD_NAMES)}
     return S, g(env.obs_buf), g(env.privileged_obs_buf)
@@ -385,7 +389,7 @@ def test_ppo_graphed_update_matches_eager():
 @pytest.fixture(scope="module")
 def terrain_env():
     _need_gpu()
-    return _make_env(N_ENVS, "v2", terrain__mesh_type="heightfield")
+    return _make_env(N_ENVS, "v2", terrain__mesh_type="heightfield", terrain__measure_heights=True)
 
 
 def test_step_physics_parity_heightfield(terrain_env):
@@ -412,3 +416,71 @@ def test_step_physics_parity_heightfield(terrain_env):
         assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
     # the robots stand on terrain: base heights follow the sub-terrain origins, not z = 0
     assert np.isfinite(g(env.root_states)).all()
+
+
+def _heights_ref(root, hs_samples, pts_xy, border, hscale, vscale):
+    """torch-CPU restatement of _get_heights (humanoid_env.py:949-985) + quat_apply_yaw."""
+    q = root[:, 3:7].clone()
+    q[:, :2] = 0.0
+    q = q / q.norm(dim=-1, keepdim=True).clamp(min=1e-9)
+    P = pts_xy.shape[0]
+    v = torch.cat([pts_xy, torch.zeros(P, 1)], dim=1).unsqueeze(0).expand(root.shape[0], P, 3).reshape(-1, 3)
+    qq = q.repeat_interleave(P, dim=0)
+    xyz = qq[:, :3]
+    t = torch.cross(xyz, v, dim=-1) * 2
+    pts = (v + qq[:, 3:] * t + torch.cross(xyz, t, dim=-1)).view(root.shape[0], P, 3) + root[:, :3].unsqueeze(1)
+    pts = pts + border
+    pts = (pts / hscale).long()
+    px = pts[:, :, 0].reshape(-1).clip(0, hs_samples.shape[0] - 2)
+    py = pts[:, :, 1].reshape(-1).clip(0, hs_samples.shape[1] - 2)
+    h = torch.min(torch.min(hs_samples[px, py], hs_samples[px + 1, py]), hs_samples[px, py + 1])
+    return h.view(root.shape[0], -1).float() * vscale
+
+
+def test_measured_heights(terrain_env):
+    env = terrain_env
+    for _ in range(5):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    h = env._get_heights().cpu()
+    ref = _heights_ref(env.root_states.cpu(), env.height_samples.cpu().long(), env._height_xy.cpu(),
+                       env.cfg.terrain.border_size, env.cfg.terrain.horizontal_scale, env.cfg.terrain.vertical_scale)
+    assert h.shape == (env.num_envs, 187)
+    exact = (h == ref).float().mean().item()
+    assert exact > 0.999, exact  # cell-boundary float ties aside, bit-exact
+    assert (h - ref).abs().max().item() <= 0.1
+    sub = env._get_heights(env_ids=[3, 5]).cpu()
+    torch.testing.assert_close(sub, h[[3, 5]])
+
+
+def test_terrain_curriculum_parity():
+    """Curriculum on: resets move robots that walked > 4 m one level up, robots that walked less
+    than |cmd| * T_ep / 2 one level down, past-the-top levels re-drawn (Philox), origins follow
+    (humanoid_env.py:1075-1095); against the numpy pipeline on the same state."""
+    _need_gpu()
+    import pipeline_ref as PR
+    env = _make_env(N_ENVS, "v2", terrain__mesh_type="heightfield", terrain__curriculum=True)
+    assert env._hgcfg.curriculum == 1
+    for _ in range(3):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    torch.cuda.synchronize()
+    n = 16
+    env.contact_forces[0:n, 0, 2] = 50.0                          # terminate envs 0..15
+    env.root_states[0:4, 0] = env.env_origins[0:4, 0] + 5.0        # walked far: level up
+    env.terrain_levels[2:4] = env.cfg.terrain.num_rows - 1         # ... past the top: re-draw
+    env.root_states[4:8, :2] = env.env_origins[4:8, :2]            # stood still ...
+    env.commands[4:8, 0] = 0.5                                     # ... under a command: level down
+    env.terrain_levels[6:8] = 0                                    # ... already at 0: clip
+    counter = 777
+    S, hist_o, hist_p = snapshot(env)
+    cfg = _oracle_cfg(env)
+    lv0 = S["terrain_levels"].copy()
+    obs, priv, rew, reset, timeout, terms = PR.post(cfg, S, counter, hist_o, hist_p)
+    _post_once(env, counter)
+    gpu = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    assert reset[:n].all()
+    np.testing.assert_array_equal(gpu(env.terrain_levels), S["terrain_levels"])
+    np.testing.assert_allclose(gpu(env.env_origins), S["env_origins"], rtol=0, atol=0)
+    np.testing.assert_allclose(gpu(env.root_states), S["root_states"], rtol=1e-6, atol=1e-6)
+    lv = S["terrain_levels"]
+    assert (lv[0:2] == lv0[0:2] + 1).all() and (lv[4:6] == lv0[4:6] - 1).all() and (lv[6:8] == 0).all()
+    assert ((lv[2:4] >= 0) & (lv[2:4] < env.cfg.terrain.num_rows)).all()
