@@ -484,3 +484,38 @@ def test_terrain_curriculum_parity():
     lv = S["terrain_levels"]
     assert (lv[0:2] == lv0[0:2] + 1).all() and (lv[4:6] == lv0[4:6] - 1).all() and (lv[6:8] == 0).all()
     assert ((lv[2:4] >= 0) & (lv[2:4] < env.cfg.terrain.num_rows)).all()
+
+
+def test_train_checkpoint_resume_export(tmp_path):
+    """Caller path of train.py / play.py: task_registry.make_env + make_alg_runner, learn with
+    logging and checkpoints, resume through get_load_path, export TorchScript + ONNX."""
+    _need_gpu()
+    import os
+    from humanoid.envs import XBotLCfgPPO  # noqa: F401  (registers humanoid_ppo)
+    from humanoid.utils import get_args, task_registry
+    from humanoid.utils.helpers import export_policy_as_jit, get_load_path
+    from humanoid.utils.onnx_io import export_policy_as_onnx, load_onnx_mlp
+    args = get_args(["--num_envs", "64", "--max_iterations", "2", "--headless", "--run_name", "t"])
+    env, _ = task_registry.make_env("humanoid_ppo", args=args)
+    _, tcfg = task_registry.get_cfgs("humanoid_ppo")
+    tcfg.runner.num_steps_per_env = 8
+    runner, tcfg = task_registry.make_alg_runner(env, args=args, train_cfg=tcfg, log_root=str(tmp_path))
+    runner.learn(2, init_at_random_ep_len=True)
+    ckpt = get_load_path(str(tmp_path))
+    assert ckpt.endswith("model_2.pt") and os.path.exists(ckpt)
+    logs = os.listdir(os.path.dirname(ckpt))
+    assert any(f.startswith("events") or f.endswith(".jsonl") for f in logs), logs
+    sd = {k: v.clone() for k, v in runner.alg.actor_critic.state_dict().items()}
+    args2 = get_args(["--num_envs", "64", "--headless", "--resume"])
+    runner2, _ = task_registry.make_alg_runner(env, args=args2, train_cfg=tcfg, log_root=str(tmp_path))
+    for k, v in runner2.alg.actor_critic.state_dict().items():
+        torch.testing.assert_close(v, sd[k])
+    assert runner2.current_learning_iteration == 2
+    out = tmp_path / "exported"
+    export_policy_as_jit(runner2.alg.actor_critic, str(out))
+    export_policy_as_onnx(runner2.alg.actor_critic, str(out))
+    policy = runner2.get_inference_policy(device="cuda:0")
+    obs = env.get_observations()
+    m = load_onnx_mlp(str(out / "policy.onnx")).to("cuda:0")
+    with torch.no_grad():
+        torch.testing.assert_close(m(obs), policy(obs), rtol=1e-5, atol=1e-5)
