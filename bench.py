@@ -11,10 +11,12 @@ no checkpoint), all physics/env inputs resident in HBM.
 Multi-GPU: one process per GPU (torch.distributed.run), envs sharded (4096 per rank, weak
 scaling), policy gradients all-reduced with RCCL (backend "nccl") once per minibatch.
 
-The roofline object is for the dominant kernel, K_step (FP32 VALU bound: state lives in
-registers/scratch across the 10 substeps, HBM traffic is ~1.5 KB/env-step); its launch time is
-measured with HIP events recorded on the stream the kernel runs on (torch's current stream,
-which the env passes to hg_step).  cpu_baseline times the oracle port (C reference physics,
+The roofline object is for the dominant kernel, K_step (FP32 bound, VALU + f32 MFMA: state lives
+in registers/LDS across the 10 substeps, algorithmic HBM traffic ~1.8 KB/env-step); its launch
+time is measured with HIP events recorded on the stream the kernel runs on (torch's current
+stream, which the env passes to hg_step).  ``traffic`` is the HBM bytes per K_step launch from
+the committed rocprofv3 PMC passes (profiles/<round>/pmc_summary.json: FETCH_SIZE doubled per
+MI355X_MICROARCH.md + WRITE_SIZE), for the same workload.  cpu_baseline times the oracle port (C reference physics,
 numpy env logic, torch-CPU PPO) on a bounded sample on the host cores.
 """
 import argparse
@@ -32,6 +34,17 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) dense peak
 HBM_PEAK_GBS = 8000.0
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_v3", "pmc_summary.json")
+
+
+def pmc_traffic(kernel="k_step2"):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (None if absent)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)[kernel]
+        return int(d["hbm_bytes_per_launch_corrected"]), os.path.relpath(PMC_SUMMARY, REPO)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 class KernelTimer:
@@ -210,12 +223,15 @@ def main():
     env_steps = args.envs * args.T * args.steps * world
     value = env_steps / elapsed
     rows = active_rows(env)
+    traffic, traffic_src = pmc_traffic("k_step2") if args.envs == 4096 and args.terrain == "plane" else (None, None)
     ms_step = timer.mean_ms("k_step")
     flops = physics_flops_per_env_step(rows) * args.envs
     achieved_tflops = flops / (ms_step * 1e-3) / 1e12
     roofline = {"kernel": "k_step", "bound": "mfma", "pipe": "fp32-valu (f32 MFMA peak = f32 vector peak)",
                 "achieved": round(achieved_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 6), "traffic": None,
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": 1808 * args.envs,
                 "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
                 "flops_per_launch": flops, "active_rows_per_env": round(rows, 2),
                 "k_post_avg_ms": round(timer.mean_ms("k_post"), 4)}

@@ -205,7 +205,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   __shared__ EnvSh shm[2];
   const int half = threadIdx.x >> 5;
   const int l = threadIdx.x & 31;
-  const int e_raw = blockIdx.x * 2 + half;
+  // XCD-aware env mapping: workgroups are dispatched round-robin over the 8 XCDs (block b ->
+  // XCD b % 8), each with its own L2.  Giving every XCD a contiguous range of env pairs keeps the
+  // 16 envs of one 64-byte SoA line on one L2, so their 4-byte state stores merge there instead of
+  // being written back as 8 partial lines from 8 caches.
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
+  const int pair = xcd * (nb >> 3) + min(xcd, nb & 7) + kx;
+  const int e_raw = pair * 2 + half;
   const bool valid = e_raw < S.n;
   const int e = valid ? e_raw : S.n - 1;
   EnvSh& E = shm[half];
