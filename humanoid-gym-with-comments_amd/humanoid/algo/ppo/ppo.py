@@ -23,6 +23,7 @@ import torch.nn.functional as F
 import torch.optim as optim
 
 from .actor_critic import ActorCritic
+from .hg_adam import HgAdam
 from .rollout_storage import RolloutStorage
 
 
@@ -57,9 +58,8 @@ class PPO:
             with torch.no_grad():
                 for p in self._params:
                     dist.broadcast(p.data, src=0)
-        if self.world_size > 1 or self._on_device:
-            # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack
-            # copies; fixed gradient addresses for the captured update graph
+        if self.world_size > 1:
+            # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack copies
             numel = sum(p.numel() for p in self._params)
             self._flat_grad = torch.zeros(numel, device=self._params[0].device, dtype=torch.float32)
             off = 0
@@ -71,7 +71,8 @@ class PPO:
             # Adam kernel reads
             self._lr_t = torch.tensor(float(learning_rate), dtype=torch.float64, device=device)
             self._lr_f32 = self._lr_t.float()
-            self.optimizer = optim.Adam(self._params, lr=self._lr_f32, fused=True, capturable=True)
+            # fused clip + Adam HIP kernel (csrc/hg_optim.hip); torch.optim.Adam state layout
+            self.optimizer = HgAdam(self._params, lr=self._lr_f32)
         else:
             self._lr_t = None
             self.optimizer = optim.Adam(self._params, lr=learning_rate)
@@ -232,6 +233,15 @@ class PPO:
                 + self.sym_coef * sym_loss + self.base_lin_vel_coef * base_lin_vel_loss)
         return loss, value_loss, surrogate_loss, base_lin_vel_loss, sym_loss
 
+    def _clip_and_step(self):
+        """clip_grad_norm_(params, max_grad_norm); optimizer.step() (ppo.py:212-214) — one fused
+        HIP launch pair on the device."""
+        if isinstance(self.optimizer, HgAdam):
+            self.optimizer.step(max_norm=self.max_grad_norm)
+        else:
+            nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
+            self.optimizer.step()
+
     def update(self):
         if self._on_device and self.use_graphs:
             return self._update_graphed()
@@ -260,8 +270,7 @@ class PPO:
             else:
                 self.optimizer.zero_grad()
                 loss.backward()
-            nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
-            self.optimizer.step()
+            self._clip_and_step()
             if self._on_device:
                 acc = torch.stack([value_loss.detach(), surrogate_loss.detach(), base_lin_vel_loss.detach()])
                 sums = acc if sums is None else sums + acc
@@ -290,7 +299,8 @@ class PPO:
     # ------------------------------------------------------------------------------------------
     def _storage_key(self):
         st = self.storage
-        return (st.observations.data_ptr(), st.num_envs, st.num_transitions_per_env)
+        return (st.observations.data_ptr(), st.num_envs, st.num_transitions_per_env,
+                getattr(self.optimizer, "version", 0))
 
     def _capture(self, mb):
         st = self.storage
@@ -306,8 +316,11 @@ class PPO:
         self._kl = torch.zeros((), dtype=torch.float32, device=dev)
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         torch.cuda.synchronize(dev)
+        if self._flat_grad is None:
+            self.optimizer.zero_grad(set_to_none=True)  # backward allocates the grads in the graph pool
         with torch.cuda.graph(ga):
-            self._flat_grad.zero_()
+            if self._flat_grad is not None:
+                self._flat_grad.zero_()
             i = self._idx
             b = {k: v[i] for k, v in flat.items()}
             loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
@@ -323,8 +336,7 @@ class PPO:
                 self._kl.div_(self.world_size)
             if self._adaptive:
                 self._lr_rule_device(self._kl)
-            nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
-            self.optimizer.step()
+            self._clip_and_step()
         self._graphs = (ga, gb, mb, self._storage_key())
 
     def _update_graphed(self):

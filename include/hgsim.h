@@ -38,6 +38,7 @@ extern "C" {
 #define HG_MAX_DOF 12
 #define HG_MAX_CONTACTS 16
 #define HG_NUM_REWARDS 22
+#define HG_MAX_TENSORS 32
 
 /* Articulated model table (output of tools/urdf_compile.py; replaces gym.load_asset +
  * get_asset_* queries, humanoid_env.py:455-470).  Body 0 is the floating base; body b>=1 is
@@ -203,6 +204,29 @@ int hg_gae_scan(const float* rewards, const uint8_t* dones, const float* values,
  * `count` elements (count = T*N*world_size after an all-reduce of stats). */
 int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int64_t n_local,
                      void* stream);
+
+/* ---- PPO optimizer: fused global-norm clip + Adam (replaces
+ * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----
+ * A list of float32 device tensors (param, grad, Adam exp_avg / exp_avg_sq, per-tensor step
+ * counter as a 1-float device scalar), split into fixed chunks of hg_adam_chunk() elements:
+ * chunk_start[t] = first chunk of tensor t, chunk_start[count] = total chunks. */
+typedef struct hg_tensor_list {
+  int32_t count;
+  int32_t _pad;
+  float* param[HG_MAX_TENSORS];
+  const float* grad[HG_MAX_TENSORS];
+  float* exp_avg[HG_MAX_TENSORS];
+  float* exp_avg_sq[HG_MAX_TENSORS];
+  float* step[HG_MAX_TENSORS];
+  int64_t numel[HG_MAX_TENSORS];
+  int32_t chunk_start[HG_MAX_TENSORS + 1];
+} hg_tensor_list;
+/* lr: device float (read at run time, so a device-side LR schedule needs no host round trip);
+ * max_norm <= 0 disables clipping; partial: device scratch of chunk_start[count] floats.
+ * Deterministic (fixed-order reductions); two launches; graph-capturable. */
+int hg_adam_step(const hg_tensor_list* tensors, const float* lr, float beta1, float beta2, float eps,
+                 float max_norm, float* partial, void* stream);
+int hg_adam_chunk(void);
 
 /* library build info */
 const char* hg_version(void);

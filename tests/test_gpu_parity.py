@@ -519,3 +519,36 @@ def test_train_checkpoint_resume_export(tmp_path):
     m = load_onnx_mlp(str(out / "policy.onnx")).to("cuda:0")
     with torch.no_grad():
         torch.testing.assert_close(m(obs), policy(obs), rtol=1e-5, atol=1e-5)
+
+
+def test_hg_adam_matches_torch_clip_adam():
+    """hg_adam_step (fused global-norm clip + Adam, csrc/hg_optim.hip) == clip_grad_norm_ +
+    torch.optim.Adam over several steps, including steps where clipping is active; state dicts
+    interchange with torch.optim.Adam."""
+    _need_gpu()
+    from humanoid.algo.ppo.hg_adam import HgAdam
+    g = torch.Generator(device="cpu").manual_seed(3)
+    shapes = [(512, 705), (512,), (256, 512), (256,), (12, 128), (12,), (12,)]
+    init = [torch.randn(*s, generator=g) * 0.1 for s in shapes]
+    grads = [[torch.randn(*s, generator=g) * sc for s in shapes] for sc in (0.001, 0.5, 0.01, 2.0)]
+    lr = torch.tensor(3e-4, device="cuda:0")
+    pa = [torch.nn.Parameter(x.clone().cuda()) for x in init]
+    pb = [torch.nn.Parameter(x.clone().cuda()) for x in init]
+    oa = HgAdam(pa, lr=lr)
+    ob = torch.optim.Adam(pb, lr=3e-4, foreach=False)
+    for gs in grads:
+        for p, x in zip(pa, gs):
+            p.grad = x.cuda()
+        for p, x in zip(pb, gs):
+            p.grad = x.cuda()
+        oa.step(max_norm=1.0)
+        torch.nn.utils.clip_grad_norm_(pb, 1.0)
+        ob.step()
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-7)
+    sa = oa.state_dict()
+    assert set(sa["state"][0]) == {"step", "exp_avg", "exp_avg_sq"} and float(sa["state"][0]["step"]) == 4
+    oc = HgAdam([torch.nn.Parameter(x.clone().cuda()) for x in init], lr=lr)
+    oc.load_state_dict(ob.state_dict())
+    assert oc.version == 1
+    torch.testing.assert_close(oc.state_dict()["state"][0]["exp_avg"], ob.state_dict()["state"][0]["exp_avg"])
