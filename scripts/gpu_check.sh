@@ -10,6 +10,13 @@ rc=$?
 echo "pytest rc=$rc"
 tail -30 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -z "$SKIP_DP" ]; then
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29512 scripts/dp_check.py > gpurun_out/dp_check.log 2>&1
+  drc=$?
+  echo "dp_check rc=$drc"; grep "dp_check" gpurun_out/dp_check.log | tail -2
+  if [ $drc -ne 0 ]; then tail -30 gpurun_out/dp_check.log; exit $drc; fi
+fi
 if [ -n "$SKIP_BENCH" ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 brc=$?
