@@ -93,7 +93,7 @@ def active_rows(env):
     return float((3 * contacts + limits).mean().item())
 
 
-def make_env(num_envs, device, seed, terrain="plane"):
+def make_env(num_envs, device, seed, terrain="plane", push_curriculum=False):
     from humanoid.envs import XBotLCfg
     from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
     from humanoid.utils.helpers import SimParams
@@ -102,14 +102,17 @@ def make_env(num_envs, device, seed, terrain="plane"):
     cfg.seed = seed
     cfg.terrain.mesh_type = terrain
     cfg.terrain.seed = 5  # identical heightfield on every rank
+    cfg.domain_rand.push_curriculum = push_curriculum
     return XBotLFreeEnv(cfg, SimParams(), "hg_sim", device, True)
 
 
-def train_cfg(T):
+def train_cfg(T, policy_dtype="fp32", obs_dtype="fp32"):
     from humanoid.envs import XBotLCfgPPO
     from humanoid.utils.helpers import class_to_dict
     t = XBotLCfgPPO()
     t.runner.num_steps_per_env = T
+    t.policy.policy_dtype = policy_dtype
+    t.runner.storage_obs_dtype = obs_dtype
     return class_to_dict(t)
 
 
@@ -186,8 +189,16 @@ def main():
     ap.add_argument("--no-gemm-table", action="store_true", help="hipBLASLt default GEMM heuristics")
     ap.add_argument("--terrain", default="plane", choices=["plane", "heightfield"],
                     help="plane = config 2; heightfield = config 3 (2100x2100 generated terrain)")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
+                    help="BASELINE.json configs: 2 plane (default), 3 heightfield, 5 push-recovery curriculum "
+                         "with 8192 envs/GPU, fp16 observation storage and a bf16 policy")
     args = ap.parse_args()
 
+    if args.config == 3:
+        args.terrain = "heightfield"
+    c5 = args.config == 5
+    if c5 and args.envs == 4096:
+        args.envs = 8192
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -200,8 +211,9 @@ def main():
     from humanoid.algo.ppo import OnPolicyRunner
     from humanoid.utils.blas_tuning import use_tuned_gemms
     tuned = use_tuned_gemms() if not args.no_gemm_table else False
-    env = make_env(args.envs, device, seed=5 + rank, terrain=args.terrain)
-    runner = OnPolicyRunner(env, train_cfg(args.T), log_dir=None, device=device)
+    env = make_env(args.envs, device, seed=5 + rank, terrain=args.terrain, push_curriculum=c5)
+    runner = OnPolicyRunner(env, train_cfg(args.T, "bf16" if c5 else "fp32", "fp16" if c5 else "fp32"),
+                            log_dir=None, device=device)
     timer = KernelTimer()
     env.kernel_timer = timer
     runner.learn(args.warmup, init_at_random_ep_len=True)
@@ -223,7 +235,8 @@ def main():
     env_steps = args.envs * args.T * args.steps * world
     value = env_steps / elapsed
     rows = active_rows(env)
-    traffic, traffic_src = pmc_traffic("k_step2") if args.envs == 4096 and args.terrain == "plane" else (None, None)
+    traffic, traffic_src = (pmc_traffic("k_step2") if args.envs == 4096 and args.terrain == "plane" and not c5
+                            else (None, None))
     ms_step = timer.mean_ms("k_step")
     flops = physics_flops_per_env_step(rows) * args.envs
     achieved_tflops = flops / (ms_step * 1e-3) / 1e12
@@ -239,8 +252,11 @@ def main():
         "metric": "env-steps/sec (whole node) at 4096 envs + PPO iters/sec, 1/2/4/8 MI355X",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ppo_iters_per_sec": round(args.steps / elapsed, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": ("XBot-L flat terrain, 4096 envs/GPU, PPO 24-step rollout (BASELINE configs[1])"
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32 physics + bf16 policy" if c5 else "f32", "data": "synthetic",
+        "config": {"workload": (f"XBot-L push-recovery curriculum, {args.envs} envs/GPU, fp16 obs storage + bf16 "
+                                "policy, PPO 24-step rollout (config 5)" if c5 else
+                                "XBot-L flat terrain, 4096 envs/GPU, PPO 24-step rollout (BASELINE configs[1])"
                                 if args.terrain == "plane" else
                                 "XBot-L heightfield terrain 2100x2100, 4096 envs/GPU, PPO 24-step rollout (config 3)"),
                    "envs_per_gpu": args.envs, "num_steps_per_env": args.T, "parallelism": f"dp{world}",

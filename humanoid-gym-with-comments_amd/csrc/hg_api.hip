@@ -314,6 +314,24 @@ int hg_post(void* sim, uint64_t common_step_counter, void* stream) {
   return do_post(s, common_step_counter, 0, nullptr, stream);
 }
 
+int hg_update_cfg(void* sim, const hg_cfg* cfg, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s || !cfg) return HG_ERR_ARG;
+  const hg_cfg& o = s->cfg;
+  if (cfg->num_envs != o.num_envs || cfg->frame_stack != o.frame_stack || cfg->c_frame_stack != o.c_frame_stack ||
+      cfg->decimation != o.decimation || cfg->terrain_type != o.terrain_type || cfg->hf_rows != o.hf_rows ||
+      cfg->hf_cols != o.hf_cols || cfg->heightfield != o.heightfield || cfg->terrain_origins != o.terrain_origins ||
+      cfg->terrain_rows != o.terrain_rows || cfg->terrain_cols != o.terrain_cols)
+    return fail(s, HG_ERR_ARG, "hg_update_cfg: layout fields cannot change after hg_create");
+  if (cfg->pgs_iterations < 0 || cfg->pgs_iterations > 1000 || !(cfg->sim_dt > 0.f))
+    return fail(s, HG_ERR_ARG, "hg_update_cfg: bad solver parameters");
+  s->cfg = *cfg;
+  // the device copy is read by every launch; the host source stays valid (it is the handle's)
+  if (hipMemcpyAsync((void*)s->S.cfg, &s->cfg, sizeof(hg_cfg), hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess)
+    return fail(s, HG_ERR_HIP, "hg_update_cfg: copy failed");
+  return HG_OK;
+}
+
 int hg_reset_masked(void* sim, const uint8_t* mask, uint64_t counter, void* stream) {
   Sim* s = (Sim*)sim;
   if (!s) return HG_ERR_ARG;

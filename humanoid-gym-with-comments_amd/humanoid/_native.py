@@ -86,7 +86,7 @@ T = {name: i for i, name in enumerate(TENSOR_IDS)}
 
 # every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
-           "hg_post", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
+           "hg_post", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_version"]
 
 _LIB = None
@@ -116,6 +116,8 @@ def load_library(path=LIB_PATH):
     L.hg_step.argtypes = [vp, vp, ctypes.c_uint64, vp]
     L.hg_post.restype = ctypes.c_int
     L.hg_post.argtypes = [vp, ctypes.c_uint64, vp]
+    L.hg_update_cfg.restype = ctypes.c_int
+    L.hg_update_cfg.argtypes = [vp, ctypes.POINTER(HgCfg), vp]
     L.hg_reset_masked.restype = ctypes.c_int
     L.hg_reset_masked.argtypes = [vp, vp, ctypes.c_uint64, vp]
     L.hg_set_dof_state_indexed.restype = ctypes.c_int

@@ -57,7 +57,11 @@ def _mlp(in_dim, hidden, out_dim, activation):
 class ActorCritic(nn.Module):
     def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=[256, 256, 256],
                  critic_hidden_dims=[256, 256, 256], base_lin_vel_hidden_dims=[128, 128], init_noise_std=1.0,
-                 activation=nn.ELU(), **kwargs):
+                 activation=nn.ELU(), policy_dtype="fp32", **kwargs):
+        """policy_dtype "bf16" (config 5): the three MLPs run under bf16 autocast on the GPU
+        (fp32 master weights and gradients, outputs returned as fp32); "fp32" is the reference."""
+        if policy_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"policy_dtype must be 'fp32' or 'bf16', got {policy_dtype!r}")
         if kwargs:
             print("ActorCritic.__init__ got unexpected arguments, which will be ignored: " + str(list(kwargs)))
         super().__init__()
@@ -69,6 +73,13 @@ class ActorCritic(nn.Module):
         print(f"Critic MLP: {self.critic}")
         self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
         self.distribution = None
+        self.policy_dtype = policy_dtype
+
+    def _mlp(self, net, x):
+        if self.policy_dtype == "bf16" and x.is_cuda:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return net(x).float()
+        return net(x if x.dtype == torch.float32 else x.float())
 
     @staticmethod
     def init_weights(sequential, scales):
@@ -94,7 +105,7 @@ class ActorCritic(nn.Module):
         return self.distribution.entropy().sum(dim=-1)
 
     def update_distribution(self, observations):
-        mean = self.actor(observations)
+        mean = self._mlp(self.actor, observations)
         self.distribution = _DiagGaussian(mean, mean * 0.0 + self.std)
 
     def act(self, observations, **kwargs):
@@ -105,10 +116,10 @@ class ActorCritic(nn.Module):
         return self.distribution.log_prob(actions).sum(dim=-1)
 
     def act_inference(self, observations):
-        return self.actor(observations)
+        return self._mlp(self.actor, observations)
 
     def evaluate(self, critic_observations, **kwargs):
-        return self.critic(critic_observations)
+        return self._mlp(self.critic, critic_observations)
 
     def base_get_lin_vel(self, observations):
-        return self.base_lin_vel(observations)
+        return self._mlp(self.base_lin_vel, observations)

@@ -64,8 +64,9 @@ class OnPolicyRunner:
         self.alg = alg_cls(actor_critic, device=self.device, **self.alg_cfg)
         self.num_steps_per_env = self.cfg["num_steps_per_env"]
         self.save_interval = self.cfg["save_interval"]
+        obs_dtype = {"fp32": torch.float32, "fp16": torch.float16}[self.cfg.get("storage_obs_dtype", "fp32")]
         self.alg.init_storage(env.num_envs, self.num_steps_per_env, [env.num_obs], [env.num_privileged_obs],
-                              [env.num_actions])
+                              [env.num_actions], obs_dtype=obs_dtype)
         self.log_dir = log_dir if _rank() == 0 else None
         self.writer = None
         self.tot_timesteps = 0
@@ -92,6 +93,8 @@ class OnPolicyRunner:
         cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
         tot_iter = self.current_learning_iteration + num_learning_iterations
         for it in range(self.current_learning_iteration, tot_iter):
+            if hasattr(self.env, "update_push_curriculum"):
+                self.env.update_push_curriculum(it)
             start = time.time()
             with torch.inference_mode():
                 for _ in range(self.num_steps_per_env):

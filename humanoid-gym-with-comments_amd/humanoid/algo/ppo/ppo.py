@@ -121,9 +121,10 @@ class PPO:
             for g in self.optimizer.param_groups:
                 g["lr"] = self._lr
 
-    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape,
+                     obs_dtype=torch.float32):
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
-                                      action_shape, self.device)
+                                      action_shape, self.device, obs_dtype=obs_dtype)
 
     def test_mode(self):
         self.actor_critic.eval()
@@ -228,7 +229,7 @@ class PPO:
         if self.sym_loss:
             mirror_act = ac.actor(torch.matmul(obs_b, self.obs_perm_mat))
             sym_loss = (mu_b - torch.matmul(mirror_act, self.act_perm_mat)).pow(2).mean()
-        base_lin_vel_loss = F.mse_loss(est_lin_vel, lin_vel_b)
+        base_lin_vel_loss = F.mse_loss(est_lin_vel, lin_vel_b.float())
         loss = (surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean()
                 + self.sym_coef * sym_loss + self.base_lin_vel_coef * base_lin_vel_loss)
         return loss, value_loss, surrogate_loss, base_lin_vel_loss, sym_loss

@@ -33,7 +33,10 @@ class RolloutStorage:
             self.__init__()
 
     def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, actions_shape,
-                 device="cpu"):
+                 device="cpu", obs_dtype=torch.float32):
+        """obs_dtype float16 (config 5) halves the observation buffers, the largest part of the
+        storage (705 + 219 floats per env-step); minibatches are handed out in that dtype and the
+        policy consumes them under autocast."""
         self.device = device
         self.obs_shape = obs_shape
         self.privileged_obs_shape = privileged_obs_shape
@@ -43,8 +46,10 @@ class RolloutStorage:
         def z(*shape, dtype=torch.float32):
             return torch.zeros(T, N, *shape, device=device, dtype=dtype)
 
-        self.observations = z(*obs_shape)
-        self.privileged_observations = z(*privileged_obs_shape) if privileged_obs_shape[0] is not None else None
+        self.obs_dtype = obs_dtype
+        self.observations = z(*obs_shape, dtype=obs_dtype)
+        self.privileged_observations = (z(*privileged_obs_shape, dtype=obs_dtype)
+                                        if privileged_obs_shape[0] is not None else None)
         self.rewards = z(1)
         self.actions = z(*actions_shape)
         self.dones = z(1, dtype=torch.uint8)

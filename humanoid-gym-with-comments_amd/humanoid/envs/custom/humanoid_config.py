@@ -154,6 +154,12 @@ class XBotLCfg(BaseConfig):
         push_interval_s = 4
         max_push_vel_xy = 0.2
         max_push_ang_vel = 0.4
+        # push-recovery curriculum (BUILD-DEFINED, config 5; the reference only has fixed pushes,
+        # humanoid_env.py:665-681): push magnitudes ramp linearly with the PPO iteration
+        push_curriculum = False
+        push_curriculum_iterations = 1000
+        max_push_vel_xy_final = 1.0
+        max_push_ang_vel_final = 1.0
         dynamic_randomization = 0.02
 
     class commands:
@@ -229,6 +235,7 @@ class XBotLCfgPPO(BaseConfig):
         init_noise_std = 1.0
         actor_hidden_dims = [512, 256, 128]
         critic_hidden_dims = [768, 256, 128]
+        policy_dtype = "fp32"      # "bf16": MLPs under bf16 autocast (config 5)
 
     class algorithm:
         value_loss_coef = 1.0
@@ -248,6 +255,7 @@ class XBotLCfgPPO(BaseConfig):
         policy_class_name = "ActorCritic"
         algorithm_class_name = "PPO"
         num_steps_per_env = 60
+        storage_obs_dtype = "fp32"  # "fp16": observation buffers of the rollout storage (config 5)
         max_iterations = 3001
         save_interval = 100
         experiment_name = "XBot_ppo"

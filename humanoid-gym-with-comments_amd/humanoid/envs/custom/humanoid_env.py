@@ -421,6 +421,22 @@ class XBotLFreeEnv(BaseTask):
             "time_outs": self.time_out_buf,
         }
 
+    def update_push_curriculum(self, iteration):
+        """Push-recovery curriculum (config 5, BUILD-DEFINED): max push velocities ramp linearly
+        from the configured values to *_final over push_curriculum_iterations PPO iterations.
+        Called by OnPolicyRunner.learn once per iteration; no-op unless enabled."""
+        dr = self.cfg.domain_rand
+        if not getattr(dr, "push_curriculum", False):
+            return
+        f = min(1.0, max(0.0, iteration / max(1, int(dr.push_curriculum_iterations))))
+        vxy = dr.max_push_vel_xy + f * (dr.max_push_vel_xy_final - dr.max_push_vel_xy)
+        vang = dr.max_push_ang_vel + f * (dr.max_push_ang_vel_final - dr.max_push_ang_vel)
+        if (self._hgcfg.max_push_vel_xy, self._hgcfg.max_push_ang_vel) != (np.float32(vxy), np.float32(vang)):
+            self._hgcfg.max_push_vel_xy = vxy
+            self._hgcfg.max_push_ang_vel = vang
+            N.check(self.hg.hg_update_cfg(self.sim, ctypes.byref(self._hgcfg), self._stream()), self.sim)
+        self.push_scale = (float(self._hgcfg.max_push_vel_xy), float(self._hgcfg.max_push_ang_vel))
+
     def _launch_reset(self, mask_u8):
         mp = ctypes.c_void_p(mask_u8.data_ptr()) if mask_u8 is not None else None
         N.check(self.hg.hg_reset_masked(self.sim, mp, ctypes.c_uint64(self.common_step_counter), self._stream()),

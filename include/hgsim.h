@@ -174,6 +174,10 @@ int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream
  * (:654-657): derived state, commands, push, termination, rewards, masked reset, observations.
  * common_step_counter is the reference's host-side counter (:781). */
 int hg_post(void* sim, uint64_t common_step_counter, void* stream);
+/* Runtime parameter update (curricula, e.g. the push-recovery ramp of config 5): copies *cfg into
+ * the handle and, stream-ordered, into the device copy the kernels read.  Fields that size or
+ * lay out the arena (num_envs, frame stacks, terrain tables, decimation) must be unchanged. */
+int hg_update_cfg(void* sim, const hg_cfg* cfg, void* stream);
 /* replaces reset_idx() (humanoid_env.py:1109-1163) for an explicit device mask [N] (u8). */
 int hg_reset_masked(void* sim, const uint8_t* mask, uint64_t counter, void* stream);
 

@@ -552,3 +552,34 @@ def test_hg_adam_matches_torch_clip_adam():
     oc.load_state_dict(ob.state_dict())
     assert oc.version == 1
     torch.testing.assert_close(oc.state_dict()["state"][0]["exp_avg"], ob.state_dict()["state"][0]["exp_avg"])
+
+
+def test_config5_bf16_policy_fp16_storage_push_curriculum():
+    """Config 5 pieces: push-recovery curriculum through hg_update_cfg (pushes reach the ramped
+    1.0 m/s bound, post still matches the oracle with the updated cfg), bf16-autocast policy and
+    fp16 observation storage through two captured PPO iterations."""
+    _need_gpu()
+    import pipeline_ref as PR
+    from humanoid.algo.ppo import OnPolicyRunner
+    import bench
+    env = _make_env(N_ENVS, "v2", domain_rand__push_curriculum=True)
+    env.update_push_curriculum(0)
+    assert abs(env._hgcfg.max_push_vel_xy - 0.2) < 1e-6
+    env.update_push_curriculum(10 ** 6)
+    assert abs(env._hgcfg.max_push_vel_xy - 1.0) < 1e-6 and abs(env._hgcfg.max_push_ang_vel - 1.0) < 1e-6
+    for _ in range(2):
+        env.step(torch.zeros(env.num_envs, 12, device="cuda:0"))
+    counter = int(env._hgcfg.push_interval) * 7
+    S, hist_o, hist_p = snapshot(env)
+    obs, priv, rew, reset, timeout, _ = PR.post(_oracle_cfg(env), S, counter, hist_o, hist_p)
+    _post_once(env, counter)
+    v = env.root_states[:, 7:9].cpu().numpy()
+    np.testing.assert_allclose(v, S["root_states"][:, 7:9], rtol=1e-6, atol=1e-6)
+    assert np.abs(v).max() > 0.2 and np.abs(v).max() <= 1.0 + 1e-6
+    runner = OnPolicyRunner(env, bench.train_cfg(8, "bf16", "fp16"), log_dir=None, device="cuda:0")
+    assert runner.alg.storage.observations.dtype == torch.float16
+    assert runner.alg.actor_critic.policy_dtype == "bf16"
+    runner.learn(3, init_at_random_ep_len=True)
+    st = runner.last_iteration_stats
+    assert np.isfinite(st["value_loss"]) and np.isfinite(st["surrogate_loss"])
+    assert all(torch.isfinite(p).all() for p in runner.alg.actor_critic.parameters())
