@@ -131,6 +131,7 @@ def cpu_baseline(n_envs=256, T=24, threads=None):
     threads = threads or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     os.environ["OMP_NUM_THREADS"] = str(threads)
+    P.set_threads(threads)
     cfg = XBotLCfg()
     model, js = N.load_model(armature=cfg.sim.hg.armature)
     hc, _ = build_hg_cfg(cfg, n_envs, cfg.sim.dt, 5, js)
@@ -184,7 +185,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--T", type=int, default=24, help="rollout length (num_steps_per_env)")
-    ap.add_argument("--cpu-envs", type=int, default=256)
+    ap.add_argument("--cpu-envs", type=int, default=4096, help="CPU baseline sample on all host threads")
+    ap.add_argument("--cpu-envs-1core", type=int, default=256, help="CPU baseline sample on one thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-table", action="store_true", help="hipBLASLt default GEMM heuristics")
     ap.add_argument("--terrain", default="plane", choices=["plane", "heightfield"],
@@ -268,8 +270,14 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         v, threads, dt = cpu_baseline(args.cpu_envs, args.T)
+        v1, _, dt1 = cpu_baseline(args.cpu_envs_1core, args.T, threads=1)
         result["cpu_baseline"] = {"value": round(v, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-                                  "sample": f"1 PPO iteration, {args.cpu_envs} envs x {args.T} steps, {dt:.1f} s"}
+                                  "sample": f"1 PPO iteration, {args.cpu_envs} envs x {args.T} steps, {dt:.1f} s "
+                                            f"(oracle physics + numpy env logic + torch-CPU PPO)",
+                                  "value_1_core": round(v1, 1),
+                                  "sample_1_core": f"1 PPO iteration, {args.cpu_envs_1core} envs x {args.T} steps, "
+                                                   f"{dt1:.1f} s"}
+        torch.set_num_threads(threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -35,6 +35,9 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../include/hgsim.h"
 
@@ -580,3 +583,14 @@ int API(ref_dynamics)(const hg_model* hm, const real* root, const real* q, const
 }
 
 int API(ref_lamw)(void) { return LAMW; }
+
+/* host threads of the OpenMP env loop (bench.py cpu_baseline: all cores, then one core) */
+#ifndef REF_FLOAT
+void ref_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+#endif

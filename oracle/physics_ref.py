@@ -31,6 +31,11 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def set_threads(n):
+    """OpenMP threads of the C reference's env loop."""
+    lib().ref_set_threads(ctypes.c_int(int(n)))
+
+
 class RefSim:
     """AoS CPU simulator state for n envs (root[n,13], q/qd[n,12], warm-start lambdas)."""
 
