@@ -37,6 +37,15 @@ HBM_PEAK_GBS = 8000.0
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_v3", "pmc_summary.json")
 
 
+def sq_issue(kernel_file=os.path.join(REPO, "profiles", "r1_v3", "sq_counters_k_step2.json")):
+    """SIMD VALU issue utilisation of K_step from the committed SQ counter passes (None if absent)."""
+    try:
+        with open(kernel_file) as f:
+            return json.load(f)["simd_valu_busy_est"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def pmc_traffic(kernel="k_step2"):
     """HBM bytes per launch of `kernel` from the committed PMC summary (None if absent)."""
     try:
@@ -247,6 +256,10 @@ def main():
                 "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": 1808 * args.envs,
+                "hbm_achieved_GBs": round(1808 * args.envs / (ms_step * 1e-3) / 1e9, 1),
+                "hbm_frac": round(1808 * args.envs / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "valu_issue_util": sq_issue(),
+                "valu_issue_source": "profiles/r1_v3/sq_counters_k_step2.json (2 x SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES)",
                 "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
                 "flops_per_launch": flops, "active_rows_per_env": round(rows, 2),
                 "k_post_avg_ms": round(timer.mean_ms("k_post"), 4)}
