@@ -114,3 +114,71 @@ extern "C" int hg_adam_step(const hg_tensor_list* T, const float* lr, float beta
 }
 
 extern "C" int hg_adam_chunk(void) { return CHUNK; }
+
+// ---------------------------------------------------------------------------------------------
+// Adaptive-KL learning rate (ppo.py:162-176): one launch for the KL mean, one for the rule, so
+// the schedule stays on the device (and inside the captured update graph).
+//   kl_row = sum_a [ log(s/s_old + 1e-5) + (s_old^2 + (m_old - m)^2) / (2 s^2) - 0.5 ]
+//   kl     = mean_rows kl_row           (row sums in fp32 in action order; per-block then final
+//                                        fp64 sums in a fixed order: deterministic)
+//   lr     = kl > 2d ? max(lr/1.5, lr_min) : (0 < kl < d/2 ? min(lr*1.5, lr_max) : lr)   (fp64)
+// ---------------------------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) k_kl_partial(const float* __restrict__ mu, const float* __restrict__ sigma,
+                                                   const float* __restrict__ old_mu,
+                                                   const float* __restrict__ old_sigma, int64_t rows, int A,
+                                                   double* __restrict__ partial) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double acc = 0.0;
+  if (r < rows) {
+    float s = 0.f;
+    for (int a = 0; a < A; a++) {
+      const int64_t i = r * A + a;
+      const float sg = sigma[i], so = old_sigma[i], d = old_mu[i] - mu[i];
+      s += logf(sg / so + 1.0e-5f) + (so * so + d * d) / (2.0f * (sg * sg)) - 0.5f;
+    }
+    acc = (double)s;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  __shared__ double ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (ws[0] + ws[1]) + (ws[2] + ws[3]);
+}
+
+__global__ void __launch_bounds__(64) k_kl_final(const double* __restrict__ partial, int nb, int64_t rows,
+                                                 float* __restrict__ kl_out) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 64) acc += partial[i];
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (threadIdx.x == 0) *kl_out = (float)(acc / (double)rows);
+}
+
+__global__ void k_lr_rule(const float* __restrict__ kl, double* __restrict__ lr64, float* __restrict__ lr32,
+                          double desired, double lr_min, double lr_max) {
+  const double k = (double)*kl;
+  double lr = *lr64;
+  if (k > desired * 2.0) lr = fmax(lr / 1.5, lr_min);
+  else if (k < desired / 2.0 && k > 0.0) lr = fmin(lr * 1.5, lr_max);
+  *lr64 = lr;
+  *lr32 = (float)lr;
+}
+}  // namespace
+
+extern "C" int hg_kl_mean(const float* mu, const float* sigma, const float* old_mu, const float* old_sigma,
+                          int64_t rows, int num_actions, float* kl_out, double* scratch, void* stream) {
+  if (!mu || !sigma || !old_mu || !old_sigma || !kl_out || !scratch || rows <= 0 || num_actions <= 0)
+    return HG_ERR_ARG;
+  const int nb = (int)((rows + 255) / 256);
+  hipLaunchKernelGGL(k_kl_partial, dim3(nb), dim3(256), 0, (hipStream_t)stream, mu, sigma, old_mu, old_sigma, rows,
+                     num_actions, scratch);
+  hipLaunchKernelGGL(k_kl_final, dim3(1), dim3(64), 0, (hipStream_t)stream, scratch, nb, rows, kl_out);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+extern "C" int hg_kl_lr_rule(const float* kl, double* lr64, float* lr32, double desired_kl, double lr_min,
+                             double lr_max, void* stream) {
+  if (!kl || !lr64 || !lr32) return HG_ERR_ARG;
+  hipLaunchKernelGGL(k_lr_rule, dim3(1), dim3(1), 0, (hipStream_t)stream, kl, lr64, lr32, desired_kl, lr_min, lr_max);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

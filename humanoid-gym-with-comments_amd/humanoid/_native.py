@@ -87,7 +87,8 @@ T = {name: i for i, name in enumerate(TENSOR_IDS)}
 # every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
            "hg_post", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
-           "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_version"]
+           "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
+           "hg_version"]
 
 _LIB = None
 
@@ -131,6 +132,10 @@ def load_library(path=LIB_PATH):
                               ctypes.c_float, ctypes.c_int, vp]
     L.hg_gae_normalize.restype = ctypes.c_int
     L.hg_gae_normalize.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64, vp]
+    L.hg_kl_mean.restype = ctypes.c_int
+    L.hg_kl_mean.argtypes = [vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp]
+    L.hg_kl_lr_rule.restype = ctypes.c_int
+    L.hg_kl_lr_rule.argtypes = [vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.hg_adam_chunk.restype = ctypes.c_int
     L.hg_adam_chunk.argtypes = []
     L.hg_version.restype = ctypes.c_char_p

@@ -16,6 +16,8 @@ the fused Adam kernel as a tensor; the three loss means are accumulated on the d
 once per update.  The host therefore never waits for the GPU inside the minibatch loop.  On the
 CPU the reference's host-side arithmetic is kept verbatim (this is what the golden tests pin).
 """
+import ctypes
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -159,7 +161,20 @@ class PPO:
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         self.storage.compute_returns(last_values, self.gamma, self.lam)
 
-    def _kl_mean(self, mu, sigma, old_mu, old_sigma):
+    def _kl_mean(self, mu, sigma, old_mu, old_sigma, out=None):
+        if self._on_device:
+            # one HIP launch (csrc/hg_optim.hip k_kl_mean) instead of ~13 elementwise kernels
+            from humanoid import _native as N
+            out = torch.empty((), dtype=torch.float32, device=mu.device) if out is None else out
+            t = [x.detach().contiguous() for x in (mu, sigma, old_mu, old_sigma)]
+            rows, A = t[0].shape[0], t[0].shape[-1]
+            nb = (rows + 255) // 256
+            if getattr(self, "_kl_scratch", None) is None or self._kl_scratch.numel() < nb:
+                self._kl_scratch = torch.empty(nb, dtype=torch.float64, device=mu.device)
+            s = ctypes.c_void_p(torch.cuda.current_stream(mu.device).cuda_stream)
+            N.check(N.lib().hg_kl_mean(*[ctypes.c_void_p(x.data_ptr()) for x in t], ctypes.c_int64(rows), A,
+                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self._kl_scratch.data_ptr()), s))
+            return out
         with torch.inference_mode():
             kl = torch.sum(torch.log(sigma / old_sigma + 1.0e-5)
                            + (torch.square(old_sigma) + torch.square(old_mu - mu)) / (2.0 * torch.square(sigma))
@@ -169,15 +184,10 @@ class PPO:
     def _lr_rule_device(self, kl_mean):
         """The reference's adaptive rule (ppo.py:168-176) in float64 on the device (kl promoted
         exactly as Python promotes kl_mean.item())."""
-        with torch.inference_mode():
-            k = kl_mean.double()
-            lr = self._lr_t
-            down = torch.clamp_min(lr / 1.5, 1e-5)
-            up = torch.clamp_max(lr * 1.5, 1e-2)
-            new = torch.where(k > self.desired_kl * 2.0, down,
-                              torch.where((k < self.desired_kl / 2.0) & (k > 0.0), up, lr))
-            self._lr_t.copy_(new)
-            self._lr_f32.copy_(new)
+        from humanoid import _native as N
+        s = ctypes.c_void_p(torch.cuda.current_stream(self._lr_t.device).cuda_stream)
+        N.check(N.lib().hg_kl_lr_rule(ctypes.c_void_p(kl_mean.data_ptr()), ctypes.c_void_p(self._lr_t.data_ptr()),
+                                      ctypes.c_void_p(self._lr_f32.data_ptr()), float(self.desired_kl), 1e-5, 1e-2, s))
 
     def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
         kl_mean = self._kl_mean(mu, sigma, old_mu, old_sigma)
@@ -328,7 +338,7 @@ class PPO:
                 b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"], b["logp"])
             if self._adaptive:
                 ac = self.actor_critic
-                self._kl.copy_(self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"]))
+                self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
             self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
             loss.backward()
         with torch.cuda.graph(gb, pool=ga.pool()):

@@ -231,6 +231,15 @@ typedef struct hg_tensor_list {
 int hg_adam_step(const hg_tensor_list* tensors, const float* lr, float beta1, float beta2, float eps,
                  float max_norm, float* partial, void* stream);
 int hg_adam_chunk(void);
+/* Adaptive-KL learning rate (replaces the kl/lr block of ppo.py:162-176 on the device):
+ * hg_kl_mean writes mean_rows sum_a KL(N(old_mu, old_sigma) || N(mu, sigma)) (the reference's
+ * expression, with its 1e-5 inside the log) over [rows, num_actions] row-major inputs;
+ * hg_kl_lr_rule applies lr /= 1.5 (floor lr_min) above 2*desired_kl, lr *= 1.5 (cap lr_max) in
+ * (0, desired_kl/2), in float64 on lr64 and mirrors it into lr32.  Three launches in all. */
+int hg_kl_mean(const float* mu, const float* sigma, const float* old_mu, const float* old_sigma, int64_t rows,
+               int num_actions, float* kl_out, double* scratch /* >= ceil(rows/256) doubles */, void* stream);
+int hg_kl_lr_rule(const float* kl, double* lr64, float* lr32, double desired_kl, double lr_min, double lr_max,
+                  void* stream);
 
 /* library build info */
 const char* hg_version(void);

@@ -5,7 +5,11 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=${STEPS:-5}
-timeout -k 10 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+if [ -n "$PYTEST_K" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} -k "$PYTEST_K" > gpurun_out/pytest_gpu.log 2>&1
+else
+  timeout -k 10 900 python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+fi
 rc=$?
 echo "pytest rc=$rc"
 tail -30 gpurun_out/pytest_gpu.log

@@ -583,3 +583,31 @@ def test_config5_bf16_policy_fp16_storage_push_curriculum():
     st = runner.last_iteration_stats
     assert np.isfinite(st["value_loss"]) and np.isfinite(st["surrogate_loss"])
     assert all(torch.isfinite(p).all() for p in runner.alg.actor_critic.parameters())
+
+
+def test_kl_mean_and_lr_rule_kernels():
+    """hg_kl_mean == the reference KL expression (ppo.py:162-166) in fp64; hg_kl_lr_rule == the
+    Python schedule (ppo.py:168-176) bit for bit in float64 for kl above, inside and below the band."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    from test_ppo_golden import SMALL
+    ppo = PPO(ActorCritic(**SMALL), learning_rate=1e-3, schedule="adaptive", desired_kl=0.01, device="cuda:0")
+    g = torch.Generator().manual_seed(7)
+    mu, omu = torch.randn(3000, 12, generator=g), torch.randn(3000, 12, generator=g) * 0.1
+    sg, osg = torch.rand(3000, 12, generator=g) + 0.3, torch.rand(3000, 12, generator=g) + 0.3
+    ref = (torch.log(sg.double() / osg.double() + 1e-5) + (osg.double() ** 2 + (omu.double() - mu.double()) ** 2)
+           / (2 * sg.double() ** 2) - 0.5).sum(-1).mean().item()
+    kl = ppo._kl_mean(mu.cuda(), sg.cuda(), omu.cuda(), osg.cuda())
+    assert abs(kl.item() - ref) <= 1e-5 * abs(ref)
+    lr = 1e-3
+    for k in (0.5, 0.03, 0.015, 0.004, 0.0, -1.0, 0.001, 1e3, 1e3, 1e3, 1e3, 1e3, 1e3, 1e3, 1e3, 1e3, 1e3,
+              1e3, 1e3, 1e3, 1e3, 1e3, 1e-4, 1e-4):
+        kt = torch.tensor(k, dtype=torch.float32, device="cuda:0")
+        ppo._lr_rule_device(kt)
+        kf = float(np.float32(k))
+        if kf > 0.02:
+            lr = max(1e-5, lr / 1.5)
+        elif kf < 0.005 and kf > 0.0:
+            lr = min(1e-2, lr * 1.5)
+        assert ppo.learning_rate == lr, (k, ppo.learning_rate, lr)
+        assert ppo._lr_f32.item() == np.float32(lr)
