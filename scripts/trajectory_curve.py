@@ -1,0 +1,60 @@
+"""SURVEY 8(d) parity trajectory: 1000 policy steps (10,000 substeps), seed 5, open-loop actions
+a_t[j] = 0.5 sin(2 pi t 0.01 / 0.64 + j pi / 6), DR and noise off; HIP K_step vs the CPU reference
+(oracle/physics_ref.c) in f64, with the CPU f32-vs-f64 divergence as the yardstick.  Writes the
+per-step max |dq| and |dtau| curves (variant A fixed base, variant B floating base on the plane)."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(REPO, "humanoid-gym-with-comments_amd"), os.path.join(REPO, "oracle"), REPO,
+          os.path.join(REPO, "tests")):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import test_gpu_parity as T  # noqa: E402  (helpers only: _make_env, snapshot, _ref_sim, _step_only)
+
+
+def run(fixed, steps, n=16):
+    import pipeline_ref as PR
+    env = T._make_env(n, "v2", asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
+                      domain_rand__push_robots=False, noise__add_noise=False)
+    S, _, _ = T.snapshot(env)
+    oc = T._oracle_cfg(env)
+    r64, r32 = T._ref_sim(env, S, "f64"), T._ref_sim(env, S, "f32")
+    prev = np.zeros((n, 12), np.float32)
+    j = np.arange(12)
+    out = {"gpu_vs_f64_q": [], "gpu_vs_f64_tau": [], "f32_vs_f64_q": [], "f32_vs_f64_tau": []}
+    for t in range(steps):
+        a = np.tile(0.5 * np.sin(2 * np.pi * t * 0.01 / 0.64 + j * np.pi / 6), (n, 1)).astype(np.float32)
+        a_ref = PR.preprocess_actions(oc, a, prev, t)
+        T._step_only(env, torch.from_numpy(a).cuda(), t)
+        prev = env.actions.cpu().numpy()
+        r64.step(a_ref.astype(np.float64))
+        r32.step(a_ref)
+        q, tau = env.dof_pos.cpu().numpy(), env.torques.cpu().numpy()
+        out["gpu_vs_f64_q"].append(float(np.abs(q - r64.q).max()))
+        out["gpu_vs_f64_tau"].append(float(np.abs(tau - r64.torques).max()))
+        out["f32_vs_f64_q"].append(float(np.abs(r32.q - r64.q).max()))
+        out["f32_vs_f64_tau"].append(float(np.abs(r32.torques - r64.torques).max()))
+    return out
+
+
+def main():
+    steps = int(os.environ.get("STEPS", 1000))
+    res = {"spec": "SURVEY 8(d) parity trajectory, 16 envs, seed 5, DR/noise off", "steps": steps}
+    for name, fixed in (("A_fixed_base", True), ("B_floating_base", False)):
+        c = run(fixed, steps)
+        res[name] = {k: [round(x, 9) for x in v] for k, v in c.items()}
+        res[name + "_summary"] = {k: {"max": max(v), "at_100": v[min(99, steps - 1)], "final": v[-1]}
+                                  for k, v in c.items()}
+        print(name, json.dumps(res[name + "_summary"]), flush=True)
+    out = os.environ.get("OUT", os.path.join(REPO, "gpurun_out", "trajectory_curve.json"))
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    with open(out, "w") as f:
+        json.dump(res, f)
+
+
+if __name__ == "__main__":
+    main()
