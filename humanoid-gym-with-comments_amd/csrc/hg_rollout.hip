@@ -1,0 +1,120 @@
+// hg_rollout.hip — fused rollout-storage writes of the PPO collection loop (gfx950).
+//
+// Replaces, per policy step, the elementwise tail of PPO.act + RolloutStorage.add_transitions
+// (humanoid/algo/ppo/ppo.py:116-138, rollout_storage.py:83-100): ~25 small launches become two.
+//   hg_rollout_act (before env.step): a = mu + sigma * z, z ~ N(0,1) (Philox, Box–Muller);
+//     log p(a) = sum_j [ -(a_j - mu_j)^2 / (2 sigma_j^2) - log sigma_j - log sqrt(2 pi) ]
+//     (torch.distributions.Normal.log_prob summed over actions); writes actions, log-prob, mu,
+//     sigma, value into slot t of the storage, and copies the observation / critic observation
+//     rows into slot t (fp32 or fp16 storage) in the same launch.
+//   hg_rollout_env (after env.step): rewards[t] = r + gamma * V * time_out (the time-out
+//     bootstrap of ppo.py:132-133), dones[t] = reset.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "hg_common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr uint32_t RNG_ACTION_SAMPLE = 9;
+
+__device__ inline u4 philox_key(uint64_t seed, uint32_t env, uint64_t step, uint32_t block) {
+  u4 c = {env, (uint32_t)step, (block & 0xFFFFu) | ((uint32_t)(step >> 32) << 16), RNG_ACTION_SAMPLE};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+template <typename OT>
+__device__ inline void store_obs(OT* dst, float v);
+template <>
+__device__ inline void store_obs<float>(float* dst, float v) { *dst = v; }
+template <>
+__device__ inline void store_obs<__half>(__half* dst, float v) { *dst = __float2half(v); }
+
+template <typename OT>
+__global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, const float* __restrict__ std,
+                                            const float* __restrict__ value, const float* __restrict__ obs,
+                                            const float* __restrict__ cobs, int n, int A, int64_t obs_w,
+                                            int64_t cobs_w, float* __restrict__ act_out, float* __restrict__ logp_out,
+                                            float* __restrict__ mu_out, float* __restrict__ sigma_out,
+                                            float* __restrict__ value_out, OT* __restrict__ obs_out,
+                                            OT* __restrict__ cobs_out, uint64_t seed, uint64_t counter,
+                                            int env_blocks) {
+  if ((int)blockIdx.x < env_blocks) {
+    const int e = blockIdx.x * TPB + threadIdx.x;
+    if (e >= n) return;
+    const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
+    float lp = 0.f;
+    float z4[4];
+    for (int j = 0; j < A; j++) {
+      if ((j & 3) == 0) normals4(philox_key(seed, (uint32_t)e, counter, (uint32_t)(j >> 2)), z4);
+      const float m = mean[(size_t)e * A + j], s = std[j];
+      const float a = m + s * z4[j & 3];
+      const float d = a - m;
+      lp += -(d * d) / (2.0f * (s * s)) - logf(s) - c;
+      act_out[(size_t)e * A + j] = a;
+      mu_out[(size_t)e * A + j] = m;
+      sigma_out[(size_t)e * A + j] = s;
+    }
+    logp_out[e] = lp;
+    value_out[e] = value[e];
+    return;
+  }
+  // observation rows -> storage slot (grid-stride over both tables)
+  const int64_t tot_o = (int64_t)n * obs_w, tot_c = (int64_t)n * cobs_w;
+  const int64_t stride = (int64_t)(gridDim.x - env_blocks) * TPB;
+  for (int64_t i = (int64_t)(blockIdx.x - env_blocks) * TPB + threadIdx.x; i < tot_o + tot_c; i += stride) {
+    if (i < tot_o) store_obs<OT>(obs_out + i, obs[i]);
+    else store_obs<OT>(cobs_out + (i - tot_o), cobs[i - tot_o]);
+  }
+}
+
+__global__ void __launch_bounds__(TPB) k_env(const float* __restrict__ rew, const uint8_t* __restrict__ reset,
+                                            const uint8_t* __restrict__ time_out, const float* __restrict__ values,
+                                            int n, float gamma, float* __restrict__ rew_out,
+                                            uint8_t* __restrict__ dones_out) {
+  const int e = blockIdx.x * TPB + threadIdx.x;
+  if (e >= n) return;
+  float r = rew[e];
+  if (time_out) r += gamma * (values[e] * (float)time_out[e]);
+  rew_out[e] = r;
+  dones_out[e] = reset[e];
+}
+
+}  // namespace
+
+extern "C" int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
+                              const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
+                              int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
+                              float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out,
+                              int obs_fp16, uint64_t seed, uint64_t counter, void* stream) {
+  if (!mean || !std || !value || !obs || !actions_out || !logp_out || !mu_out || !sigma_out || !value_out ||
+      !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 ||
+      (critic_obs_width > 0 && (!critic_obs || !critic_obs_out)))
+    return HG_ERR_ARG;
+  const int env_blocks = (num_envs + TPB - 1) / TPB;
+  const int copy_blocks = 512;
+  hipStream_t s = (hipStream_t)stream;
+  if (obs_fp16)
+    hipLaunchKernelGGL(k_act<__half>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
+                       critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
+                       actions_out, logp_out, mu_out, sigma_out, value_out, (__half*)obs_out,
+                       (__half*)critic_obs_out, seed, counter, env_blocks);
+  else
+    hipLaunchKernelGGL(k_act<float>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
+                       critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
+                       actions_out, logp_out, mu_out, sigma_out, value_out, (float*)obs_out, (float*)critic_obs_out,
+                       seed, counter, env_blocks);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+extern "C" int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs,
+                              const float* values, int num_envs, float gamma, float* rewards_out,
+                              uint8_t* dones_out, void* stream) {
+  if (!rewards || !reset || !values || !rewards_out || !dones_out || num_envs <= 0) return HG_ERR_ARG;
+  hipLaunchKernelGGL(k_env, dim3((num_envs + TPB - 1) / TPB), dim3(TPB), 0, (hipStream_t)stream, rewards, reset,
+                     time_outs, values, num_envs, gamma, rewards_out, dones_out);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

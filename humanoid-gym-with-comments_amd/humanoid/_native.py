@@ -88,6 +88,7 @@ T = {name: i for i, name in enumerate(TENSOR_IDS)}
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
            "hg_post", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
+           "hg_rollout_act", "hg_rollout_env",
            "hg_version"]
 
 _LIB = None
@@ -136,6 +137,11 @@ def load_library(path=LIB_PATH):
     L.hg_kl_mean.argtypes = [vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp]
     L.hg_kl_lr_rule.restype = ctypes.c_int
     L.hg_kl_lr_rule.argtypes = [vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
+    L.hg_rollout_act.restype = ctypes.c_int
+    L.hg_rollout_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                 vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+    L.hg_rollout_env.restype = ctypes.c_int
+    L.hg_rollout_env.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_float, vp, vp, vp]
     L.hg_adam_chunk.restype = ctypes.c_int
     L.hg_adam_chunk.argtypes = []
     L.hg_version.restype = ctypes.c_char_p

@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.optim as optim
 
-from .actor_critic import ActorCritic
+from .actor_critic import ActorCritic, _DiagGaussian
 from .hg_adam import HgAdam
 from .rollout_storage import RolloutStorage
 
@@ -79,6 +79,11 @@ class PPO:
             self._lr_t = None
             self.optimizer = optim.Adam(self._params, lr=learning_rate)
         self.transition = RolloutStorage.Transition()
+        # fused rollout-storage writes on the device (hg_rollout_act / hg_rollout_env); the
+        # action noise is Philox keyed by this seed (drawn from torch's generator) and a counter
+        self.use_fused_rollout = True
+        self._rollout_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self._on_device else 0
+        self._rollout_counter = 0
         self.clip_param = clip_param
         self.num_learning_epochs = num_learning_epochs
         self.num_mini_batches = num_mini_batches
@@ -134,7 +139,47 @@ class PPO:
     def train_mode(self):
         self.actor_critic.train()
 
+    def _fused_rollout_ok(self, obs, critic_obs):
+        st = self.storage
+        return (self._on_device and self.use_fused_rollout and st is not None and hasattr(self.actor_critic, "_mlp")
+                and obs.is_cuda and obs.dtype == torch.float32 and obs.is_contiguous()
+                and critic_obs.dtype == torch.float32 and critic_obs.is_contiguous()
+                and st.step < st.num_transitions_per_env)
+
+    def _act_fused(self, obs, critic_obs):
+        """PPO.act + the pre-step half of add_transitions in one HIP launch (hg_rollout_act):
+        the policy MLPs run in torch, the sample / log-prob / storage writes in the kernel."""
+        from humanoid import _native as N
+        st, ac, tr = self.storage, self.actor_critic, self.transition
+        t = st.step
+        mean = ac._mlp(ac.actor, obs).contiguous()
+        value = ac._mlp(ac.critic, critic_obs).contiguous()
+        std = ac.std.detach().contiguous()
+        ac.distribution = _DiagGaussian(mean, std.expand_as(mean))
+        p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        priv = st.privileged_observations
+        s = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
+        N.check(N.lib().hg_rollout_act(
+            p(mean), p(std), p(value), p(obs), p(critic_obs) if priv is not None else None, obs.shape[0],
+            mean.shape[1], ctypes.c_int64(obs.shape[1]), ctypes.c_int64(critic_obs.shape[1] if priv is not None else 0),
+            p(st.actions[t]), p(st.actions_log_prob[t]), p(st.mu[t]), p(st.sigma[t]), p(st.values[t]),
+            p(st.observations[t]), p(priv[t]) if priv is not None else None,
+            int(st.observations.dtype == torch.float16), ctypes.c_uint64(self._rollout_seed),
+            ctypes.c_uint64(self._rollout_counter), s))
+        self._rollout_counter += 1
+        tr.actions = st.actions[t]
+        tr.values = st.values[t]
+        tr.actions_log_prob = st.actions_log_prob[t].view(-1)
+        tr.action_mean = st.mu[t]
+        tr.action_sigma = st.sigma[t]
+        tr.observations = obs
+        tr.critic_observations = critic_obs
+        tr.fused_slot = t
+        return tr.actions
+
     def act(self, obs, critic_obs):
+        if self._fused_rollout_ok(obs, critic_obs):
+            return self._act_fused(obs, critic_obs)
         t = self.transition
         # actor_critic.act() would also run the lin-vel MLP, whose output the rollout discards
         self.actor_critic.update_distribution(obs)
@@ -149,6 +194,24 @@ class PPO:
 
     def process_env_step(self, rewards, dones, infos):
         t = self.transition
+        if getattr(t, "fused_slot", None) is not None:
+            # post-step half of add_transitions (hg_rollout_env): time-out bootstrap, dones
+            from humanoid import _native as N
+            st, k = self.storage, t.fused_slot
+            if st.step != k:
+                raise AssertionError("rollout storage slot mismatch")
+            p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+            to = infos.get("time_outs")
+            r = rewards.contiguous().float()
+            d = dones.contiguous().view(torch.uint8)
+            to = to.contiguous().view(torch.uint8) if to is not None else None
+            s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
+            N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, p(st.values[k]),
+                                           r.shape[0], ctypes.c_float(self.gamma), p(st.rewards[k]), p(st.dones[k]), s))
+            st.step += 1
+            self.transition.clear()
+            self.actor_critic.reset(dones)
+            return
         t.rewards = rewards.clone()
         t.dones = dones
         if "time_outs" in infos:  # bootstrap on time-outs (ppo.py:132-133)

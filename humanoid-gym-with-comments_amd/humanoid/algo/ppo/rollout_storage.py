@@ -28,6 +28,7 @@ class RolloutStorage:
             self.action_mean = None
             self.action_sigma = None
             self.hidden_states = None
+            self.fused_slot = None  # storage slot already written by hg_rollout_act (device path)
 
         def clear(self):
             self.__init__()

@@ -209,6 +209,22 @@ int hg_gae_scan(const float* rewards, const uint8_t* dones, const float* values,
 int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int64_t n_local,
                      void* stream);
 
+/* ---- rollout storage writes (replace the tail of PPO.act / process_env_step and
+ * RolloutStorage.add_transitions, ppo.py:116-138, rollout_storage.py:83-100) ----
+ * hg_rollout_act: actions = mean + std * N(0,1) (Philox keyed by seed, env, counter), their
+ * Normal log-prob summed over actions, mu, sigma, value, and the observation / critic
+ * observation rows, all into storage slot t (obs_out/critic_obs_out fp32, or fp16 when
+ * obs_fp16).  mean [N,A], std [A], value [N], obs [N,obs_width], critic_obs [N,critic_width]:
+ * contiguous device f32.  hg_rollout_env: rewards_out = rewards + gamma * values * time_outs
+ * (time_outs may be NULL), dones_out = reset. */
+int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
+                   const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
+                   int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
+                   float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out, int obs_fp16,
+                   uint64_t seed, uint64_t counter, void* stream);
+int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
+                   int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, void* stream);
+
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----
  * A list of float32 device tensors (param, grad, Adam exp_avg / exp_avg_sq, per-tensor step

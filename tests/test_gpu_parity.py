@@ -611,3 +611,43 @@ def test_kl_mean_and_lr_rule_kernels():
             lr = min(1e-2, lr * 1.5)
         assert ppo.learning_rate == lr, (k, ppo.learning_rate, lr)
         assert ppo._lr_f32.item() == np.float32(lr)
+
+
+@pytest.mark.parametrize("obs_dtype", [torch.float32, torch.float16])
+def test_fused_rollout_writes(obs_dtype):
+    """hg_rollout_act / hg_rollout_env == the reference PPO.act + process_env_step +
+    add_transitions arithmetic (ppo.py:116-138, rollout_storage.py:83-100): same mu / sigma /
+    value / obs rows, log-prob of the drawn action by the Normal formula, N(0,1) noise
+    statistics, time-out bootstrap and dones."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    torch.manual_seed(2)
+    n = 4096
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     init_noise_std=0.7)
+    ppo = PPO(ac, device="cuda:0", gamma=0.994)
+    ppo.init_storage(n, 4, [705], [219], [12], obs_dtype=obs_dtype)
+    obs, cobs = torch.randn(n, 705, device="cuda:0"), torch.randn(n, 219, device="cuda:0")
+    with torch.inference_mode():
+        a = ppo.act(obs, cobs)
+        mean, val = ac.actor(obs), ac.critic(cobs)
+    st = ppo.storage
+    assert ppo.transition.fused_slot == 0
+    torch.testing.assert_close(st.mu[0], mean, rtol=0, atol=0)
+    torch.testing.assert_close(st.values[0], val, rtol=0, atol=0)
+    torch.testing.assert_close(st.sigma[0], ac.std.detach().expand_as(mean), rtol=0, atol=0)
+    torch.testing.assert_close(st.observations[0], obs.to(obs_dtype), rtol=0, atol=0)
+    torch.testing.assert_close(st.privileged_observations[0], cobs.to(obs_dtype), rtol=0, atol=0)
+    scale = ac.std.detach().expand_as(mean)
+    ref_lp = (-((a - mean) ** 2) / (2 * scale ** 2) - scale.log() - np.log(np.sqrt(2 * np.pi))).sum(-1)
+    torch.testing.assert_close(st.actions_log_prob[0, :, 0], ref_lp, rtol=1e-5, atol=1e-4)
+    z = ((a - mean) / scale).double()
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1.0) < 0.01
+    rew = torch.randn(n, device="cuda:0")
+    dones = (torch.rand(n, device="cuda:0") < 0.1).to(torch.uint8)
+    to = (torch.rand(n, device="cuda:0") < 0.5).to(torch.uint8)
+    ppo.process_env_step(rew, dones, {"time_outs": to})
+    assert st.step == 1
+    ref_r = rew + 0.994 * torch.squeeze(val * to.unsqueeze(1), 1)
+    torch.testing.assert_close(st.rewards[0, :, 0], ref_r, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(st.dones[0, :, 0], dones, rtol=0, atol=0)
