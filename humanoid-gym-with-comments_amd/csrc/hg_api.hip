@@ -411,4 +411,33 @@ extern "C" int hg_measure_heights(void* sim, const float* points_xy, int num_poi
   return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_heights launch failed");
 }
 
+__global__ void k_set_root_all(HgState S, const float* root) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  for (int f = 0; f < 13; f++) S.root[f * S.np + e] = root[(size_t)e * 13 + f];
+  for (int c = 0; c < HG_NC * 3; c++) S.lambda[c * S.np + e] = 0.f;
+}
+__global__ void k_set_props(HgState S, const float* fric, const float* mass) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= S.n) return;
+  if (fric) S.friction[e] = fric[e];
+  if (mass) S.body_mass[e] = mass[e];
+}
+
+extern "C" int hg_set_root_state(void* sim, const float* root, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s || !root) return HG_ERR_ARG;
+  hipLaunchKernelGGL(k_set_root_all, dim3((s->S.n + 255) / 256), dim3(256), 0, (hipStream_t)stream, s->S, root);
+  return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_root_all launch failed");
+}
+
+extern "C" int hg_set_env_props(void* sim, const float* friction, const float* base_mass, void* stream) {
+  Sim* s = (Sim*)sim;
+  if (!s) return HG_ERR_ARG;
+  if (!friction && !base_mass) return HG_OK;
+  hipLaunchKernelGGL(k_set_props, dim3((s->S.n + 255) / 256), dim3(256), 0, (hipStream_t)stream, s->S, friction,
+                     base_mass);
+  return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_props launch failed");
+}
+
 extern "C" const char* hg_version(void) { return "hg_sim 0.2 (gfx950, physics v2: 32 lanes/env, LDS-resident, Delassus PGS)"; }

@@ -87,6 +87,7 @@ T = {name: i for i, name in enumerate(TENSOR_IDS)}
 # every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
            "hg_post", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
+           "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
            "hg_rollout_act", "hg_rollout_env",
            "hg_version"]
@@ -128,6 +129,10 @@ def load_library(path=LIB_PATH):
     L.hg_set_root_state_indexed.argtypes = [vp, vp, ctypes.c_int, vp, vp]
     L.hg_measure_heights.restype = ctypes.c_int
     L.hg_measure_heights.argtypes = [vp, vp, ctypes.c_int, vp, vp]
+    L.hg_set_root_state.restype = ctypes.c_int
+    L.hg_set_root_state.argtypes = [vp, vp, vp]
+    L.hg_set_env_props.restype = ctypes.c_int
+    L.hg_set_env_props.argtypes = [vp, vp, vp, vp]
     L.hg_gae_scan.restype = ctypes.c_int
     L.hg_gae_scan.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                               ctypes.c_float, ctypes.c_int, vp]

@@ -186,6 +186,12 @@ int hg_reset_masked(void* sim, const uint8_t* mask, uint64_t counter, void* stre
 int hg_set_dof_state_indexed(void* sim, const int32_t* env_ids, int n, const float* dof_pos,
                              const float* dof_vel, void* stream);
 int hg_set_root_state_indexed(void* sim, const int32_t* env_ids, int n, const float* root, void* stream);
+/* all envs (replaces set_actor_root_state_tensor, humanoid_env.py:680-681): root device [N,13] */
+int hg_set_root_state(void* sim, const float* root, void* stream);
+/* creation-time domain randomisation (replaces the friction / base-mass writes of
+ * _process_rigid_shape_props / _process_rigid_body_props, humanoid_env.py:528-553,578-584):
+ * friction, base_mass: device [N] f32 (either may be NULL) */
+int hg_set_env_props(void* sim, const float* friction, const float* base_mass, void* stream);
 
 /* ---- measured heights (replaces _get_heights, humanoid_env.py:949-985) ----
  * points_xy: device f32 [P,2] sample points in the base frame (the _init_height_points grid,

@@ -651,3 +651,22 @@ def test_fused_rollout_writes(obs_dtype):
     ref_r = rew + 0.994 * torch.squeeze(val * to.unsqueeze(1), 1)
     torch.testing.assert_close(st.rewards[0, :, 0], ref_r, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(st.dones[0, :, 0], dones, rtol=0, atol=0)
+
+
+def test_set_root_state_and_env_props(env):
+    """hg_set_root_state (all envs, clears contact warm-starts) and hg_set_env_props (DR
+    friction / base mass) through the C ABI."""
+    import ctypes as C
+    from humanoid import _native as N
+    L, s = N.lib(), C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    root = torch.randn(env.num_envs, 13, device="cuda:0")
+    N.check(L.hg_set_root_state(env.sim, C.c_void_p(root.data_ptr()), s), env.sim)
+    fr = torch.rand(env.num_envs, device="cuda:0") + 0.1
+    ms = torch.rand(env.num_envs, device="cuda:0") + 30.0
+    N.check(L.hg_set_env_props(env.sim, C.c_void_p(fr.data_ptr()), C.c_void_p(ms.data_ptr()), s), env.sim)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(env.root_states, root, rtol=0, atol=0)
+    torch.testing.assert_close(env.env_frictions.reshape(-1), fr, rtol=0, atol=0)
+    torch.testing.assert_close(env.body_mass.reshape(-1), ms, rtol=0, atol=0)
+    lam = env._view(N.T["CONTACT_LAMBDA"])
+    assert (lam[:, :48] == 0).all()
