@@ -39,6 +39,19 @@ extern "C" int hg_debug_stamps(unsigned long long* out, int reset) {
 namespace {
 
 constexpr int RMAX = 32;
+// timing experiments only (scripts/phase_cost.sh): repeat an idempotent phase to measure its cost
+#ifndef HG_REP_KIN
+#define HG_REP_KIN 1
+#endif
+#ifndef HG_REP_MINV
+#define HG_REP_MINV 1
+#endif
+#ifndef HG_REP_CHOL
+#define HG_REP_CHOL 1
+#endif
+#ifndef HG_REP_MFMA
+#define HG_REP_MFMA 1
+#endif
 
 struct RowC {  // per-row constants of the PGS, one 16-byte broadcast read
   float tgt, invD, invD2;  // target velocity, 1/W_rr, 1/W_(r+1)(r+1) (tangent pair partner)
@@ -262,11 +275,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     STAMP(1);
     // ---- A2/A3: kinematics + RNEA forward
-    kin_local(E, M, l);
-    __syncthreads();
-    if (l < 2) kin_chain(E, M, l, gz, true);
-    if (l == 2) { st3(E.u.kin.al[0], mk(0, 0, 0)); st3(E.u.kin.ac[0], mk(0, 0, -gz)); }
-    __syncthreads();
+    for (int rep = 0; rep < HG_REP_KIN; rep++) {
+      kin_local(E, M, l);
+      __syncthreads();
+      if (l < 2) kin_chain(E, M, l, gz, true);
+      if (l == 2) { st3(E.u.kin.al[0], mk(0, 0, 0)); st3(E.u.kin.ac[0], mk(0, 0, -gz)); }
+      __syncthreads();
+    }
     STAMP(2);
     // ---- A4: per-body inertia, RNEA forces, composite inertia seeds
     if (l < 13) {
@@ -385,10 +400,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // right of a lane's diagonal are never read.
     {
       float a[18];
-#pragma unroll
-      for (int k = 0; k < 18; k++) a[k] = (l < 18) ? E.u.fac.M[l < 18 ? l : 0][k] : 0.f;
       float myinv = 0.f;
       bool nonpd = false;
+      for (int rep = 0; rep < HG_REP_CHOL; rep++) {
+#pragma unroll
+      for (int k = 0; k < 18; k++) a[k] = (l < 18) ? E.u.fac.M[l < 18 ? l : 0][k] : 0.f;
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < 18; j++) {
         if (j >= off) {
@@ -402,6 +419,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           for (int k = j + 1; k < 18; k++) a[k] -= a[j] * RL(a[j], k);
         }
       }
+      }
       if (l < 18) {
 #pragma unroll
         for (int k = 0; k < 18; k++) E.u.fac.M[l][k] = a[k];
@@ -412,6 +430,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     STAMP(6);
     // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i)
+    for (int rep = 0; rep < HG_REP_MINV; rep++) {
     if (l < 18) {
       float y[18];
 #pragma unroll
@@ -441,6 +460,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       for (int k = 0; k < 18; k++) E.u.fac.Minv[k][l] = (k < off) ? 0.f : y[k];
     }
     __syncthreads();
+    }
     STAMP(7);
     // ---- A10: unconstrained velocity nu* = nu + dt M^-1 (tau - h)
     float nu_star = 0.f;
@@ -547,7 +567,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     //   B = J_h^T.  D layout: lane (kk, n), vgpr v holds Y_h[8(v/4) + 4kk + v%4][n].
     //   W_h = J_h Y_h: contraction pairs follow that layout, k = 8(q/4) + q%4 (+4 for kk = 1),
     //   so Y's accumulators are the B operands as they stand.
-    f32x16 dy0 = {0}, dy1 = {0};
+    f32x16 dy0 = {0}, dy1 = {0}, dw0 = {0}, dw1 = {0};
+    for (int rep = 0; rep < HG_REP_MFMA; rep++) {
+    if (HG_REP_MFMA > 1) {
+#pragma unroll
+      for (int i = 0; i < 18; i++) asm volatile("v_mov_b32 %0, %1" : "=v"(J[i]) : "v"(J[i]));
+      dy0 = f32x16{0}; dy1 = f32x16{0}; dw0 = f32x16{0}; dw1 = f32x16{0};
+    }
 #pragma unroll
     for (int p = 0; p < 9; p++) {
       const float am0 = (l < 18) ? shm[0].u.fac.Minv[l < 18 ? l : 0][2 * p + half] : 0.f;
@@ -557,7 +583,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       dy0 = __builtin_amdgcn_mfma_f32_32x32x2f32(am0, b0, dy0, 0, 0, 0);
       dy1 = __builtin_amdgcn_mfma_f32_32x32x2f32(am1, b1, dy1, 0, 0, 0);
     }
-    f32x16 dw0 = {0}, dw1 = {0};
 #pragma unroll
     for (int q = 0; q < 10; q++) {
       const int klo = 8 * (q / 4) + q % 4, khi = klo + 4;
@@ -565,6 +590,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       swap32(J[klo], khi < 18 ? J[khi < 18 ? khi : 0] : 0.f, a0, a1);
       dw0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, dy0[q], dw0, 0, 0, 0);
       dw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, dy1[q], dw1, 0, 0, 0);
+    }
     }
     // Y rows to LDS for the velocity update (A15): this lane holds Y_h[i][l] for its 10 dofs
 #pragma unroll
