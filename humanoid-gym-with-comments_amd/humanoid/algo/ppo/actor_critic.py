@@ -106,7 +106,10 @@ class ActorCritic(nn.Module):
 
     def update_distribution(self, observations):
         mean = self._mlp(self.actor, observations)
-        self.distribution = _DiagGaussian(mean, mean * 0.0 + self.std)
+        # the reference's `mean * 0.0 + self.std` materialises the same [B, A] values; the
+        # broadcast view avoids two kernels per call (and their backward) with identical
+        # values and gradients (d std = sum over the batch either way)
+        self.distribution = _DiagGaussian(mean, self.std.expand_as(mean))
 
     def act(self, observations, **kwargs):
         self.update_distribution(observations)

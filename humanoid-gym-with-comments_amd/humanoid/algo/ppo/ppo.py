@@ -381,10 +381,12 @@ class PPO:
         dev = st.observations.device
         obs = st.observations.flatten(0, 1)
         critic = st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else obs
-        flat = {"obs": obs, "critic": critic, "lin_vel": critic[:, 53:56],
-                "actions": st.actions.flatten(0, 1), "values": st.values.flatten(0, 1),
-                "returns": st.returns.flatten(0, 1), "logp": st.actions_log_prob.flatten(0, 1),
-                "adv": st.advantages.flatten(0, 1), "mu": st.mu.flatten(0, 1), "sigma": st.sigma.flatten(0, 1)}
+        # the per-sample scalars/12-vectors are packed once per update into one [T*N, 40] table so a
+        # minibatch needs three gathers (obs, critic obs, table) instead of ten
+        A = st.actions.shape[-1]
+        self._pack_src = [st.actions, st.values, st.returns, st.actions_log_prob, st.advantages, st.mu, st.sigma]
+        widths = [t.shape[-1] for t in self._pack_src]
+        self._packed = torch.empty(obs.shape[0], sum(widths), dtype=torch.float32, device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
         self._sums = torch.zeros(3, dtype=torch.float32, device=dev)
         self._kl = torch.zeros((), dtype=torch.float32, device=dev)
@@ -396,7 +398,12 @@ class PPO:
             if self._flat_grad is not None:
                 self._flat_grad.zero_()
             i = self._idx
-            b = {k: v[i] for k, v in flat.items()}
+            crit_b = critic[i]
+            b = {"obs": obs[i], "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
+            pk = self._packed[i]
+            for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma"),
+                                  pk.split(widths, dim=1)):
+                b[name] = part
             loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
                 b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"], b["logp"])
             if self._adaptive:
@@ -432,6 +439,7 @@ class PPO:
             self._capture(mb)
         ga, gb = self._graphs[0], self._graphs[1]
         indices = torch.randperm(nmb * mb, requires_grad=False, device=st.observations.device)
+        torch.cat([t.flatten(0, 1) for t in self._pack_src], dim=1, out=self._packed)
         self._sums.zero_()
         for _ in range(self.num_learning_epochs):
             for i in range(nmb):
