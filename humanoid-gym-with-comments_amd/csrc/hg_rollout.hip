@@ -8,7 +8,8 @@
 //     sigma, value into slot t of the storage, and copies the observation / critic observation
 //     rows into slot t (fp32 or fp16 storage) in the same launch.
 //   hg_rollout_env (after env.step): rewards[t] = r + gamma * V * time_out (the time-out
-//     bootstrap of ppo.py:132-133), dones[t] = reset.
+//     bootstrap of ppo.py:132-133), dones[t] = reset; with values == NULL the bootstrap is
+//     deferred: rewards[t] = r and time_outs[t] is kept for the batched value pass.
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -59,7 +60,7 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
       sigma_out[(size_t)e * A + j] = s;
     }
     logp_out[e] = lp;
-    value_out[e] = value[e];
+    if (value) value_out[e] = value[e];
     return;
   }
   // observation rows -> storage slot (grid-stride over both tables)
@@ -74,13 +75,14 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
 __global__ void __launch_bounds__(TPB) k_env(const float* __restrict__ rew, const uint8_t* __restrict__ reset,
                                             const uint8_t* __restrict__ time_out, const float* __restrict__ values,
                                             int n, float gamma, float* __restrict__ rew_out,
-                                            uint8_t* __restrict__ dones_out) {
+                                            uint8_t* __restrict__ dones_out, uint8_t* __restrict__ time_out_out) {
   const int e = blockIdx.x * TPB + threadIdx.x;
   if (e >= n) return;
   float r = rew[e];
-  if (time_out) r += gamma * (values[e] * (float)time_out[e]);
+  if (time_out && values) r += gamma * (values[e] * (float)time_out[e]);
   rew_out[e] = r;
   dones_out[e] = reset[e];
+  if (time_out_out) time_out_out[e] = time_out ? time_out[e] : (uint8_t)0;
 }
 
 }  // namespace
@@ -90,7 +92,7 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
                               int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
                               float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out,
                               int obs_fp16, uint64_t seed, uint64_t counter, void* stream) {
-  if (!mean || !std || !value || !obs || !actions_out || !logp_out || !mu_out || !sigma_out || !value_out ||
+  if (!mean || !std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out ||
       !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 ||
       (critic_obs_width > 0 && (!critic_obs || !critic_obs_out)))
     return HG_ERR_ARG;
@@ -112,9 +114,9 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
 
 extern "C" int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs,
                               const float* values, int num_envs, float gamma, float* rewards_out,
-                              uint8_t* dones_out, void* stream) {
-  if (!rewards || !reset || !values || !rewards_out || !dones_out || num_envs <= 0) return HG_ERR_ARG;
+                              uint8_t* dones_out, uint8_t* time_outs_out, void* stream) {
+  if (!rewards || !reset || !rewards_out || !dones_out || num_envs <= 0) return HG_ERR_ARG;
   hipLaunchKernelGGL(k_env, dim3((num_envs + TPB - 1) / TPB), dim3(TPB), 0, (hipStream_t)stream, rewards, reset,
-                     time_outs, values, num_envs, gamma, rewards_out, dones_out);
+                     time_outs, values, num_envs, gamma, rewards_out, dones_out, time_outs_out);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

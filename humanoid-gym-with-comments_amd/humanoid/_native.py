@@ -146,7 +146,7 @@ def load_library(path=LIB_PATH):
     L.hg_rollout_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                  vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
     L.hg_rollout_env.restype = ctypes.c_int
-    L.hg_rollout_env.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_float, vp, vp, vp]
+    L.hg_rollout_env.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp]
     L.hg_adam_chunk.restype = ctypes.c_int
     L.hg_adam_chunk.argtypes = []
     L.hg_version.restype = ctypes.c_char_p

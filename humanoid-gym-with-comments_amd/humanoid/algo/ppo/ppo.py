@@ -82,6 +82,7 @@ class PPO:
         # fused rollout-storage writes on the device (hg_rollout_act / hg_rollout_env); the
         # action noise is Philox keyed by this seed (drawn from torch's generator) and a counter
         self.use_fused_rollout = True
+        self.defer_values = True
         self._rollout_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self._on_device else 0
         self._rollout_counter = 0
         self.clip_param = clip_param
@@ -153,16 +154,19 @@ class PPO:
         st, ac, tr = self.storage, self.actor_critic, self.transition
         t = st.step
         mean = ac._mlp(ac.actor, obs).contiguous()
-        value = ac._mlp(ac.critic, critic_obs).contiguous()
+        defer = self._defer_values()
+        value = None if defer else ac._mlp(ac.critic, critic_obs).contiguous()
         std = ac.std.detach().contiguous()
         ac.distribution = _DiagGaussian(mean, std.expand_as(mean))
         p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
         priv = st.privileged_observations
         s = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
         N.check(N.lib().hg_rollout_act(
-            p(mean), p(std), p(value), p(obs), p(critic_obs) if priv is not None else None, obs.shape[0],
+            p(mean), p(std), p(value) if value is not None else None, p(obs),
+            p(critic_obs) if priv is not None else None, obs.shape[0],
             mean.shape[1], ctypes.c_int64(obs.shape[1]), ctypes.c_int64(critic_obs.shape[1] if priv is not None else 0),
-            p(st.actions[t]), p(st.actions_log_prob[t]), p(st.mu[t]), p(st.sigma[t]), p(st.values[t]),
+            p(st.actions[t]), p(st.actions_log_prob[t]), p(st.mu[t]), p(st.sigma[t]),
+            p(st.values[t]) if value is not None else None,
             p(st.observations[t]), p(priv[t]) if priv is not None else None,
             int(st.observations.dtype == torch.float16), ctypes.c_uint64(self._rollout_seed),
             ctypes.c_uint64(self._rollout_counter), s))
@@ -206,8 +210,18 @@ class PPO:
             d = dones.contiguous().view(torch.uint8)
             to = to.contiguous().view(torch.uint8) if to is not None else None
             s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
-            N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, p(st.values[k]),
-                                           r.shape[0], ctypes.c_float(self.gamma), p(st.rewards[k]), p(st.dones[k]), s))
+            if self._defer_values():
+                # time-out bootstrap deferred to the batched value pass in compute_returns
+                if st.time_outs is None:
+                    st.time_outs = torch.zeros_like(st.dones)
+                N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, None, r.shape[0],
+                                               ctypes.c_float(self.gamma), p(st.rewards[k]), p(st.dones[k]),
+                                               p(st.time_outs[k]), s))
+                st.values_deferred = True
+            else:
+                N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, p(st.values[k]),
+                                               r.shape[0], ctypes.c_float(self.gamma), p(st.rewards[k]),
+                                               p(st.dones[k]), None, s))
             st.step += 1
             self.transition.clear()
             self.actor_critic.reset(dones)
@@ -220,7 +234,26 @@ class PPO:
         self.transition.clear()
         self.actor_critic.reset(dones)
 
+    def _defer_values(self):
+        """Values V(s_t) of the whole rollout in one batched critic pass at compute_returns
+        instead of T per-step passes (the critic does not change during collection); only with
+        fp32 observation storage, so the critic sees exactly the observations the step saw."""
+        st = self.storage
+        return (self.defer_values and self._on_device and st is not None and st.privileged_observations is not None
+                and st.privileged_observations.dtype == torch.float32)
+
+    def _finish_deferred_values(self):
+        st, ac = self.storage, self.actor_critic
+        T, n = st.num_transitions_per_env, st.num_envs
+        v = ac._mlp(ac.critic, st.privileged_observations.flatten(0, 1)).view(T, n, 1)
+        st.values.copy_(v)
+        # time-out bootstrap, as process_env_step (ppo.py:132-133): r += gamma * V * time_out
+        st.rewards.add_(self.gamma * (st.values * st.time_outs))
+        st.values_deferred = False
+
     def compute_returns(self, last_critic_obs):
+        if getattr(self.storage, "values_deferred", False):
+            self._finish_deferred_values()
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         self.storage.compute_returns(last_values, self.gamma, self.lam)
 

@@ -66,6 +66,8 @@ class RolloutStorage:
         self.saved_hidden_states_c = None
         self.step = 0
         self.gae_fn = None  # optional override (tests); default: HIP kernel
+        self.time_outs = None  # [T, N, 1] u8, only when PPO defers the value pass (device path)
+        self.values_deferred = False
         self._stats = torch.zeros(2, dtype=torch.float64, device=device)
 
     def add_transitions(self, transition: Transition):

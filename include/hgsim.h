@@ -221,15 +221,18 @@ int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int6
  * Normal log-prob summed over actions, mu, sigma, value, and the observation / critic
  * observation rows, all into storage slot t (obs_out/critic_obs_out fp32, or fp16 when
  * obs_fp16).  mean [N,A], std [A], value [N], obs [N,obs_width], critic_obs [N,critic_width]:
- * contiguous device f32.  hg_rollout_env: rewards_out = rewards + gamma * values * time_outs
- * (time_outs may be NULL), dones_out = reset. */
+ * contiguous device f32; value may be NULL (values computed later in one batched critic pass).
+ * hg_rollout_env: rewards_out = rewards + gamma * values * time_outs (time_outs may be NULL),
+ * dones_out = reset; values == NULL defers the time-out bootstrap (rewards_out = rewards) and
+ * time_outs_out (optional) keeps the time-out flags for it. */
 int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
                    const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
                    int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
                    float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out, int obs_fp16,
                    uint64_t seed, uint64_t counter, void* stream);
 int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
-                   int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, void* stream);
+                   int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
+                   void* stream);
 
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----

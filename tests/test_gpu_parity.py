@@ -626,6 +626,7 @@ def test_fused_rollout_writes(obs_dtype):
     ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
                      init_noise_std=0.7)
     ppo = PPO(ac, device="cuda:0", gamma=0.994)
+    ppo.defer_values = False
     ppo.init_storage(n, 4, [705], [219], [12], obs_dtype=obs_dtype)
     obs, cobs = torch.randn(n, 705, device="cuda:0"), torch.randn(n, 219, device="cuda:0")
     with torch.inference_mode():
@@ -670,3 +671,35 @@ def test_set_root_state_and_env_props(env):
     torch.testing.assert_close(env.body_mass.reshape(-1), ms, rtol=0, atol=0)
     lam = env._view(N.T["CONTACT_LAMBDA"])
     assert (lam[:, :48] == 0).all()
+
+
+def test_deferred_value_pass_matches_per_step():
+    """Values of the rollout computed in one batched critic pass at compute_returns (with the
+    time-out bootstrap applied there) == per-step values and bootstrap in process_env_step."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    torch.manual_seed(4)
+    n, T = 1024, 6
+    init = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128]).state_dict()
+    g = torch.Generator(device="cpu").manual_seed(9)
+    steps = [(torch.randn(n, 705, generator=g), torch.randn(n, 219, generator=g), torch.randn(n, generator=g),
+              (torch.rand(n, generator=g) < 0.1).to(torch.uint8), (torch.rand(n, generator=g) < 0.3).to(torch.uint8))
+             for _ in range(T + 1)]
+    res = []
+    for defer in (False, True):
+        ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128])
+        ac.load_state_dict(init)
+        ppo = PPO(ac, device="cuda:0", gamma=0.994, lam=0.9)
+        ppo.defer_values = defer
+        ppo.init_storage(n, T, [705], [219], [12])
+        with torch.inference_mode():
+            for t in range(T):
+                o, c, r, d, to = (x.cuda() for x in steps[t])
+                ppo.act(o, c)
+                ppo.process_env_step(r, d, {"time_outs": to})
+            assert ppo.storage.values_deferred == defer
+            ppo.compute_returns(steps[T][1].cuda())
+        st = ppo.storage
+        res.append({k: getattr(st, k).detach().cpu().clone() for k in ("values", "rewards", "returns", "advantages")})
+    for k in res[0]:
+        torch.testing.assert_close(res[1][k], res[0][k], rtol=1e-5, atol=1e-5, msg=k)
