@@ -150,7 +150,7 @@ __device__ void reset_env(const hg_cfg* cfg, HgState& S, int e, uint64_t step, i
 }  // namespace
 
 // mode 0: full post_physics_step; mode 1: reset envs in `mask` (all if null) + observe
-__global__ void __launch_bounds__(256) k_post(HgState S, uint64_t counter, int mode, const uint8_t* mask,
+__global__ void __launch_bounds__(64) k_post(HgState S, uint64_t counter, int mode, const uint8_t* mask,
                                               float* frame_obs, float* frame_priv) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
@@ -481,7 +481,7 @@ extern "C" int hg_launch_post(const HgState* S, uint64_t counter, int mode, cons
                               float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
                               hipStream_t stream) {
   const int n = S->n;
-  hipLaunchKernelGGL(k_post, dim3((n + 255) / 256), dim3(256), 0, stream, *S, counter, mode, mask, frame_obs,
+  hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
                      frame_priv);
   const int64_t to = (int64_t)n * frame_stack * HG_OBS1, tp = (int64_t)n * c_frame_stack * HG_PRIV1;
   int go = (int)std::min<int64_t>((to + 255) / 256, 4096), gp = (int)std::min<int64_t>((tp + 255) / 256, 4096);
