@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   __syncthreads();
   const float scale0 = E.mass0 / M->mass[0];
-  const int off = fixed ? 6 : 0;
+
 
   for (int sub = 0; sub < cfg->decimation; sub++) {
     STAMP(0);
@@ -395,20 +395,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     STAMP(5);
-    // ---- A8: Cholesky in registers: lane i holds row i of M (lower part); column j's entries
-    // L[k][j] reach the other rows by v_readlane (no LDS round trips, no barriers).  Entries
-    // right of a lane's diagonal are never read.
+    // ---- A8: Cholesky in registers, in the legs-first order [left leg, right leg, base]
+    // (new index i <-> dof o(i) = i < 12 ? 6 + i : i - 12).  M's arrow structure (each leg
+    // couples only to itself and the base) then gives L no left-right-leg block, so those
+    // columns are skipped.  Lane i holds row i; column j's entries L[k][j] reach the other rows
+    // by v_readlane (no LDS round trips, no barriers).  Fixed base: the base block (i >= 12) is
+    // dropped.  Entries right of a lane's diagonal are never read.
+    const int nf = fixed ? 12 : 18;  // factorised size
     {
       float a[18];
       float myinv = 0.f;
       bool nonpd = false;
+      const int ol = l < 12 ? 6 + l : l - 12;  // this lane's dof
       for (int rep = 0; rep < HG_REP_CHOL; rep++) {
 #pragma unroll
-      for (int k = 0; k < 18; k++) a[k] = (l < 18) ? E.u.fac.M[l < 18 ? l : 0][k] : 0.f;
+      for (int k = 0; k < 18; k++) {
+        const int ok = k < 12 ? 6 + k : k - 12;
+        // M holds the lower triangle in dof order (upper entries are zero)
+        a[k] = (l < 18) ? (ol >= ok ? E.u.fac.M[l < 18 ? ol : 0][ok] : E.u.fac.M[ok][l < 18 ? ol : 0]) : 0.f;
+      }
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < 18; j++) {
-        if (j >= off) {
+        if (j < nf) {
           const float d = RL(a[j], j);
           nonpd |= !(d > 0.f);
           const float sd = sqrtf(fmaxf(d, 1e-20f));
@@ -416,7 +425,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           a[j] = (l == j) ? sd : (l > j ? a[j] * inv : a[j]);
           myinv = (l == j) ? inv : myinv;
 #pragma unroll
-          for (int k = j + 1; k < 18; k++) a[k] -= a[j] * RL(a[j], k);
+          for (int k = j + 1; k < 18; k++) {
+            if (j < 6 && k >= 6 && k < 12) continue;  // structural zero: left-leg pivot, right-leg row
+            if (k >= nf) continue;
+            a[k] -= a[j] * RL(a[j], k);
+          }
         }
       }
       }
@@ -429,35 +442,46 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     STAMP(6);
-    // ---- A9: explicit M^-1, lane i solves L L^T x = e_i (column i)
+    // ---- A9: explicit M^-1: lane i solves L L^T x = e_i in the legs-first order (skipping the
+    // structural zeros) and stores column i back in dof order
     for (int rep = 0; rep < HG_REP_MINV; rep++) {
     if (l < 18) {
       float y[18];
 #pragma unroll
       for (int k = 0; k < 18; k++) y[k] = 0.f;
-      if (l >= off) {
+      if (l < nf) {
         const float (*A)[20] = E.u.fac.M;
 #pragma unroll
         for (int k = 0; k < 18; k++) {
-          if (k < off) continue;
+          if (k >= nf) continue;
           float s = (k == l) ? 1.f : 0.f;
 #pragma unroll
-          for (int m = 0; m < k; m++) s -= A[k][m] * y[m];
+          for (int m = 0; m < k; m++) {
+            if (k >= 6 && k < 12 && m < 6) continue;
+            s -= A[k][m] * y[m];
+          }
           y[k] = s * E.u.fac.invd[k];
           __builtin_amdgcn_sched_barrier(0);  // keep the row's LDS loads next to their use
         }
 #pragma unroll
         for (int k = 17; k >= 0; k--) {
-          if (k < off) continue;
+          if (k >= nf) continue;
           const float xk = y[k] * E.u.fac.invd[k];
           y[k] = xk;
 #pragma unroll
-          for (int m = 0; m < k; m++) y[m] -= A[k][m] * xk;
+          for (int m = 0; m < k; m++) {
+            if (k >= 6 && k < 12 && m < 6) continue;
+            y[m] -= A[k][m] * xk;
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      const int ol = l < 12 ? 6 + l : l - 12;
 #pragma unroll
-      for (int k = 0; k < 18; k++) E.u.fac.Minv[k][l] = (k < off) ? 0.f : y[k];
+      for (int k = 0; k < 18; k++) {
+        const int ok = k < 12 ? 6 + k : k - 12;
+        E.u.fac.Minv[ok][ol] = (k < nf && l < nf) ? y[k] : 0.f;
+      }
     }
     __syncthreads();
     }
