@@ -703,3 +703,65 @@ def test_deferred_value_pass_matches_per_step():
         res.append({k: getattr(st, k).detach().cpu().clone() for k in ("values", "rewards", "returns", "advantages")})
     for k in res[0]:
         torch.testing.assert_close(res[1][k], res[0][k], rtol=1e-5, atol=1e-5, msg=k)
+
+
+def test_initial_state_parity():
+    """hg_create + the construction-time masked reset of every env (k_init + hg_reset_masked at
+    step 0) vs pipeline_ref.initial_state: root/dof state, commands, first observation stacks."""
+    _need_gpu()
+    import pipeline_ref as PR
+    env = _make_env(N_ENVS, "v2")
+    g = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    S, obs, priv = PR.initial_state(_oracle_cfg(env), g(env.env_origins), g(env.body_mass)[:, 0],
+                                    g(env.env_frictions)[:, 0])
+    np.testing.assert_allclose(g(env.root_states), S["root_states"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(g(env.dof_pos), S["dof_pos"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(g(env.commands), S["commands"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(g(env.obs_buf), obs, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(g(env.privileged_obs_buf), priv, rtol=1e-4, atol=1e-4)
+
+
+def test_reset_idx_and_indexed_writes():
+    """reset_idx(env_ids) (hg_reset_masked) resets exactly those envs as the oracle's reset_envs
+    (humanoid_env.py:1109-1163) and leaves the others untouched; hg_set_dof_state_indexed /
+    hg_set_root_state_indexed write only the listed envs and clear their warm-starts."""
+    _need_gpu()
+    import copy
+    import ctypes as C
+    import pipeline_ref as PR
+    from humanoid import _native as N
+    env = _make_env(N_ENVS, "v2")
+    for _ in range(4):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    torch.cuda.synchronize()
+    S, _, _ = snapshot(env)
+    g = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    S["projected_gravity"] = g(env.projected_gravity)
+    ids = np.array([1, 5, 9, 33])
+    R = copy.deepcopy(S)
+    PR.reset_envs(_oracle_cfg(env), R, ids, env.common_step_counter)
+    env.reset_idx(torch.tensor(ids, device="cuda:0"))
+    torch.cuda.synchronize()
+    keep = np.setdiff1d(np.arange(env.num_envs), ids)
+    for k in ("root_states", "dof_pos", "dof_vel", "commands", "last_actions", "episode_length_buf"):
+        np.testing.assert_allclose(g(getattr(env, k))[ids], R[k][ids], rtol=1e-6, atol=1e-6, err_msg=k)
+        np.testing.assert_array_equal(g(getattr(env, k))[keep], S[k][keep], err_msg=k)
+    assert (g(env.reset_buf)[ids] == 1).all()
+    # indexed state writes
+    L, s = N.lib(), C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wid = torch.tensor([2, 7], dtype=torch.int32, device="cuda:0")
+    q, qd = torch.randn(2, 12, device="cuda:0"), torch.randn(2, 12, device="cuda:0")
+    root = torch.randn(2, 13, device="cuda:0")
+    before = g(env.dof_pos).copy()
+    N.check(L.hg_set_dof_state_indexed(env.sim, C.c_void_p(wid.data_ptr()), 2, C.c_void_p(q.data_ptr()),
+                                       C.c_void_p(qd.data_ptr()), s), env.sim)
+    N.check(L.hg_set_root_state_indexed(env.sim, C.c_void_p(wid.data_ptr()), 2, C.c_void_p(root.data_ptr()), s),
+            env.sim)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(env.dof_pos[[2, 7]], q, rtol=0, atol=0)
+    torch.testing.assert_close(env.dof_vel[[2, 7]], qd, rtol=0, atol=0)
+    torch.testing.assert_close(env.root_states[[2, 7]], root, rtol=0, atol=0)
+    others = [i for i in range(env.num_envs) if i not in (2, 7)]
+    np.testing.assert_array_equal(g(env.dof_pos)[others], before[others])
+    lam = g(env._view(N.T["CONTACT_LAMBDA"]))
+    assert (lam[[2, 7]] == 0).all()
