@@ -13,6 +13,7 @@
 //             with g' = g * clip_coef and the learning rate read from device memory (so the
 //             adaptive-KL schedule never leaves the GPU and the step is graph-capturable).
 // HBM per step: 7 x 4 B per parameter (read p, g, m, v; write p, m, v) + 4 B for the norm pass.
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -180,5 +181,197 @@ extern "C" int hg_kl_lr_rule(const float* kl, double* lr64, float* lr32, double 
                              double lr_max, void* stream) {
   if (!kl || !lr64 || !lr32) return HG_ERR_ARG;
   hipLaunchKernelGGL(k_lr_rule, dim3(1), dim3(1), 0, (hipStream_t)stream, kl, lr64, lr32, desired_kl, lr_min, lr_max);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused PPO minibatch loss (ppo.py:155-210).  One thread per sample row:
+//   logp   = sum_a [ -(a - mu)^2 / (2 s^2) - log s - log sqrt(2 pi) ]
+//   ratio  = exp(logp - old_logp)
+//   surr   = max(-A ratio, -A clamp(ratio, lo, hi))
+//   vloss  = max((v - R)^2, (T + clamp(v - T, -c, c) - R)^2)      (or (R - v)^2)
+//   lvloss = sum_k (p_k - t_k)^2                                   (MSE numerator)
+//   kl     = sum_a [ log(s / s_old + 1e-5) + (s_old^2 + (mu_old - mu)^2) / (2 s^2) - 0.5 ]
+// and the row's gradient contributions d loss / d {mu, std, v, p}; the entropy term depends only
+// on std and is added once by the final kernel.  torch's backward conventions: maximum splits the
+// gradient evenly on ties, clamp passes it on [lo, hi] inclusive.
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int LOSS_TPB = 64;        // one wave per block: 384 blocks at the 24576-row minibatch
+constexpr int LOSS_MAX_A = 32;
+constexpr float LOG_SQRT_2PI = 0.91893853320467274178f;
+
+__device__ inline float max_w(float x, float y) { return x > y ? 1.f : (x == y ? 0.5f : 0.f); }
+
+__global__ void __launch_bounds__(LOSS_TPB) k_ppo_loss_rows(hg_ppo_batch Bt, int64_t rows, int A, float lo, float hi,
+                                                           float vclip, int clipped_value, float c_s, float c_v,
+                                                           float c_l, float* __restrict__ g_mu,
+                                                           float* __restrict__ g_v, float* __restrict__ g_p,
+                                                           double* __restrict__ partial) {
+  const int64_t r = (int64_t)blockIdx.x * LOSS_TPB + threadIdx.x;
+  const int K = 4 + A;
+  // per-row terms: [0] surrogate, [1] value loss, [2] lin-vel squared error, [3] kl, [4+a] d std_a
+  float t_surr = 0.f, t_v = 0.f, t_l = 0.f, t_kl = 0.f;
+  float gs[LOSS_MAX_A];
+#pragma unroll
+  for (int a = 0; a < LOSS_MAX_A; a++) gs[a] = 0.f;
+  if (r < rows) {
+    const float* mu = Bt.mu + r * Bt.mu_ld;
+    const float* act = Bt.actions + r * Bt.actions_ld;
+    const float* omu = Bt.old_mu + r * Bt.old_mu_ld;
+    const float* osg = Bt.old_sigma + r * Bt.old_sigma_ld;
+    float logp = 0.f;
+#pragma unroll
+    for (int a = 0; a < LOSS_MAX_A; a++) {
+      if (a >= A) break;
+      const float s = Bt.std[a], m = mu[a];
+      const float d = act[a] - m;
+      logp += -(d * d) / (2.0f * (s * s)) - logf(s) - LOG_SQRT_2PI;
+      const float so = osg[a], dm = omu[a] - m;
+      t_kl += logf(s / so + 1.0e-5f) + (so * so + dm * dm) / (2.0f * (s * s)) - 0.5f;
+    }
+    const float ratio = expf(logp - Bt.old_logp[r * Bt.old_logp_ld]);
+    const float adv = Bt.advantages[r * Bt.advantages_ld];
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const float s1 = -adv * ratio, s2 = -adv * rc;
+    t_surr = fmaxf(s1, s2);
+    const float in_r = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+    const float d_ratio = max_w(s1, s2) * (-adv) + max_w(s2, s1) * (-adv) * in_r;
+    const float d_logp = c_s * d_ratio * ratio;
+#pragma unroll
+    for (int a = 0; a < LOSS_MAX_A; a++) {
+      if (a >= A) break;
+      const float s = Bt.std[a];
+      const float d = act[a] - mu[a];
+      const float inv_s2 = 1.0f / (s * s);
+      g_mu[r * A + a] = d_logp * d * inv_s2;
+      gs[a] = d_logp * (d * d * inv_s2 / s - 1.0f / s);
+    }
+    // value loss
+    const float v = Bt.value[r * Bt.value_ld], R = Bt.returns[r * Bt.returns_ld];
+    float dv;
+    if (clipped_value) {
+      const float T = Bt.target_values[r * Bt.target_values_ld];
+      const float dvt = v - T;
+      const float vc = T + fminf(fmaxf(dvt, -vclip), vclip);
+      const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+      t_v = fmaxf(l1, l2);
+      const float in_v = (dvt >= -vclip && dvt <= vclip) ? 1.f : 0.f;
+      dv = max_w(l1, l2) * 2.0f * (v - R) + max_w(l2, l1) * 2.0f * (vc - R) * in_v;
+    } else {
+      t_v = (R - v) * (R - v);
+      dv = 2.0f * (v - R);
+    }
+    g_v[r] = c_v * dv;
+    // lin-vel MSE
+    const float* p = Bt.lin_vel + r * Bt.lin_vel_ld;
+    const float* tg = Bt.lin_vel_target + r * Bt.lin_vel_target_ld;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float e = p[k] - tg[k];
+      t_l += e * e;
+      g_p[r * 3 + k] = c_l * 2.0f * e;
+    }
+  }
+  // wave reduction in float64, fixed order
+  auto wsum = [](double x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+  };
+  double* out = partial + (int64_t)blockIdx.x * K;
+  const double s0 = wsum(t_surr), s1 = wsum(t_v), s2 = wsum(t_l), s3 = wsum(t_kl);
+  if (threadIdx.x == 0) {
+    out[0] = s0;
+    out[1] = s1;
+    out[2] = s2;
+    out[3] = s3;
+  }
+#pragma unroll
+  for (int a = 0; a < LOSS_MAX_A; a++) {
+    if (a >= A) break;
+    const double s = wsum(gs[a]);
+    if (threadIdx.x == 0) out[4 + a] = s;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_ppo_loss_final(const double* __restrict__ partial, int nb, int64_t rows,
+                                                      int A, const float* __restrict__ std, float c_v, float c_e,
+                                                      float c_l, float* __restrict__ loss_out,
+                                                      float* __restrict__ stats, float* __restrict__ g_std) {
+  __shared__ double col[4 + LOSS_MAX_A];
+  const int K = 4 + A;
+  for (int k = threadIdx.x; k < K; k += 64) {
+    double s = 0.0;
+    for (int b = 0; b < nb; b++) s += partial[(int64_t)b * K + k];
+    col[k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < A) {
+    const float s = std[threadIdx.x];
+    // entropy = mean_rows sum_a (0.5 + log sqrt(2 pi) + log s_a): d/ds_a = 1/s_a
+    g_std[threadIdx.x] = (float)col[4 + threadIdx.x] - c_e / s;
+  }
+  if (threadIdx.x == 0) {
+    const double n = (double)rows;
+    double ent = 0.0;
+    for (int a = 0; a < A; a++) ent += 0.5 + (double)LOG_SQRT_2PI + log((double)std[a]);
+    const double surr = col[0] / n, vl = col[1] / n, lv = col[2] / (3.0 * n), kl = col[3] / n;
+    loss_out[0] = (float)(surr + (double)c_v * vl - (double)c_e * ent + (double)c_l * lv);
+    stats[0] = (float)vl;
+    stats[1] = (float)surr;
+    stats[2] = (float)lv;
+    stats[3] = (float)kl;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_ppo_loss_bwd(const float* __restrict__ g, int64_t rows, int A,
+                                                     float* __restrict__ g_mu, float* __restrict__ g_std,
+                                                     float* __restrict__ g_v, float* __restrict__ g_p) {
+  const float s = *g;
+  const int64_t n_mu = rows * A, n_v = rows, n_p = rows * 3;
+  const int64_t tot = n_mu + n_v + n_p + A;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (int64_t)gridDim.x * 256) {
+    if (i < n_mu) g_mu[i] *= s;
+    else if (i < n_mu + n_v) g_v[i - n_mu] *= s;
+    else if (i < n_mu + n_v + n_p) g_p[i - n_mu - n_v] *= s;
+    else g_std[i - n_mu - n_v - n_p] *= s;
+  }
+}
+}  // namespace
+
+extern "C" int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions) {
+  return ((rows + LOSS_TPB - 1) / LOSS_TPB) * (4 + (int64_t)num_actions);
+}
+
+extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float clip_lo, float clip_hi, float value_clip,
+                           int clipped_value_loss, float value_loss_coef, float entropy_coef, float lin_vel_coef,
+                           float* loss_out, float* stats_out, float* grad_mu, float* grad_std, float* grad_value,
+                           float* grad_lin_vel, double* scratch, void* stream) {
+  if (!B || rows <= 0 || A <= 0 || A > LOSS_MAX_A || !loss_out || !stats_out || !grad_mu || !grad_std ||
+      !grad_value || !grad_lin_vel || !scratch || !B->mu || !B->std || !B->value || !B->lin_vel ||
+      !B->lin_vel_target || !B->actions || !B->old_logp || !B->advantages || !B->returns || !B->old_mu ||
+      !B->old_sigma || (clipped_value_loss && !B->target_values))
+    return HG_ERR_ARG;
+  const int64_t nb64 = (rows + LOSS_TPB - 1) / LOSS_TPB;
+  if (nb64 > INT32_MAX) return HG_ERR_ARG;
+  const int nb = (int)nb64;
+  const double n = (double)rows;
+  const float c_s = (float)(1.0 / n), c_v = (float)((double)value_loss_coef / n),
+              c_l = (float)((double)lin_vel_coef / (3.0 * n));
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_ppo_loss_rows, dim3(nb), dim3(LOSS_TPB), 0, s, *B, rows, A, clip_lo, clip_hi, value_clip,
+                     clipped_value_loss, c_s, c_v, c_l, grad_mu, grad_value, grad_lin_vel, scratch);
+  hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(64), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
+                     entropy_coef, lin_vel_coef, loss_out, stats_out, grad_std);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+extern "C" int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int A, float* grad_mu, float* grad_std,
+                                    float* grad_value, float* grad_lin_vel, void* stream) {
+  if (!grad_loss || rows <= 0 || A <= 0 || !grad_mu || !grad_std || !grad_value || !grad_lin_vel) return HG_ERR_ARG;
+  const int64_t tot = rows * (A + 4) + A;
+  const int nb = (int)std::min<int64_t>((tot + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_ppo_loss_bwd, dim3(nb), dim3(256), 0, (hipStream_t)stream, grad_loss, rows, A, grad_mu,
+                     grad_std, grad_value, grad_lin_vel);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

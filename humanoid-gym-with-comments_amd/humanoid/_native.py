@@ -89,7 +89,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_post", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
-           "hg_rollout_act", "hg_rollout_env",
+           "hg_rollout_act", "hg_rollout_env", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
            "hg_version"]
 
 _LIB = None
@@ -149,6 +149,13 @@ def load_library(path=LIB_PATH):
     L.hg_rollout_env.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp]
     L.hg_adam_chunk.restype = ctypes.c_int
     L.hg_adam_chunk.argtypes = []
+    L.hg_ppo_loss.restype = ctypes.c_int
+    L.hg_ppo_loss.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                              ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float] + [vp] * 8
+    L.hg_ppo_loss_scratch.restype = ctypes.c_int64
+    L.hg_ppo_loss_scratch.argtypes = [ctypes.c_int64, ctypes.c_int]
+    L.hg_ppo_loss_backward.restype = ctypes.c_int
+    L.hg_ppo_loss_backward.argtypes = [vp, ctypes.c_int64, ctypes.c_int] + [vp] * 5
     L.hg_version.restype = ctypes.c_char_p
     L.hg_version.argtypes = []
     return L

@@ -26,6 +26,7 @@ import torch.optim as optim
 
 from .actor_critic import ActorCritic, _DiagGaussian
 from .hg_adam import HgAdam
+from .hg_loss import ppo_loss
 from .rollout_storage import RolloutStorage
 
 
@@ -82,6 +83,9 @@ class PPO:
         # fused rollout-storage writes on the device (hg_rollout_act / hg_rollout_env); the
         # action noise is Philox keyed by this seed (drawn from torch's generator) and a counter
         self.use_fused_rollout = True
+        # the minibatch loss and its gradient on the fused HIP kernels (hg_loss.py); the symmetry
+        # loss configuration keeps the op-by-op expression
+        self.use_fused_loss = True
         self.defer_values = True
         self._rollout_seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self._on_device else 0
         self._rollout_counter = 0
@@ -286,7 +290,9 @@ class PPO:
                                       ctypes.c_void_p(self._lr_f32.data_ptr()), float(self.desired_kl), 1e-5, 1e-2, s))
 
     def _adapt_lr(self, mu, sigma, old_mu, old_sigma):
-        kl_mean = self._kl_mean(mu, sigma, old_mu, old_sigma)
+        self._adapt_lr_from_kl(self._kl_mean(mu, sigma, old_mu, old_sigma))
+
+    def _adapt_lr_from_kl(self, kl_mean):
         if self.world_size > 1:
             with torch.inference_mode():
                 dist.all_reduce(kl_mean)
@@ -305,6 +311,26 @@ class PPO:
     @property
     def _adaptive(self):
         return self.desired_kl is not None and self.schedule == "adaptive"
+
+    @property
+    def _fused_loss(self):
+        return self._on_device and self.use_fused_loss and not self.sym_loss
+
+    def _losses_fused(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
+                      old_mu_b, old_sigma_b):
+        """The loss of _losses (and the adaptive schedule's KL mean) from the three network
+        outputs in one fused HIP forward launch pair and one backward launch (hg_loss.py).
+        Returns (loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean]."""
+        ac = self.actor_critic
+        mu = ac._mlp(ac.actor, obs_b)
+        ac.distribution = _DiagGaussian(mu, ac.std.expand_as(mu))
+        est_lin_vel = ac.base_get_lin_vel(obs_b)
+        value_b = ac.evaluate(critic_b)
+        data = {"actions": actions_b, "old_logp": old_logp_b, "advantages": adv_b, "target_values": target_values_b,
+                "returns": returns_b, "old_mu": old_mu_b, "old_sigma": old_sigma_b,
+                "lin_vel_target": lin_vel_b if lin_vel_b.dtype == torch.float32 else lin_vel_b.float()}
+        return ppo_loss(mu, ac.std, value_b, est_lin_vel, data, self.clip_param, self.value_loss_coef,
+                        self.entropy_coef, self.base_lin_vel_coef, self.use_clipped_value_loss)
 
     def _losses(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b):
         """Minibatch loss (ppo.py:155-214).  The reference calls actor_critic.act() here and
@@ -364,10 +390,17 @@ class PPO:
         gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
         for (obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b, old_mu_b,
              old_sigma_b, hid_b, masks_b) in gen:
-            loss, value_loss, surrogate_loss, base_lin_vel_loss, sym_loss = self._losses(
-                obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b)
-            if self._adaptive:
-                self._adapt_lr(ac.action_mean, ac.action_std, old_mu_b, old_sigma_b)
+            if self._fused_loss:
+                loss, stats = self._losses_fused(obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b,
+                                                 returns_b, old_logp_b, old_mu_b, old_sigma_b)
+                value_loss, surrogate_loss, base_lin_vel_loss = stats[0], stats[1], stats[2]
+                if self._adaptive:
+                    self._adapt_lr_from_kl(stats[3].clone())
+            else:
+                loss, value_loss, surrogate_loss, base_lin_vel_loss, sym_loss = self._losses(
+                    obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b)
+                if self._adaptive:
+                    self._adapt_lr(ac.action_mean, ac.action_std, old_mu_b, old_sigma_b)
             if self._flat_grad is not None:
                 self._flat_grad.zero_()
                 loss.backward()
@@ -437,12 +470,20 @@ class PPO:
             for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma"),
                                   pk.split(widths, dim=1)):
                 b[name] = part
-            loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
-                b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"], b["logp"])
-            if self._adaptive:
-                ac = self.actor_critic
-                self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
-            self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
+            if self._fused_loss:
+                loss, stats = self._losses_fused(b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"],
+                                                 b["adv"], b["returns"], b["logp"], b["mu"], b["sigma"])
+                if self._adaptive:
+                    self._kl.copy_(stats[3])
+                self._sums.add_(stats[:3])
+            else:
+                loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
+                    b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"],
+                    b["logp"])
+                if self._adaptive:
+                    ac = self.actor_critic
+                    self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
+                self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
             loss.backward()
         with torch.cuda.graph(gb, pool=ga.pool()):
             if self.world_size > 1:

@@ -266,6 +266,43 @@ int hg_kl_mean(const float* mu, const float* sigma, const float* old_mu, const f
 int hg_kl_lr_rule(const float* kl, double* lr64, float* lr32, double desired_kl, double lr_min, double lr_max,
                   void* stream);
 
+/* ---- fused PPO minibatch loss (replaces ppo.py:155-210 between the network outputs and
+ * loss.backward(): log-prob, ratio, clipped surrogate, clipped value loss, entropy bonus,
+ * lin-vel MSE, and the KL mean of the adaptive schedule) ----
+ * Row-wise inputs are [rows, width] float32 with a row stride in elements (*_ld), so they may be
+ * column slices of a packed table.  hg_ppo_loss writes
+ *   loss_out[0] = surrogate + value_loss_coef*value_loss - entropy_coef*entropy
+ *                 + lin_vel_coef*lin_vel_loss
+ *   stats_out[0..3] = value_loss, surrogate_loss, lin_vel_loss, kl_mean
+ * and the gradients of loss_out[0] with respect to mu [rows, A], std [A], value [rows] and
+ * lin_vel [rows, 3] (contiguous) — unscaled; hg_ppo_loss_backward multiplies them in place by
+ * the device scalar grad_loss (the chain rule of loss.backward()).  Ties of torch.max and the
+ * clamp boundaries follow torch's backward (max: half each on ties; clamp: pass-through on
+ * [lo, hi]).  Deterministic: per-block partials, fixed-order float64 sums.  Two launches +
+ * one for the backward; graph-capturable. */
+typedef struct hg_ppo_batch {
+  const float* mu;             int64_t mu_ld;             /* current policy mean  [rows, A] */
+  const float* std;                                       /* current policy std   [A] */
+  const float* value;          int64_t value_ld;          /* current critic value [rows] */
+  const float* lin_vel;        int64_t lin_vel_ld;        /* lin-vel estimate     [rows, 3] */
+  const float* lin_vel_target; int64_t lin_vel_target_ld; /* critic_obs[:, 53:56] */
+  const float* actions;        int64_t actions_ld;        /* stored actions       [rows, A] */
+  const float* old_logp;       int64_t old_logp_ld;
+  const float* advantages;     int64_t advantages_ld;
+  const float* target_values;  int64_t target_values_ld;
+  const float* returns;        int64_t returns_ld;
+  const float* old_mu;         int64_t old_mu_ld;
+  const float* old_sigma;      int64_t old_sigma_ld;
+} hg_ppo_batch;
+int hg_ppo_loss(const hg_ppo_batch* batch, int64_t rows, int num_actions, float clip_lo, float clip_hi,
+                float value_clip, int clipped_value_loss, float value_loss_coef, float entropy_coef,
+                float lin_vel_coef, float* loss_out, float* stats_out, float* grad_mu, float* grad_std,
+                float* grad_value, float* grad_lin_vel, double* scratch /* >= hg_ppo_loss_scratch() doubles */,
+                void* stream);
+int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions);
+int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int num_actions, float* grad_mu, float* grad_std,
+                         float* grad_value, float* grad_lin_vel, void* stream);
+
 /* library build info */
 const char* hg_version(void);
 

@@ -6,6 +6,7 @@
   * 1000-step seeded trajectories, fixed base (tight) and floating base (divergence curve)
   * determinism: the same state and actions twice -> bitwise identical
 """
+import math
 import ctypes
 
 import numpy as np
@@ -765,3 +766,72 @@ def test_reset_idx_and_indexed_writes():
     np.testing.assert_array_equal(g(env.dof_pos)[others], before[others])
     lam = g(env._view(N.T["CONTACT_LAMBDA"]))
     assert (lam[[2, 7]] == 0).all()
+
+
+@pytest.mark.parametrize("clipped_value", [True, False])
+def test_fused_ppo_loss_matches_torch(clipped_value):
+    """hg_ppo_loss / hg_ppo_loss_backward (hg_loss.py) == the op-by-op minibatch loss of
+    ppo.py:155-210 (PPO._losses + KL expression): loss, its parts, KL mean and every parameter
+    gradient, with ratios inside and on both sides of the clip band, value deltas on both sides
+    of the value clip, and exact ties (torch's max/clamp backward rules)."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    from test_ppo_golden import SMALL
+    torch.manual_seed(11)
+    ac = ActorCritic(**SMALL).cuda()
+    with torch.no_grad():
+        ac.std.copy_(torch.rand(12) * 0.8 + 0.4)
+    ppo = PPO(ac, clip_param=0.2, value_loss_coef=1.0, entropy_coef=0.001, use_clipped_value_loss=clipped_value,
+              learning_rate=1e-3, schedule="adaptive", desired_kl=0.01, device="cuda:0")
+    B = 5000
+    g = torch.Generator().manual_seed(5)
+    obs = torch.randn(B, 141, generator=g).cuda()
+    critic = torch.randn(B, 73, generator=g).cuda()
+    with torch.no_grad():
+        mu0 = ac.act_inference(obs)
+        v0 = ac.evaluate(critic)
+    actions = (mu0 + torch.randn(B, 12, generator=g).cuda() * ac.std.detach()).contiguous()
+    with torch.no_grad():
+        logp_cur = _DiagGaussianLogp(mu0, ac.std, actions)
+    # old log-probs: ratio exactly 1 (ties) for a third, spread inside / outside the band for the rest
+    shift = torch.randn(B, generator=g).cuda() * 0.4
+    shift[: B // 3] = 0.0
+    old_logp = (logp_cur - shift).unsqueeze(1)
+    adv = torch.randn(B, 1, generator=g).cuda()
+    target_values = v0 + torch.randn(B, 1, generator=g).cuda() * 0.3
+    target_values[:100] = v0[:100]  # value delta exactly 0
+    returns = target_values + torch.randn(B, 1, generator=g).cuda()
+    old_mu = mu0 + torch.randn(B, 12, generator=g).cuda() * 0.05
+    old_sigma = ac.std.detach().expand(B, 12) * (1 + torch.rand(B, 12, generator=g).cuda() * 0.1)
+    lin_vel = critic[:, 53:56]
+
+    def run(fused):
+        ppo.use_fused_loss = fused
+        for p in ac.parameters():
+            p.grad = None
+        if fused:
+            loss, stats = ppo._losses_fused(obs, critic, lin_vel, actions, target_values, adv, returns, old_logp,
+                                            old_mu, old_sigma)
+            parts = stats.clone()
+        else:
+            loss, vl, sl, lvl, _ = ppo._losses(obs, critic, lin_vel, actions, target_values, adv, returns, old_logp)
+            kl = ppo._kl_mean(ac.action_mean, ac.action_std, old_mu, old_sigma)
+            parts = torch.stack([vl.detach(), sl.detach(), lvl.detach(), kl])
+        (loss * 0.7).backward()  # a non-unit incoming gradient exercises the backward scaling
+        return loss.detach().clone(), parts, [p.grad.clone() for p in ac.parameters()]
+
+    l_ref, p_ref, g_ref = run(False)
+    l_f, p_f, g_f = run(True)
+    torch.testing.assert_close(l_f, l_ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p_f, p_ref, rtol=1e-5, atol=1e-6)
+    bad = []
+    for (name, _), a, b in zip(ac.named_parameters(), g_f, g_ref):
+        if not torch.allclose(a, b, rtol=1e-4, atol=1e-6):
+            bad.append(f"{name}: max|d| {(a - b).abs().max().item():.3e} max|ref| {b.abs().max().item():.3e}"
+                       f" fused[:4] {a.flatten()[:4].tolist()} ref[:4] {b.flatten()[:4].tolist()}")
+    assert not bad, "\n".join(bad)
+
+
+def _DiagGaussianLogp(mu, std, a):
+    var = std ** 2
+    return (-((a - mu) ** 2) / (2 * var) - std.log() - math.log(math.sqrt(2 * math.pi))).sum(-1)
