@@ -294,17 +294,34 @@ __global__ void __launch_bounds__(LOSS_TPB) k_ppo_loss_rows(hg_ppo_batch Bt, int
   }
 }
 
-__global__ void __launch_bounds__(64) k_ppo_loss_final(const double* __restrict__ partial, int nb, int64_t rows,
-                                                      int A, const float* __restrict__ std, float c_v, float c_e,
-                                                      float c_l, float* __restrict__ loss_out,
-                                                      float* __restrict__ stats, float* __restrict__ g_std) {
+__global__ void __launch_bounds__(256) k_ppo_loss_final(const double* __restrict__ partial, int nb, int64_t rows,
+                                                       int A, const float* __restrict__ std, float c_v, float c_e,
+                                                       float c_l, float* __restrict__ loss_out,
+                                                       float* __restrict__ stats, float* __restrict__ g_std) {
+  // thread t sums blocks t, t+256, ... of every column (independent loads in flight), then a
+  // fixed-order wave and cross-wave reduction: deterministic
+  __shared__ double ws[4][4 + LOSS_MAX_A];
   __shared__ double col[4 + LOSS_MAX_A];
   const int K = 4 + A;
-  for (int k = threadIdx.x; k < K; k += 64) {
-    double s = 0.0;
-    for (int b = 0; b < nb; b++) s += partial[(int64_t)b * K + k];
-    col[k] = s;
+  double acc[4 + LOSS_MAX_A];
+#pragma unroll
+  for (int k = 0; k < 4 + LOSS_MAX_A; k++) acc[k] = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256) {
+    const double* row = partial + (int64_t)b * K;
+#pragma unroll
+    for (int k = 0; k < 4 + LOSS_MAX_A; k++)
+      if (k < K) acc[k] += row[k];
   }
+#pragma unroll
+  for (int k = 0; k < 4 + LOSS_MAX_A; k++) {
+    if (k < K) {  // uniform over the block
+      double x = acc[k];
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6][k] = x;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < K) col[threadIdx.x] = (ws[0][threadIdx.x] + ws[1][threadIdx.x]) + (ws[2][threadIdx.x] + ws[3][threadIdx.x]);
   __syncthreads();
   if (threadIdx.x < A) {
     const float s = std[threadIdx.x];
@@ -361,7 +378,7 @@ extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float cli
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_ppo_loss_rows, dim3(nb), dim3(LOSS_TPB), 0, s, *B, rows, A, clip_lo, clip_hi, value_clip,
                      clipped_value_loss, c_s, c_v, c_l, grad_mu, grad_value, grad_lin_vel, scratch);
-  hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(64), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
+  hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(256), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
                      entropy_coef, lin_vel_coef, loss_out, stats_out, grad_std);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

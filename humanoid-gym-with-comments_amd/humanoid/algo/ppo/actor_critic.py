@@ -12,6 +12,8 @@ import math
 import torch
 import torch.nn as nn
 
+from . import hg_mlp
+
 _LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
 _ENTROPY_CONST = 0.5 + 0.5 * math.log(2 * math.pi)
 
@@ -74,12 +76,22 @@ class ActorCritic(nn.Module):
         self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
         self.distribution = None
         self.policy_dtype = policy_dtype
+        self.fused_mlp = True
+        self._fusable = {}
 
     def _mlp(self, net, x):
         if self.policy_dtype == "bf16" and x.is_cuda:
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 return net(x).float()
-        return net(x if x.dtype == torch.float32 else x.float())
+        x = x if x.dtype == torch.float32 else x.float()
+        if self.fused_mlp and x.is_cuda and torch.is_grad_enabled():
+            # training pass: activation backward + bias gradient fused per layer (hg_mlp.py)
+            ok = self._fusable.get(id(net))
+            if ok is None:
+                ok = self._fusable[id(net)] = hg_mlp.fusable(net)
+            if ok:
+                return hg_mlp.mlp_forward(net, x)
+        return net(x)
 
     @staticmethod
     def init_weights(sequential, scales):

@@ -303,6 +303,16 @@ int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions);
 int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int num_actions, float* grad_mu, float* grad_std,
                          float* grad_value, float* grad_lin_vel, void* stream);
 
+/* ---- policy MLP backward: activation backward + bias gradient in one pass (replaces, per
+ * Linear(+ELU) layer of actor_critic.py:36-149, torch's ELU backward and grad_bias = gh.sum(0))
+ * gh = gy * elu'(h) with elu'(h) = 1 for y > 0, y + 1 otherwise (y = the layer's ELU output);
+ * y == NULL: identity activation, gh is gy (gh not written).  grad_bias[width] = column sums of
+ * gh, deterministic (per-128-row tile partials in scratch, fixed-order column sums).
+ * [rows, width] contiguous row-major float32; two launches. */
+int hg_mlp_act_backward(const float* gy, const float* y, float* gh, int64_t rows, int width, float* grad_bias,
+                        float* scratch /* >= hg_mlp_act_backward_scratch() floats */, void* stream);
+int64_t hg_mlp_act_backward_scratch(int64_t rows, int width);
+
 /* library build info */
 const char* hg_version(void);
 

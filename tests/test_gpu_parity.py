@@ -835,3 +835,39 @@ def test_fused_ppo_loss_matches_torch(clipped_value):
 def _DiagGaussianLogp(mu, std, a):
     var = std ** 2
     return (-((a - mu) ** 2) / (2 * var) - std.log() - math.log(math.sqrt(2 * math.pi))).sum(-1)
+
+
+def test_fused_mlp_backward_matches_torch():
+    """hg_mlp_act_backward (ELU backward + bias gradient in one pass, hg_mlp.py) == torch's
+    nn.Sequential backward for the full-size actor / lin-vel / critic MLPs (actor_critic.py:36-149),
+    at a row count that is not a multiple of the 128-row tile."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic
+    torch.manual_seed(3)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     base_lin_vel_hidden_dims=[128, 128]).cuda()
+    B = 3001
+    obs = torch.randn(B, 705, device="cuda:0")
+    critic = torch.randn(B, 219, device="cuda:0")
+    w_mu, w_v, w_lv = (torch.randn(B, 12, device="cuda:0"), torch.randn(B, 1, device="cuda:0"),
+                       torch.randn(B, 3, device="cuda:0"))
+
+    def run(fused):
+        ac.fused_mlp = fused
+        for p in ac.parameters():
+            p.grad = None
+        x = obs.clone().requires_grad_()
+        mu = ac._mlp(ac.actor, x)
+        v = ac._mlp(ac.critic, critic)
+        lv = ac._mlp(ac.base_lin_vel, x)
+        ((mu * w_mu).sum() + (v * w_v).sum() + (lv * w_lv).sum()).backward()
+        return [t.detach().clone() for t in (mu, v, lv)], [p.grad.clone() for p in ac.parameters() if p.grad is not None], x.grad.clone()
+
+    out_t, g_t, gx_t = run(False)
+    out_f, g_f, gx_f = run(True)
+    for a, b in zip(out_f, out_t):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    assert len(g_f) == len(g_t)
+    for (name, _), a, b in zip([(n, p) for n, p in ac.named_parameters() if n != "std"], g_f, g_t):
+        torch.testing.assert_close(a, b, rtol=2e-4, atol=2e-5, msg=lambda m: f"{name}: {m}")
+    torch.testing.assert_close(gx_f, gx_t, rtol=2e-4, atol=2e-5)
