@@ -152,3 +152,190 @@ extern "C" int hg_mlp_act_backward(const float* gy, const float* y, float* gh, i
                      grad_bias);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Skinny output layers (width N <= 16 over K = 128 inputs: the actor's 12 actions, the lin-vel
+// head's 3, the critic's single value): y = x W^T + b and its backward.  BLAS runs these
+// [rows, 128] x [128, N] products at a few TFLOP/s (latency and tile-shape bound); here each is a
+// streaming pass over the [rows, 128] activation:
+//   forward: 16 lanes per row (8 inputs each, two float4 loads = one coalesced 512-B row per
+//            16-lane group), the lane's W slice in registers, a 4-step xor reduction per output;
+//   dX:      lanes along K (2 columns each), the tile's gh rows staged in LDS (broadcast reads);
+//   dW, db:  same mapping, per-64-row-tile partials of gh^T h and of gh, then the fixed-order
+//            column sums of k_colsum_final over the N*K + N partial columns.
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int SK_K = 128;
+constexpr int SK_ROWS = 64;
+
+template <int N>
+__global__ void __launch_bounds__(256) k_skinny_fwd(const float* __restrict__ x, int64_t ldx,
+                                                   const float* __restrict__ W, const float* __restrict__ b,
+                                                   float* __restrict__ y, int64_t rows) {
+  const int q = threadIdx.x & 15;  // lane within the row's 16-lane group
+  const int k0 = 8 * q;
+  float w[N][8];
+#pragma unroll
+  for (int n = 0; n < N; n++) {
+    const float4 a = *reinterpret_cast<const float4*>(W + n * SK_K + k0);
+    const float4 c = *reinterpret_cast<const float4*>(W + n * SK_K + k0 + 4);
+    w[n][0] = a.x; w[n][1] = a.y; w[n][2] = a.z; w[n][3] = a.w;
+    w[n][4] = c.x; w[n][5] = c.y; w[n][6] = c.z; w[n][7] = c.w;
+  }
+  const float bq = q < N ? b[q] : 0.f;
+  const int64_t groups = (rows + 15) / 16;
+  for (int64_t gi = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); gi < rows; gi += (int64_t)gridDim.x * 16) {
+    const float* xr = x + gi * ldx + k0;
+    const float4 a = *reinterpret_cast<const float4*>(xr);
+    const float4 c = *reinterpret_cast<const float4*>(xr + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    float out = 0.f;
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; j++) s = fmaf(v[j], w[n][j], s);
+      s += __shfl_xor(s, 8, 16);
+      s += __shfl_xor(s, 4, 16);
+      s += __shfl_xor(s, 2, 16);
+      s += __shfl_xor(s, 1, 16);
+      out = (q == n) ? s : out;
+    }
+    if (q < N) y[gi * N + q] = out + bq;
+  }
+  (void)groups;
+}
+
+template <int N>
+__global__ void __launch_bounds__(64) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
+                                                 float* __restrict__ dx, int64_t rows) {
+  __shared__ float g_s[SK_ROWS * N];
+  const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
+  const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
+  for (int i = threadIdx.x; i < nr * N; i += 64) g_s[i] = gh[r0 * N + i];
+  const int c = 2 * threadIdx.x;
+  float w0[N], w1[N];
+#pragma unroll
+  for (int n = 0; n < N; n++) {
+    const float2 t = *reinterpret_cast<const float2*>(W + n * SK_K + c);
+    w0[n] = t.x;
+    w1[n] = t.y;
+  }
+  __syncthreads();
+  for (int r = 0; r < nr; r++) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      const float g = g_s[r * N + n];
+      a0 = fmaf(g, w0[n], a0);
+      a1 = fmaf(g, w1[n], a1);
+    }
+    *reinterpret_cast<float2*>(dx + (r0 + r) * SK_K + c) = make_float2(a0, a1);
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, const float* __restrict__ h,
+                                                 int64_t ldh, float* __restrict__ partial, int64_t rows) {
+  __shared__ float g_s[SK_ROWS * N];
+  const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
+  const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
+  for (int i = threadIdx.x; i < nr * N; i += 64) g_s[i] = gh[r0 * N + i];
+  __syncthreads();
+  const int c = 2 * threadIdx.x;
+  float a0[N], a1[N];
+#pragma unroll
+  for (int n = 0; n < N; n++) a0[n] = a1[n] = 0.f;
+  const float* hr = h + r0 * ldh + c;
+  int r = 0;
+  for (; r + 8 <= nr; r += 8) {
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const float2*>(hr + (int64_t)(r + u) * ldh);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+#pragma unroll
+      for (int n = 0; n < N; n++) {
+        const float g = g_s[(r + u) * N + n];
+        a0[n] = fmaf(g, v[u].x, a0[n]);
+        a1[n] = fmaf(g, v[u].y, a1[n]);
+      }
+    }
+  }
+  for (; r < nr; r++) {
+    const float2 v = *reinterpret_cast<const float2*>(hr + (int64_t)r * ldh);
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      const float g = g_s[r * N + n];
+      a0[n] = fmaf(g, v.x, a0[n]);
+      a1[n] = fmaf(g, v.y, a1[n]);
+    }
+  }
+  float* out = partial + (int64_t)blockIdx.x * (N * SK_K + N);
+#pragma unroll
+  for (int n = 0; n < N; n++) *reinterpret_cast<float2*>(out + n * SK_K + c) = make_float2(a0[n], a1[n]);
+  if (threadIdx.x < N) {
+    float gb = 0.f;
+    for (int rr = 0; rr < nr; rr++) gb += g_s[rr * N + threadIdx.x];
+    out[N * SK_K + threadIdx.x] = gb;
+  }
+}
+}  // namespace
+
+#define HG_SKINNY_SWITCH(N, CALL) \
+  switch (N) {                    \
+    case 1: CALL(1); break;       \
+    case 2: CALL(2); break;       \
+    case 3: CALL(3); break;       \
+    case 4: CALL(4); break;       \
+    case 6: CALL(6); break;       \
+    case 8: CALL(8); break;       \
+    case 12: CALL(12); break;     \
+    case 16: CALL(16); break;     \
+    default: return HG_ERR_ARG;   \
+  }
+
+extern "C" int hg_linear_skinny_supported(int n, int k) {
+  return (n == 1 || n == 2 || n == 3 || n == 4 || n == 6 || n == 8 || n == 12 || n == 16) && k == SK_K;
+}
+
+extern "C" int hg_linear_skinny_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y,
+                                        int64_t rows, int n, int k, void* stream) {
+  if (!x || !W || !b || !y || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldx < k || ldx % 4 != 0 ||
+      (uintptr_t)x % 16 != 0 || (uintptr_t)W % 16 != 0)
+    return HG_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t want = (rows + 15) / 16;  // one 16-row group per block pass
+  const dim3 grid((unsigned)(want < 1024 ? want : 1024));
+#define HG_SK_FWD(NN) hipLaunchKernelGGL(k_skinny_fwd<NN>, grid, dim3(256), 0, s, x, ldx, W, b, y, rows)
+  HG_SKINNY_SWITCH(n, HG_SK_FWD)
+#undef HG_SK_FWD
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+extern "C" int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k) {
+  return ((rows + SK_ROWS - 1) / SK_ROWS) * (int64_t)(n * k + n);
+}
+
+// gh [rows, n] (the output gradient), h [rows, k] (the layer input, row stride ldh), W [n, k].
+// grad_wb [n*k + n]: dW (row-major [n, k]) followed by db.  dx [rows, k] (contiguous) may be NULL.
+extern "C" int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, const float* W, float* dx,
+                                         float* grad_wb, int64_t rows, int n, int k, float* scratch, void* stream) {
+  if (!gh || !h || !W || !grad_wb || !scratch || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldh < k ||
+      ldh % 2 != 0 || (uintptr_t)h % 8 != 0 || (uintptr_t)W % 8 != 0 || (dx && (uintptr_t)dx % 8 != 0))
+    return HG_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = (int)((rows + SK_ROWS - 1) / SK_ROWS);
+  const dim3 grid((unsigned)tiles);
+#define HG_SK_DW(NN) hipLaunchKernelGGL(k_skinny_dw<NN>, grid, dim3(64), 0, s, gh, h, ldh, scratch, rows)
+  HG_SKINNY_SWITCH(n, HG_SK_DW)
+#undef HG_SK_DW
+  const int width = n * k + n;
+  hipLaunchKernelGGL(k_colsum_final, dim3((width + FC - 1) / FC), dim3(TPB), 0, s, scratch, tiles, width, grad_wb);
+  if (dx) {
+#define HG_SK_DX(NN) hipLaunchKernelGGL(k_skinny_dx<NN>, grid, dim3(64), 0, s, gh, W, dx, rows)
+    HG_SKINNY_SWITCH(n, HG_SK_DX)
+#undef HG_SK_DX
+  }
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

@@ -84,13 +84,14 @@ class ActorCritic(nn.Module):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 return net(x).float()
         x = x if x.dtype == torch.float32 else x.float()
-        if self.fused_mlp and x.is_cuda and torch.is_grad_enabled():
-            # training pass: activation backward + bias gradient fused per layer (hg_mlp.py)
+        if self.fused_mlp and x.is_cuda:
             ok = self._fusable.get(id(net))
             if ok is None:
                 ok = self._fusable[id(net)] = hg_mlp.fusable(net)
             if ok:
-                return hg_mlp.mlp_forward(net, x)
+                # training pass: activation backward + bias gradient fused per layer, skinny output
+                # layer on its own kernels (hg_mlp.py); inference: the output layer's kernel only
+                return hg_mlp.mlp_forward(net, x) if torch.is_grad_enabled() else hg_mlp.mlp_infer(net, x)
         return net(x)
 
     @staticmethod

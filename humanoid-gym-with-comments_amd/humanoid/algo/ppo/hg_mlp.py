@@ -49,6 +49,40 @@ def _act_backward(gy, y, rows, width, gb):
     return gh
 
 
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _skinny_ok(h, W):
+    n, k = W.shape
+    return (bool(N.lib().hg_linear_skinny_supported(n, k)) and h.dim() == 2 and h.stride(1) == 1
+            and h.stride(0) % 4 == 0 and h.data_ptr() % 16 == 0 and W.is_contiguous())
+
+
+def _skinny_forward(h, W, b):
+    rows, n = h.shape[0], W.shape[0]
+    y = torch.empty(rows, n, dtype=torch.float32, device=h.device)
+    rc = N.lib().hg_linear_skinny_forward(h.data_ptr(), h.stride(0), W.data_ptr(), b.data_ptr(), y.data_ptr(), rows,
+                                          n, W.shape[1], _stream(h.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_linear_skinny_forward failed ({rc})")
+    return y
+
+
+def _skinny_backward(g, h, W, need_dx):
+    rows, (n, k) = g.shape[0], W.shape
+    L = N.lib()
+    wb = torch.empty(n * k + n, dtype=torch.float32, device=g.device)
+    dx = torch.empty(rows, k, dtype=torch.float32, device=g.device) if need_dx else None
+    scratch = torch.empty(int(L.hg_linear_skinny_backward_scratch(rows, n, k)), dtype=torch.float32, device=g.device)
+    rc = L.hg_linear_skinny_backward(g.data_ptr(), h.data_ptr(), h.stride(0), W.data_ptr(),
+                                     dx.data_ptr() if need_dx else None, wb.data_ptr(), rows, n, k,
+                                     scratch.data_ptr(), _stream(g.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_linear_skinny_backward failed ({rc})")
+    return wb[: n * k].view(n, k), wb[n * k:], dx
+
+
 class _MLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params):
@@ -57,7 +91,10 @@ class _MLP(torch.autograd.Function):
         h = x
         for i in range(n):
             W, b = params[2 * i], params[2 * i + 1]
-            h = torch.addmm(b, h, W.t())
+            if i == n - 1 and _skinny_ok(h, W):
+                h = _skinny_forward(h, W, b)
+            else:
+                h = torch.addmm(b, h, W.t())
             if i < n - 1:
                 h = F.elu(h)
             acts.append(h)
@@ -75,23 +112,47 @@ class _MLP(torch.autograd.Function):
         g = g.contiguous()
         gx = None
         for i in range(n - 1, -1, -1):
-            rows, width = g.shape
-            gb = torch.empty(width, dtype=torch.float32, device=g.device)
-            # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
-            gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb)
-            grads[2 * i + 1] = gb
-            grads[2 * i] = torch.mm(gh.t(), ins[i])
+            need_dx = i > 0 or ctx.needs_input_grad[0]
+            if i == n - 1 and _skinny_ok(ins[i], Ws[i]):
+                # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
+                grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx)
+            else:
+                rows, width = g.shape
+                gb = torch.empty(width, dtype=torch.float32, device=g.device)
+                # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
+                gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb)
+                grads[2 * i + 1] = gb
+                grads[2 * i] = torch.mm(gh.t(), ins[i])
+                gnext = torch.mm(gh, Ws[i]) if need_dx else None
             if i > 0:
-                g = torch.mm(gh, Ws[i])
-            elif ctx.needs_input_grad[0]:
-                gx = torch.mm(gh, Ws[0])
+                # the next (lower) layer's incoming gradient goes through its ELU backward
+                g = gnext
+            else:
+                gx = gnext
         return (gx, *grads)
 
 
-def mlp_forward(net, x):
-    """net(x) for a fusable Linear/ELU nn.Sequential, with the fused backward."""
+def _params(net):
     params = []
     for m in net:
         if isinstance(m, nn.Linear):
             params += [m.weight, m.bias]
-    return _MLP.apply(x, *params)
+    return params
+
+
+def mlp_forward(net, x):
+    """net(x) for a fusable Linear/ELU nn.Sequential, with the fused backward."""
+    return _MLP.apply(x, *_params(net))
+
+
+def mlp_infer(net, x):
+    """net(x) without autograd (rollout inference): torch's Linear/ELU for the hidden layers, the
+    skinny HIP kernel for the output layer."""
+    mods = list(net)
+    h = x
+    for m in mods[:-1]:
+        h = m(h)
+    last = mods[-1]
+    if _skinny_ok(h, last.weight):
+        return _skinny_forward(h, last.weight, last.bias)
+    return last(h)

@@ -312,6 +312,17 @@ int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int num_actions, 
 int hg_mlp_act_backward(const float* gy, const float* y, float* gh, int64_t rows, int width, float* grad_bias,
                         float* scratch /* >= hg_mlp_act_backward_scratch() floats */, void* stream);
 int64_t hg_mlp_act_backward_scratch(int64_t rows, int width);
+/* Skinny output layers (n in {1,2,3,4,6,8,12,16}, k == 128): the last Linear of
+ * each policy MLP (12 actions, 3 lin-vel, 1 value).  forward: y[rows, n] = x W^T + b, x rows of
+ * stride ldx (16-byte aligned); backward: grad_wb = [dW (n x k row-major), db (n)] as
+ * deterministic column sums over 64-row tiles, dx[rows, k] = gh W (dx may be NULL). */
+int hg_linear_skinny_supported(int n, int k);
+int hg_linear_skinny_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y, int64_t rows,
+                             int n, int k, void* stream);
+int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, const float* W, float* dx,
+                              float* grad_wb, int64_t rows, int n, int k,
+                              float* scratch /* >= hg_linear_skinny_backward_scratch() floats */, void* stream);
+int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k);
 
 /* library build info */
 const char* hg_version(void);

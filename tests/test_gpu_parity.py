@@ -632,7 +632,7 @@ def test_fused_rollout_writes(obs_dtype):
     obs, cobs = torch.randn(n, 705, device="cuda:0"), torch.randn(n, 219, device="cuda:0")
     with torch.inference_mode():
         a = ppo.act(obs, cobs)
-        mean, val = ac.actor(obs), ac.critic(cobs)
+        mean, val = ac._mlp(ac.actor, obs), ac._mlp(ac.critic, cobs)  # the policy forward the rollout runs
     st = ppo.storage
     assert ppo.transition.fused_slot == 0
     torch.testing.assert_close(st.mu[0], mean, rtol=0, atol=0)
@@ -866,8 +866,12 @@ def test_fused_mlp_backward_matches_torch():
     out_t, g_t, gx_t = run(False)
     out_f, g_f, gx_f = run(True)
     for a, b in zip(out_f, out_t):
-        torch.testing.assert_close(a, b, rtol=0, atol=0)
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
     assert len(g_f) == len(g_t)
+    with torch.no_grad():  # inference path (rollout): skinny output-layer kernel
+        ac.fused_mlp = True
+        for net, inp in ((ac.actor, obs), (ac.critic, critic), (ac.base_lin_vel, obs)):
+            torch.testing.assert_close(ac._mlp(net, inp), net(inp), rtol=1e-5, atol=1e-5)
     for (name, _), a, b in zip([(n, p) for n, p in ac.named_parameters() if n != "std"], g_f, g_t):
         torch.testing.assert_close(a, b, rtol=2e-4, atol=2e-5, msg=lambda m: f"{name}: {m}")
     torch.testing.assert_close(gx_f, gx_t, rtol=2e-4, atol=2e-5)
