@@ -11,7 +11,7 @@
 
 extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
 extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
-extern "C" int hg_launch_post(const HgState* S, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
+extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
                               float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
                               float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
                               hipStream_t stream);
@@ -300,7 +300,7 @@ static int do_post(Sim* s, uint64_t counter, int mode, const uint8_t* mask, void
   float* pb0 = (float*)(s->arena + s->L.priv_buf[p]);
   float* pb1 = (float*)(s->arena + s->L.priv_buf[1 - p]);
   const float inv_len_s = 1.0f / ((float)s->cfg.max_episode_length * s->cfg.dt);
-  int rc = hg_launch_post(&s->S, counter, mode, mask, (float*)(s->arena + s->L.frame_obs),
+  int rc = hg_launch_post(&s->S, &s->cfg, counter, mode, mask, (float*)(s->arena + s->L.frame_obs),
                           (float*)(s->arena + s->L.frame_priv), ob0, ob1, pb0, pb1, s->cfg.frame_stack,
                           s->cfg.c_frame_stack, inv_len_s, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_post launch failed");
