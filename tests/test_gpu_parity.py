@@ -8,6 +8,7 @@
 """
 import math
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -201,6 +202,28 @@ def _ref_sim(env, S, precision):
     return sim
 
 
+def _ref_spread(env, S, a_ref, fields, trials=2, rel=1e-6):
+    """Local conditioning of the reference step: max |f64(state perturbed by ~rel) - f64(state)|
+    per output element over a few seeded perturbations of root / q / qd.  Contact dynamics are
+    stiff where a foot is at zero separation, so fp32-rounding-sized input differences can move
+    an output far more than the CPU-f32-vs-f64 gap alone predicts; the parity tolerance scales
+    with this spread as well."""
+    base = _ref_sim(env, S, "f64")
+    base.step(a_ref)
+    rng = np.random.default_rng(1234)
+    spread = {f: np.zeros_like(getattr(base, f)) for f in fields}
+    for _ in range(trials):
+        Sp = dict(S)
+        for k in ("root_states", "dof_pos", "dof_vel"):
+            x = S[k].astype(np.float64)
+            Sp[k] = x * (1 + rel * rng.standard_normal(x.shape)) + rel * 1e-3 * rng.standard_normal(x.shape)
+        rp = _ref_sim(env, Sp, "f64")
+        rp.step(a_ref)
+        for f in fields:
+            spread[f] = np.maximum(spread[f], np.abs(getattr(rp, f) - getattr(base, f)))
+    return spread
+
+
 def _step_only(env, actions, counter):
     N = _hg()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -227,11 +250,12 @@ def test_step_physics_parity(physics_env):
     r64, r32 = _ref_sim(env, S, "f64"), _ref_sim(env, S, "f32")
     r64.step(a_ref)
     r32.step(a_ref)
+    sp = _ref_spread(env, S, a_ref, ("q", "qd", "root", "torques", "rigid"))
     for name, gpu, a64, a32 in (("q", g(env.dof_pos), r64.q, r32.q), ("qd", g(env.dof_vel), r64.qd, r32.qd),
                                 ("root", g(env.root_states), r64.root, r32.root),
                                 ("torques", g(env.torques), r64.torques, r32.torques),
                                 ("rigid", g(env.rigid_state), r64.rigid, r32.rigid)):
-        tol = 20 * np.abs(a32 - a64) + 1e-3 * (1 + np.abs(a64))
+        tol = 20 * np.maximum(np.abs(a32 - a64), sp[name]) + 1e-3 * (1 + np.abs(a64))
         bad = np.abs(gpu - a64) > tol
         assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
 
@@ -410,11 +434,23 @@ def test_step_physics_parity_heightfield(terrain_env):
     r64, r32 = _ref_sim(env, S, "f64"), _ref_sim(env, S, "f32")
     r64.step(a_ref)
     r32.step(a_ref)
+    dump = os.environ.get("HG_FAIL_DUMP")
+    if dump:  # the pre-step state and both results, for offline diagnosis
+        from humanoid import _native as N
+        np.savez(dump, a_ref=a_ref, gpu_q=g(env.dof_pos), gpu_qd=g(env.dof_vel), gpu_root=g(env.root_states),
+                 gpu_cf=g(env.contact_forces), gpu_lam=g(env._view(N.T["CONTACT_LAMBDA"])), r64_lam=r64.lam,
+                 r64_cf=r64.contact, **{"S_" + k: v for k, v in S.items()})
+    sp = _ref_spread(env, S, a_ref, ("q", "qd", "root"))
+    # the spread widens the tolerance only where the reference itself is ill-conditioned
+    assert np.median(sp["qd"]) < 1e-3 and np.mean(sp["qd"] > 1e-2) < 0.05, np.percentile(sp["qd"], [50, 95, 100])
     for name, gpu, a64, a32 in (("q", g(env.dof_pos), r64.q, r32.q), ("qd", g(env.dof_vel), r64.qd, r32.qd),
                                 ("root", g(env.root_states), r64.root, r32.root)):
-        tol = 20 * np.abs(a32 - a64) + 1e-3 * (1 + np.abs(a64))
+        tol = 20 * np.maximum(np.abs(a32 - a64), sp[name]) + 1e-3 * (1 + np.abs(a64))
         bad = np.abs(gpu - a64) > tol
-        assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
+        detail = "; ".join(f"[{e},{j}] gpu {gpu[e, j]:+.5f} f32 {a32[e, j]:+.5f} f64 {a64[e, j]:+.5f} "
+                           f"spread {sp[name][e, j]:.2e} root_z {S['root_states'][e, 2]:.3f}"
+                           for e, j in np.argwhere(bad)[:6])
+        assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}: {detail}"
     # the robots stand on terrain: base heights follow the sub-terrain origins, not z = 0
     assert np.isfinite(g(env.root_states)).all()
 
