@@ -8,7 +8,7 @@
 //   _get_phase/_get_gait_phase/compute_ref_state :683-744, _get_noise_scale_vec :748-768,
 //   and the obs/priv clip in step() :654-657.
 // Reset is mask-based (the reference's reset_buf.nonzero() host sync :796 is gone).
-// Frame stacking (deque append + stack, :880-887) is k_stack below: a coalesced double-buffered
+// Frame stacking (deque append + stack, :880-887) is k_stack_stats below: a coalesced double-buffered
 // shift of the [N, frames*width] row-major history.
 #include "hg_common.h"
 
@@ -806,34 +806,46 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   for (int i = 0; i < 6; i++) S.last_root_vel[i * np + e] = root[7 + i];
 }
 
-// history stacking: dst[e] = [src[e][W:], frame[e]] (src zeroed for reset envs); one thread per
-// output element so both the reads and the writes are contiguous.
-__global__ void __launch_bounds__(256) k_stack(const float* __restrict__ src, float* __restrict__ dst,
-                                               const float* __restrict__ frame, const uint8_t* __restrict__ reset,
-                                               int n, int width, int frames) {
-  const int row = frames * width;
-  const int64_t total = (int64_t)n * row;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int e = (int)(i / row);
-    const int k = (int)(i - (int64_t)e * row);
-    float v;
-    if (k >= row - width) v = frame[(size_t)e * width + (k - (row - width))];
-    else v = reset[e] ? 0.f : src[(size_t)e * row + k + width];
-    dst[i] = v;
+// history stacking: dst[e] = [src[e][W:], frame[e]] (src zeroed for reset envs), for the
+// observation and the privileged tables in one launch; one thread per output element so both the
+// reads and the writes are contiguous.  The last block also folds the episode statistics
+// (ep_stats[k] = acc[k] / n_reset / episode_length_s when any env reset) and clears the
+// accumulators.
+struct StackT {
+  const float* src;
+  float* dst;
+  const float* frame;
+  int width, frames;
+};
+__global__ void __launch_bounds__(256) k_stack_stats(StackT A, StackT B, const uint8_t* __restrict__ reset, int n,
+                                                     float* ep_stats, float inv_len_s) {
+  if (blockIdx.x == gridDim.x - 1) {
+    const int k = threadIdx.x;
+    float* acc = ep_stats + 24;
+    const float cnt = acc[22];
+    __syncthreads();
+    if (k < HG_NUM_REWARDS && cnt > 0.f) ep_stats[k] = acc[k] / cnt * inv_len_s;
+    if (k == 22) ep_stats[22] = cnt;
+    if (k == 23) ep_stats[23] = cnt > 0.f ? 1.f : 0.f;
+    __syncthreads();
+    if (k < 24) acc[k] = 0.f;
+    return;
   }
-}
-
-// episode statistics: ep_stats[k] = acc[k] / n_reset / episode_length_s when any env reset
-__global__ void k_ep_stats(float* ep_stats, float inv_len_s) {
-  const int k = threadIdx.x;
-  float* acc = ep_stats + 24;
-  const float cnt = acc[22];
-  __syncthreads();
-  if (k < HG_NUM_REWARDS && cnt > 0.f) ep_stats[k] = acc[k] / cnt * inv_len_s;
-  if (k == 22) ep_stats[22] = cnt;
-  if (k == 23) ep_stats[23] = cnt > 0.f ? 1.f : 0.f;
-  __syncthreads();
-  if (k < 24) acc[k] = 0.f;
+  const int rowA = A.frames * A.width, rowB = B.frames * B.width;
+  const int64_t totA = (int64_t)n * rowA, total = totA + (int64_t)n * rowB;
+  const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const bool a = i < totA;
+    const StackT& T = a ? A : B;
+    const int row = a ? rowA : rowB;
+    const int64_t j = a ? i : i - totA;
+    const int e = (int)(j / row);
+    const int k = (int)(j - (int64_t)e * row);
+    float v;
+    if (k >= row - T.width) v = T.frame[(size_t)e * T.width + (k - (row - T.width))];
+    else v = reset[e] ? 0.f : T.src[(size_t)e * row + k + T.width];
+    T.dst[j] = v;
+  }
 }
 
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
@@ -847,12 +859,10 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
   else
     hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
                        frame_priv);
-  const int64_t to = (int64_t)n * frame_stack * HG_OBS1, tp = (int64_t)n * c_frame_stack * HG_PRIV1;
-  int go = (int)std::min<int64_t>((to + 255) / 256, 4096), gp = (int)std::min<int64_t>((tp + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_stack, dim3(go), dim3(256), 0, stream, obs_src, obs_dst, frame_obs, S->reset_buf, n, HG_OBS1,
-                     frame_stack);
-  hipLaunchKernelGGL(k_stack, dim3(gp), dim3(256), 0, stream, priv_src, priv_dst, frame_priv, S->reset_buf, n,
-                     HG_PRIV1, c_frame_stack);
-  hipLaunchKernelGGL(k_ep_stats, dim3(1), dim3(64), 0, stream, S->ep_stats, inv_len_s);
+  const int64_t tot = (int64_t)n * (frame_stack * HG_OBS1 + c_frame_stack * HG_PRIV1);
+  const int g = (int)std::min<int64_t>((tot + 255) / 256, 4096) + 1;  // + the statistics block
+  const StackT A = {obs_src, obs_dst, frame_obs, HG_OBS1, frame_stack};
+  const StackT B = {priv_src, priv_dst, frame_priv, HG_PRIV1, c_frame_stack};
+  hipLaunchKernelGGL(k_stack_stats, dim3(g), dim3(256), 0, stream, A, B, S->reset_buf, n, S->ep_stats, inv_len_s);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

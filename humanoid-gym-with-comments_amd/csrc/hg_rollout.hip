@@ -35,6 +35,17 @@ template <>
 __device__ inline void store_obs<__half>(__half* dst, float v) { *dst = __float2half(v); }
 
 template <typename OT>
+__device__ inline void store_obs4(OT* dst, float4 v);
+template <>
+__device__ inline void store_obs4<float>(float* dst, float4 v) { *reinterpret_cast<float4*>(dst) = v; }
+template <>
+__device__ inline void store_obs4<__half>(__half* dst, float4 v) {
+  const __half2 a = __floats2half2_rn(v.x, v.y), b = __floats2half2_rn(v.z, v.w);
+  reinterpret_cast<__half2*>(dst)[0] = a;
+  reinterpret_cast<__half2*>(dst)[1] = b;
+}
+
+template <typename OT>
 __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, const float* __restrict__ std,
                                             const float* __restrict__ value, const float* __restrict__ obs,
                                             const float* __restrict__ cobs, int n, int A, int64_t obs_w,
@@ -42,7 +53,7 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
                                             float* __restrict__ mu_out, float* __restrict__ sigma_out,
                                             float* __restrict__ value_out, OT* __restrict__ obs_out,
                                             OT* __restrict__ cobs_out, uint64_t seed, uint64_t counter,
-                                            int env_blocks) {
+                                            int env_blocks, int vec) {
   if ((int)blockIdx.x < env_blocks) {
     const int e = blockIdx.x * TPB + threadIdx.x;
     if (e >= n) return;
@@ -63,12 +74,23 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
     if (value) value_out[e] = value[e];
     return;
   }
-  // observation rows -> storage slot (grid-stride over both tables)
+  // observation rows -> storage slot: both [n, width] tables are contiguous, so they are copied
+  // as flat arrays, 4 elements per thread (float4 loads) with a scalar tail
   const int64_t tot_o = (int64_t)n * obs_w, tot_c = (int64_t)n * cobs_w;
+  const int64_t q_o = vec ? tot_o >> 2 : 0, q_c = vec ? tot_c >> 2 : 0;
+  const int64_t r_o = tot_o - 4 * q_o, r_c = tot_c - 4 * q_c;
   const int64_t stride = (int64_t)(gridDim.x - env_blocks) * TPB;
-  for (int64_t i = (int64_t)(blockIdx.x - env_blocks) * TPB + threadIdx.x; i < tot_o + tot_c; i += stride) {
-    if (i < tot_o) store_obs<OT>(obs_out + i, obs[i]);
-    else store_obs<OT>(cobs_out + (i - tot_o), cobs[i - tot_o]);
+  const int64_t i0 = (int64_t)(blockIdx.x - env_blocks) * TPB + threadIdx.x;
+  for (int64_t i = i0; i < q_o + q_c; i += stride) {
+    const bool o = i < q_o;
+    const int64_t k = o ? i : i - q_o;
+    const float4 v = reinterpret_cast<const float4*>(o ? obs : cobs)[k];
+    store_obs4<OT>((o ? obs_out : cobs_out) + 4 * k, v);
+  }
+  for (int64_t i = i0; i < r_o + r_c; i += stride) {
+    const bool o = i < r_o;
+    const int64_t k = o ? 4 * q_o + i : 4 * q_c + (i - r_o);
+    store_obs<OT>((o ? obs_out : cobs_out) + k, (o ? obs : cobs)[k]);
   }
 }
 
@@ -96,6 +118,10 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
       !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 ||
       (critic_obs_width > 0 && (!critic_obs || !critic_obs_out)))
     return HG_ERR_ARG;
+  // 16-byte loads / 16-byte (fp32) or 8-byte (fp16) stores when every table is aligned for them
+  const uintptr_t in_al = (uintptr_t)obs | (critic_obs_width > 0 ? (uintptr_t)critic_obs : 0);
+  const uintptr_t out_al = (uintptr_t)obs_out | (critic_obs_width > 0 ? (uintptr_t)critic_obs_out : 0);
+  const int vec = in_al % 16 == 0 && out_al % (obs_fp16 ? 8 : 16) == 0;
   const int env_blocks = (num_envs + TPB - 1) / TPB;
   const int copy_blocks = 512;
   hipStream_t s = (hipStream_t)stream;
@@ -103,12 +129,12 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
     hipLaunchKernelGGL(k_act<__half>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
                        critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
                        actions_out, logp_out, mu_out, sigma_out, value_out, (__half*)obs_out,
-                       (__half*)critic_obs_out, seed, counter, env_blocks);
+                       (__half*)critic_obs_out, seed, counter, env_blocks, vec);
   else
     hipLaunchKernelGGL(k_act<float>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
                        critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
                        actions_out, logp_out, mu_out, sigma_out, value_out, (float*)obs_out, (float*)critic_obs_out,
-                       seed, counter, env_blocks);
+                       seed, counter, env_blocks, vec);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
