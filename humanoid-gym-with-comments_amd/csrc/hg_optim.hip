@@ -297,7 +297,8 @@ __global__ void __launch_bounds__(LOSS_TPB) k_ppo_loss_rows(hg_ppo_batch Bt, int
 __global__ void __launch_bounds__(256) k_ppo_loss_final(const double* __restrict__ partial, int nb, int64_t rows,
                                                        int A, const float* __restrict__ std, float c_v, float c_e,
                                                        float c_l, float* __restrict__ loss_out,
-                                                       float* __restrict__ stats, float* __restrict__ g_std) {
+                                                       float* __restrict__ stats, int accum,
+                                                       float* __restrict__ g_std) {
   // thread t sums blocks t, t+256, ... of every column (independent loads in flight), then a
   // fixed-order wave and cross-wave reduction: deterministic
   __shared__ double ws[4][4 + LOSS_MAX_A];
@@ -334,9 +335,9 @@ __global__ void __launch_bounds__(256) k_ppo_loss_final(const double* __restrict
     for (int a = 0; a < A; a++) ent += 0.5 + (double)LOG_SQRT_2PI + log((double)std[a]);
     const double surr = col[0] / n, vl = col[1] / n, lv = col[2] / (3.0 * n), kl = col[3] / n;
     loss_out[0] = (float)(surr + (double)c_v * vl - (double)c_e * ent + (double)c_l * lv);
-    stats[0] = (float)vl;
-    stats[1] = (float)surr;
-    stats[2] = (float)lv;
+    stats[0] = accum ? stats[0] + (float)vl : (float)vl;
+    stats[1] = accum ? stats[1] + (float)surr : (float)surr;
+    stats[2] = accum ? stats[2] + (float)lv : (float)lv;
     stats[3] = (float)kl;
   }
 }
@@ -362,7 +363,8 @@ extern "C" int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions) {
 
 extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float clip_lo, float clip_hi, float value_clip,
                            int clipped_value_loss, float value_loss_coef, float entropy_coef, float lin_vel_coef,
-                           float* loss_out, float* stats_out, float* grad_mu, float* grad_std, float* grad_value,
+                           float* loss_out, float* stats_out, int accumulate_stats, float* grad_mu, float* grad_std,
+                           float* grad_value,
                            float* grad_lin_vel, double* scratch, void* stream) {
   if (!B || rows <= 0 || A <= 0 || A > LOSS_MAX_A || !loss_out || !stats_out || !grad_mu || !grad_std ||
       !grad_value || !grad_lin_vel || !scratch || !B->mu || !B->std || !B->value || !B->lin_vel ||
@@ -379,7 +381,7 @@ extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float cli
   hipLaunchKernelGGL(k_ppo_loss_rows, dim3(nb), dim3(LOSS_TPB), 0, s, *B, rows, A, clip_lo, clip_hi, value_clip,
                      clipped_value_loss, c_s, c_v, c_l, grad_mu, grad_value, grad_lin_vel, scratch);
   hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(256), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
-                     entropy_coef, lin_vel_coef, loss_out, stats_out, grad_std);
+                     entropy_coef, lin_vel_coef, loss_out, stats_out, accumulate_stats, grad_std);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 

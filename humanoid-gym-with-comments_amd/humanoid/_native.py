@@ -152,7 +152,8 @@ def load_library(path=LIB_PATH):
     L.hg_adam_chunk.argtypes = []
     L.hg_ppo_loss.restype = ctypes.c_int
     L.hg_ppo_loss.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                              ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float] + [vp] * 8
+                              ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp, ctypes.c_int] + \
+        [vp] * 6
     L.hg_ppo_loss_scratch.restype = ctypes.c_int64
     L.hg_ppo_loss_scratch.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.hg_ppo_loss_backward.restype = ctypes.c_int

@@ -62,26 +62,30 @@ class _PPOLoss(torch.autograd.Function):
             raise RuntimeError("ppo_loss: std must be a contiguous [num_actions] tensor")
         L = _lib()
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        stats = torch.empty(4, dtype=torch.float32, device=dev)
+        stats_buf, accumulate = params[5], params[6]
+        stats = torch.empty(4, dtype=torch.float32, device=dev) if stats_buf is None else stats_buf
         g_mu = torch.empty(rows, A, dtype=torch.float32, device=dev)
         g_std = torch.empty(A, dtype=torch.float32, device=dev)
         g_v = torch.empty(value.shape, dtype=torch.float32, device=dev)
         g_p = torch.empty(rows, 3, dtype=torch.float32, device=dev)
         scratch = torch.empty(int(L.hg_ppo_loss_scratch(rows, A)), dtype=torch.float64, device=dev)
-        clip, vcoef, ecoef, lcoef, clipped = params
+        clip, vcoef, ecoef, lcoef, clipped = params[:5]
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         rc = L.hg_ppo_loss(ctypes.byref(b), rows, A, float(1.0 - clip), float(1.0 + clip), float(clip),
                            int(bool(clipped)), float(vcoef), float(ecoef), float(lcoef), loss.data_ptr(),
-                           stats.data_ptr(), g_mu.data_ptr(), g_std.data_ptr(), g_v.data_ptr(), g_p.data_ptr(),
+                           stats.data_ptr(), int(bool(accumulate)), g_mu.data_ptr(), g_std.data_ptr(), g_v.data_ptr(), g_p.data_ptr(),
                            scratch.data_ptr(), s)
         if rc != 0:
             raise RuntimeError(f"hg_ppo_loss failed ({rc})")
         ctx.save_for_backward(g_mu, g_std, g_v, g_p)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
+        if stats_buf is not None:
+            return loss  # the statistics went to the caller's buffer
         ctx.mark_non_differentiable(stats)
         return loss, stats
 
     @staticmethod
-    def backward(ctx, g_loss, g_stats):
+    def backward(ctx, g_loss, g_stats=None):
         g_mu, g_std, g_v, g_p = ctx.saved_tensors
         rows, A = g_mu.shape
         g_loss = g_loss.contiguous()
@@ -94,12 +98,15 @@ class _PPOLoss(torch.autograd.Function):
 
 
 def ppo_loss(mu, std, value, lin_vel, data, clip_param, value_loss_coef, entropy_coef, lin_vel_coef,
-             use_clipped_value_loss=True):
+             use_clipped_value_loss=True, stats_out=None, accumulate=False):
     """(loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean] (detached).
+    With ``stats_out`` (a float32 [4] device buffer) the statistics are written there instead —
+    ``accumulate`` adds the three losses to its first entries — and only the loss is returned.
 
     ``mu`` [B, A] actor mean, ``std`` [A] the policy's std parameter, ``value`` [B, 1] critic
     output, ``lin_vel`` [B, 3] lin-vel estimate; ``data``: dict of the minibatch's stored
     tensors ``actions``, ``old_logp``, ``advantages``, ``target_values``, ``returns``,
     ``old_mu``, ``old_sigma`` and ``lin_vel_target`` (row views with unit column stride)."""
     return _PPOLoss.apply(mu, std, value, lin_vel, data,
-                          (clip_param, value_loss_coef, entropy_coef, lin_vel_coef, use_clipped_value_loss))
+                          (clip_param, value_loss_coef, entropy_coef, lin_vel_coef, use_clipped_value_loss,
+                           stats_out, accumulate))

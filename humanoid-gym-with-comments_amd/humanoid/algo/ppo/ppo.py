@@ -317,7 +317,7 @@ class PPO:
         return self._on_device and self.use_fused_loss and not self.sym_loss
 
     def _losses_fused(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
-                      old_mu_b, old_sigma_b):
+                      old_mu_b, old_sigma_b, stats_out=None):
         """The loss of _losses (and the adaptive schedule's KL mean) from the three network
         outputs in one fused HIP forward launch pair and one backward launch (hg_loss.py).
         Returns (loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean]."""
@@ -330,7 +330,8 @@ class PPO:
                 "returns": returns_b, "old_mu": old_mu_b, "old_sigma": old_sigma_b,
                 "lin_vel_target": lin_vel_b if lin_vel_b.dtype == torch.float32 else lin_vel_b.float()}
         return ppo_loss(mu, ac.std, value_b, est_lin_vel, data, self.clip_param, self.value_loss_coef,
-                        self.entropy_coef, self.base_lin_vel_coef, self.use_clipped_value_loss)
+                        self.entropy_coef, self.base_lin_vel_coef, self.use_clipped_value_loss,
+                        stats_out=stats_out, accumulate=stats_out is not None)
 
     def _losses(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b):
         """Minibatch loss (ppo.py:155-214).  The reference calls actor_critic.act() here and
@@ -454,8 +455,11 @@ class PPO:
         widths = [t.shape[-1] for t in self._pack_src]
         self._packed = torch.empty(obs.shape[0], sum(widths), dtype=torch.float32, device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
-        self._sums = torch.zeros(3, dtype=torch.float32, device=dev)
-        self._kl = torch.zeros((), dtype=torch.float32, device=dev)
+        # [value, surrogate, lin-vel loss sums, KL mean of the current minibatch]: the fused loss
+        # accumulates into it directly
+        self._stats4 = torch.zeros(4, dtype=torch.float32, device=dev)
+        self._sums = self._stats4[:3]
+        self._kl = self._stats4[3:]
         ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         torch.cuda.synchronize(dev)
         if self._flat_grad is None:
@@ -471,11 +475,9 @@ class PPO:
                                   pk.split(widths, dim=1)):
                 b[name] = part
             if self._fused_loss:
-                loss, stats = self._losses_fused(b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"],
-                                                 b["adv"], b["returns"], b["logp"], b["mu"], b["sigma"])
-                if self._adaptive:
-                    self._kl.copy_(stats[3])
-                self._sums.add_(stats[:3])
+                loss = self._losses_fused(b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"],
+                                          b["adv"], b["returns"], b["logp"], b["mu"], b["sigma"],
+                                          stats_out=self._stats4)
             else:
                 loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
                     b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"],

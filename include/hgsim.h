@@ -274,6 +274,8 @@ int hg_kl_lr_rule(const float* kl, double* lr64, float* lr32, double desired_kl,
  *   loss_out[0] = surrogate + value_loss_coef*value_loss - entropy_coef*entropy
  *                 + lin_vel_coef*lin_vel_loss
  *   stats_out[0..3] = value_loss, surrogate_loss, lin_vel_loss, kl_mean
+ * (accumulate_stats != 0: stats_out[0..2] += the three losses, stats_out[3] = kl_mean — the
+ * running sums of an update need no extra launch)
  * and the gradients of loss_out[0] with respect to mu [rows, A], std [A], value [rows] and
  * lin_vel [rows, 3] (contiguous) — unscaled; hg_ppo_loss_backward multiplies them in place by
  * the device scalar grad_loss (the chain rule of loss.backward()).  Ties of torch.max and the
@@ -296,7 +298,8 @@ typedef struct hg_ppo_batch {
 } hg_ppo_batch;
 int hg_ppo_loss(const hg_ppo_batch* batch, int64_t rows, int num_actions, float clip_lo, float clip_hi,
                 float value_clip, int clipped_value_loss, float value_loss_coef, float entropy_coef,
-                float lin_vel_coef, float* loss_out, float* stats_out, float* grad_mu, float* grad_std,
+                float lin_vel_coef, float* loss_out, float* stats_out, int accumulate_stats, float* grad_mu,
+                float* grad_std,
                 float* grad_value, float* grad_lin_vel, double* scratch /* >= hg_ppo_loss_scratch() doubles */,
                 void* stream);
 int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions);
