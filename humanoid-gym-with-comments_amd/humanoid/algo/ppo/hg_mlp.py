@@ -59,9 +59,11 @@ def _skinny_ok(h, W):
             and h.stride(0) % 4 == 0 and h.data_ptr() % 16 == 0 and W.is_contiguous())
 
 
-def _skinny_forward(h, W, b):
+def _skinny_forward(h, W, b, out=None):
     rows, n = h.shape[0], W.shape[0]
-    y = torch.empty(rows, n, dtype=torch.float32, device=h.device)
+    y = torch.empty(rows, n, dtype=torch.float32, device=h.device) if out is None else out
+    if y.numel() != rows * n or not y.is_contiguous() or y.dtype != torch.float32:
+        raise RuntimeError("skinny forward: out must be a contiguous float32 tensor of rows x n elements")
     rc = N.lib().hg_linear_skinny_forward(h.data_ptr(), h.stride(0), W.data_ptr(), b.data_ptr(), y.data_ptr(), rows,
                                           n, W.shape[1], _stream(h.device))
     if rc != 0:
@@ -145,14 +147,18 @@ def mlp_forward(net, x):
     return _MLP.apply(x, *_params(net))
 
 
-def mlp_infer(net, x):
+def mlp_infer(net, x, out=None):
     """net(x) without autograd (rollout inference): torch's Linear/ELU for the hidden layers, the
-    skinny HIP kernel for the output layer."""
+    skinny HIP kernel for the output layer (written into ``out`` when given)."""
     mods = list(net)
     h = x
     for m in mods[:-1]:
         h = m(h)
     last = mods[-1]
     if _skinny_ok(h, last.weight):
-        return _skinny_forward(h, last.weight, last.bias)
-    return last(h)
+        return _skinny_forward(h, last.weight, last.bias, out)
+    y = last(h)
+    if out is not None:
+        out.view_as(y).copy_(y)
+        return out
+    return y

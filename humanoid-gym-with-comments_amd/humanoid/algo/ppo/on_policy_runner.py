@@ -96,6 +96,11 @@ class OnPolicyRunner:
             if hasattr(self.env, "update_push_curriculum"):
                 self.env.update_push_curriculum(it)
             start = time.time()
+            on_gpu = self.device != "cpu" and torch.device(self.device).type == "cuda"
+            if on_gpu:
+                # phase times from HIP events: no host synchronisation between collection and learning
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                ev[0].record()
             with torch.inference_mode():
                 for _ in range(self.num_steps_per_env):
                     actions = self.alg.act(obs, critic_obs)
@@ -114,8 +119,8 @@ class OnPolicyRunner:
                         lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
                         cur_reward_sum[new_ids] = 0
                         cur_episode_length[new_ids] = 0
-                if self.device != "cpu" and torch.device(self.device).type == "cuda":
-                    torch.cuda.synchronize(self.device)
+                if on_gpu:
+                    ev[1].record()
                 stop = time.time()
                 collection_time = stop - start
                 self.env.course_gain *= self.env.course_ratio
@@ -126,6 +131,11 @@ class OnPolicyRunner:
             mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss = self.alg.update()
             stop = time.time()
             learn_time = stop - start
+            if on_gpu:
+                ev[2].record()
+                ev[2].synchronize()
+                collection_time = ev[0].elapsed_time(ev[1]) * 1e-3
+                learn_time = ev[1].elapsed_time(ev[2]) * 1e-3
             self.last_iteration_stats = dict(collection_time=collection_time, learn_time=learn_time,
                                              value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
                                              lin_vel_loss=mean_base_lin_vel_loss)

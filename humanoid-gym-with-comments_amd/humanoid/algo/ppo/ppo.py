@@ -26,6 +26,7 @@ import torch.optim as optim
 
 from .actor_critic import ActorCritic, _DiagGaussian
 from .hg_adam import HgAdam
+from . import hg_mlp
 from .hg_loss import ppo_loss
 from .rollout_storage import RolloutStorage
 
@@ -249,10 +250,20 @@ class PPO:
     def _finish_deferred_values(self):
         st, ac = self.storage, self.actor_critic
         T, n = st.num_transitions_per_env, st.num_envs
-        v = ac._mlp(ac.critic, st.privileged_observations.flatten(0, 1)).view(T, n, 1)
-        st.values.copy_(v)
-        # time-out bootstrap, as process_env_step (ppo.py:132-133): r += gamma * V * time_out
-        st.rewards.add_(self.gamma * (st.values * st.time_outs))
+        x = st.privileged_observations.flatten(0, 1)
+        if ac.policy_dtype == "fp32" and ac.fused_mlp and hg_mlp.fusable(ac.critic):
+            hg_mlp.mlp_infer(ac.critic, x if x.dtype == torch.float32 else x.float(), out=st.values)
+            # time-out bootstrap, as process_env_step (ppo.py:132-133): r += gamma * V * time_out,
+            # in place over the whole [T, N] rollout in one launch (hg_rollout_env)
+            from humanoid import _native as N
+            p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+            s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+            N.check(N.lib().hg_rollout_env(p(st.rewards), p(st.dones), p(st.time_outs), p(st.values), T * n,
+                                           ctypes.c_float(self.gamma), p(st.rewards), p(st.dones), None, s))
+        else:
+            v = ac._mlp(ac.critic, x).view(T, n, 1)
+            st.values.copy_(v)
+            st.rewards.add_(self.gamma * (st.values * st.time_outs))
         st.values_deferred = False
 
     def compute_returns(self, last_critic_obs):
