@@ -65,7 +65,9 @@ class PPO:
         if self.world_size > 1:
             # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack copies
             numel = sum(p.numel() for p in self._params)
-            self._flat_grad = torch.zeros(numel, device=self._params[0].device, dtype=torch.float32)
+            # + one trailing slot: the minibatch KL mean rides along with the gradient all-reduce
+            self._flat_grad = torch.zeros(numel + 1, device=self._params[0].device, dtype=torch.float32)
+            self._kl_slot = self._flat_grad[numel:]
             off = 0
             for p in self._params:
                 p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
@@ -497,13 +499,17 @@ class PPO:
                     ac = self.actor_critic
                     self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
                 self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
+            if self.world_size > 1 and self._adaptive:
+                self._kl_slot.copy_(self._kl)
             loss.backward()
         with torch.cuda.graph(gb, pool=ga.pool()):
+            kl = self._kl
             if self.world_size > 1:
+                # gradients and the KL mean were summed over ranks in ONE all-reduce
                 self._flat_grad.div_(self.world_size)
-                self._kl.div_(self.world_size)
+                kl = self._kl_slot
             if self._adaptive:
-                self._lr_rule_device(self._kl)
+                self._lr_rule_device(kl)
             self._clip_and_step()
         self._graphs = (ga, gb, mb, self._storage_key())
 
@@ -533,9 +539,7 @@ class PPO:
                 self._idx.copy_(indices[i * mb:(i + 1) * mb])
                 ga.replay()
                 if self.world_size > 1:
-                    dist.all_reduce(self._flat_grad)
-                    if self._adaptive:
-                        dist.all_reduce(self._kl)
+                    dist.all_reduce(self._flat_grad)  # gradients + the KL slot
                 gb.replay()
         num_updates = self.num_learning_epochs * nmb
         v, s, lv = (self._sums / num_updates).tolist()  # the one host read of the update
