@@ -85,6 +85,25 @@ def _skinny_backward(g, h, W, need_dx):
     return wb[: n * k].view(n, k), wb[n * k:], dx
 
 
+# Split-K factors for the weight gradients dW[n, k] = gh[R, n]^T x[R, k] at the 24576-row
+# minibatch: the reduction over R is cut into S row chunks computed as one batched GEMM and summed
+# in a fixed order.  Small outputs (128 x 256, 256 x 512, ...) expose too few output tiles to fill
+# 256 CUs, so BLAS runs them at 30-90 TFLOP/s; measured on MI355X with TunableOp-tuned kernels for
+# every variant (scripts/dw_probe.py): 128x256 51 -> 25 us (S=8), 256x512 80 -> 58 us (S=4),
+# 768x219 105 -> 92 us (S=4), 256x768 106 -> 86 us (S=4).
+_DW_SPLIT = {(128, 256): 8, (128, 128): 4, (256, 512): 4, (128, 705): 8, (512, 705): 2, (768, 219): 4,
+             (256, 768): 4}
+
+
+def _weight_grad(gh, x):
+    rows, n = gh.shape
+    k = x.shape[1]
+    S = _DW_SPLIT.get((n, k), 1) if rows >= 8192 else 1
+    if S == 1 or rows % S or not (gh.is_contiguous() and x.is_contiguous()):
+        return torch.mm(gh.t(), x)
+    return torch.bmm(gh.view(S, rows // S, n).transpose(1, 2), x.view(S, rows // S, k)).sum(0)
+
+
 class _MLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params):
@@ -124,7 +143,7 @@ class _MLP(torch.autograd.Function):
                 # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
                 gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb)
                 grads[2 * i + 1] = gb
-                grads[2 * i] = torch.mm(gh.t(), ins[i])
+                grads[2 * i] = _weight_grad(gh, ins[i])
                 gnext = torch.mm(gh, Ws[i]) if need_dx else None
             if i > 0:
                 # the next (lower) layer's incoming gradient goes through its ELU backward
