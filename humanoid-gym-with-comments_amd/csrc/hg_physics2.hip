@@ -232,6 +232,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const hg_model* M = S.model;
   const int np = S.np;
   const float dt = cfg->sim_dt;
+  const float inv_dt = 1.0f / dt;
   const bool fixed = cfg->fix_base_link != 0;
   const float gz = cfg->gravity_z;
   STAMP_DECL
@@ -420,8 +421,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         if (j < nf) {
           const float d = RL(a[j], j);
           nonpd |= !(d > 0.f);
-          const float sd = sqrtf(fmaxf(d, 1e-20f));
-          const float inv = 1.0f / sd;
+          // pivot: one v_rsq_f32 (1 ulp) instead of the correctly rounded sqrt + IEEE division
+          // expansions (~22 dependent instructions) on the column chain's critical path
+          const float dd = fmaxf(d, 1e-20f);
+          const float inv = __builtin_amdgcn_rsqf(dd);
+          const float sd = dd * inv;
           a[j] = (l == j) ? sd : (l > j ? a[j] * inv : a[j]);
           myinv = (l == j) ? inv : myinv;
 #pragma unroll
@@ -530,7 +534,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           f3 t1 = mk(1, 0, 0) - cn.x * cn;
           t1 = rsqrtf(dot(t1, t1)) * t1;
           f3 t2 = cross(cn, t1);
-          const float tgt = phi >= 0.f ? -phi / dt : fminf(-beta * phi / dt, vmax);
+          const float tgt = phi >= 0.f ? -phi * inv_dt : fminf(-beta * phi * inv_dt, vmax);
           for (int d = 0; d < 3; d++) {
             const int r = start + d;
             f3 dir = d == 0 ? cn : (d == 1 ? t1 : t2);
@@ -546,7 +550,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         const int j = l - 16;
         const int r = 3 * nc + __popc(ml & ((1u << j) - 1u));
         if (act_l && r < RMAX) {
-          E.rc[r].kind = 3; E.rc[r].tgt = gapv >= 0.f ? -gapv / dt : fminf(-beta * gapv / dt, vmax);
+          E.rc[r].kind = 3; E.rc[r].tgt = gapv >= 0.f ? -gapv * inv_dt : fminf(-beta * gapv * inv_dt, vmax);
           E.rPt[r] = j; E.rBody[r] = -1;
           E.rd[r][0] = sgnv;
           E.rLam[r] = E.lamst[HG_NC * 3 + j];
@@ -630,7 +634,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     float wrow[RMAX];
 #pragma unroll
     for (int m = 0; m < RMAX; m++) wrow[m] = (m % 8 < 4) ? wA[4 * (m / 8) + m % 8] : wB[4 * (m / 8) + m % 8 - 4];
-    float mylam = own ? E.rLam[l] : 0.f;
     if (own) {
       float D = 0.f;
 #pragma unroll
@@ -641,7 +644,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
       for (int m = 0; m < RMAX; m++)
         if (m < nrows) v0 += wrow[m] * E.rLam[m];
-      E.rc[l].invD = 1.0f / D;
+      E.rc[l].invD = __builtin_amdgcn_rcpf(D);
       vrow = v0;
     }
     __syncthreads();
@@ -653,14 +656,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     STAMP(10);
     STAMP(11);
-    // ---- A14: projected Gauss-Seidel, rows in order (normal, then its tangent pair).  Row state
-    // (v_r, lambda_r) lives in lane r and is read with v_readlane; the update is uniform over the
+    // ---- A14: projected Gauss-Seidel, rows in order (normal, then its tangent pair).  The row
+    // velocity v_r lives in lane r and is read with v_readlane; the impulses are replicated: every
+    // lane of an env holds all 32 of its env's impulses in registers (uniform per half-wave), so
+    // reading and updating lambda_r costs no cross-lane traffic.  The update is uniform over the
     // env's 32 lanes and branch-free (both halves of the wave run it whatever their row kinds):
     //   normal / limit row:  lambda <- max(lambda + (tgt - v) / D, 0)
     //   tangent pair (r, r+1): unconstrained 2-D step, projected onto the disc mu * lambda_n,
     //   lambda_n being the normal impulse updated one row earlier
     //   kind 2 / unused rows: no-op (rc.kind = 2 for rows >= nrows)
     {
+      float lam[RMAX];
+#pragma unroll
+      for (int m = 0; m < RMAX; m++) lam[m] = m < nrows ? E.rLam[m] : 0.f;
       const float mu = 0.5f * (E.fric + cfg->ground_friction);
       const int npgs = cfg->pgs_iterations;
       for (int it = 0; it < npgs; it++) {
@@ -669,32 +677,38 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         for (int r = 0; r < RMAX; r++) {
           if (live_rows & (1u << r)) {
           const RowC c = E.rc[r];
-          const float vr = RL(vrow, r), lr = RL(mylam, r);
+          const float vr = RL(vrow, r), lr = lam[r];
           const bool isF = c.kind == 1, isN = c.kind == 0 || c.kind == 3;
           const float ln = fmaxf(lr + (c.tgt - vr) * c.invD, 0.f);
-          float dl0 = isN ? ln - lr : 0.f, dl1 = 0.f;
+          float dl0 = isN ? ln - lr : 0.f;
           if (r + 1 < RMAX) {
-            const float vr2 = RL(vrow, r + 1), lr2 = RL(mylam, r + 1);
+            const float vr2 = RL(vrow, r + 1), lr2 = lam[r + 1];
             float l1 = lr - vr * c.invD, l2 = lr2 - vr2 * c.invD2;
             const float lim = mu * prev_ln, nn2 = l1 * l1 + l2 * l2;
             const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
             dl0 = isF ? l1 * sc - lr : dl0;
-            dl1 = isF ? l2 * sc - lr2 : 0.f;
+            const float dl1 = isF ? l2 * sc - lr2 : 0.f;
             vrow += wrow[r] * dl0 + wrow[r + 1] * dl1;
+            lam[r + 1] += dl1;
           } else {
             vrow += wrow[r] * dl0;
           }
-          mylam += (l == r ? dl0 : 0.f) + (l == r + 1 ? dl1 : 0.f);
+          lam[r] += dl0;
           prev_ln = isN ? ln : prev_ln;
           }
         }
       }
+      STAMP(12);
+      // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
+      if (l == 0) {
+#pragma unroll
+        for (int m = 0; m < RMAX; m++)
+          if (m < nrows) E.rLam[m] = lam[m];
+      }
     }
-    STAMP(12);
-    // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
-    if (own) E.rLam[l] = mylam;
     for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
     __syncthreads();
+    const float mylam = own ? E.rLam[l] : 0.f;
     float nu_new = 0.f;
     if (l < 18) {
       float s = E.nu[l];
@@ -708,7 +722,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       } else {
         E.lamst[E.rPt[l] * 3 + kind] = mylam;
         const int b = E.rBody[l];
-        const float s = mylam / dt;
+        const float s = mylam * inv_dt;
         atomicAdd(&E.cf[b][0], E.rd[l][0] * s);
         atomicAdd(&E.cf[b][1], E.rd[l][1] * s);
         atomicAdd(&E.cf[b][2], E.rd[l][2] * s);
