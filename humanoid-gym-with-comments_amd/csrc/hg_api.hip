@@ -10,7 +10,8 @@
 #include "hg_common.h"
 
 extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
-extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
+extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
+                               hipStream_t stream);
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
                               float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
                               float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
@@ -288,7 +289,7 @@ int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream
   Sim* s = (Sim*)sim;
   if (!s || !actions) return fail(s, HG_ERR_ARG, "null argument");
   const int rc = s->physics_version == 1 ? hg_launch_step(&s->S, actions, step_counter, (hipStream_t)stream)
-                                         : hg_launch_step2(&s->S, actions, step_counter, (hipStream_t)stream);
+                                         : hg_launch_step2(&s->S, actions, step_counter, s->cfg.fix_base_link, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_step launch failed");
   return HG_OK;
 }

@@ -211,9 +211,19 @@ __device__ __forceinline__ void swap32(float x, float z, float& xo, float& zo) {
   zo = __uint_as_float(r[1]);
 }
 __device__ __forceinline__ float hsel(int half, float lo, float hi) { return half ? hi : lo; }
+// the lane index through an empty volatile asm: lane masks built from it are recomputed where
+// they are used (one v_cmp) instead of being hoisted out of the substep loop into SGPR pairs
+// that spill to VGPR lanes (two v_readlane per restore)
+__device__ __forceinline__ int lane_opaque(int l) {
+  asm volatile("" : "+v"(l));
+  return l;
+}
 
 }  // namespace
 
+// FIXED = asset.fix_base_link, a compile-time constant so the factorised size and every
+// floating-base branch resolve at compile time (no per-entry scalar branches in the Cholesky)
+template <bool FIXED>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_step2(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
   __shared__ EnvSh shm[2];
   const int half = threadIdx.x >> 5;
@@ -233,7 +243,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int np = S.np;
   const float dt = cfg->sim_dt;
   const float inv_dt = 1.0f / dt;
-  const bool fixed = cfg->fix_base_link != 0;
+  constexpr bool fixed = FIXED;
   const float gz = cfg->gravity_z;
   STAMP_DECL
 
@@ -402,10 +412,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // columns are skipped.  Lane i holds row i; column j's entries L[k][j] reach the other rows
     // by v_readlane (no LDS round trips, no barriers).  Fixed base: the base block (i >= 12) is
     // dropped.  Entries right of a lane's diagonal are never read.
-    const int nf = fixed ? 12 : 18;  // factorised size
+    constexpr int nf = fixed ? 12 : 18;  // factorised size
     {
       float a[18];
-      float myinv = 0.f;
       bool nonpd = false;
       const int ol = l < 12 ? 6 + l : l - 12;  // this lane's dof
       for (int rep = 0; rep < HG_REP_CHOL; rep++) {
@@ -417,22 +426,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       }
       asm volatile("" ::: "memory");
 #pragma unroll
-      for (int j = 0; j < 18; j++) {
-        if (j < nf) {
-          const float d = RL(a[j], j);
-          nonpd |= !(d > 0.f);
-          // pivot: one v_rsq_f32 (1 ulp) instead of the correctly rounded sqrt + IEEE division
-          // expansions (~22 dependent instructions) on the column chain's critical path
-          const float dd = fmaxf(d, 1e-20f);
-          const float inv = __builtin_amdgcn_rsqf(dd);
-          const float sd = dd * inv;
-          a[j] = (l == j) ? sd : (l > j ? a[j] * inv : a[j]);
-          myinv = (l == j) ? inv : myinv;
+      for (int j = 0; j < nf; j++) {
+        const float d = RL(a[j], j);
+        nonpd |= !(d > 0.f);
+        // pivot: one v_rsq_f32 (1 ulp) instead of the correctly rounded sqrt + IEEE division
+        // expansions (~22 dependent instructions) on the column chain's critical path; the
+        // diagonal lane's d * rsq(d) is its sqrt, so one lane mask (l >= j) covers column j
+        const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));
+        a[j] = (lane_opaque(l) >= j) ? a[j] * inv : a[j];
+        // rank-1 update of the trailing rows, per half-wave: with exec restricted to one env's
+        // lanes, the column entry L[k][j] is ONE v_readlane operand of the FMA (no per-lane pick
+        // between the two envs' readlanes)
+        if (half == 0) {
 #pragma unroll
-          for (int k = j + 1; k < 18; k++) {
+          for (int k = j + 1; k < nf; k++) {
             if (j < 6 && k >= 6 && k < 12) continue;  // structural zero: left-leg pivot, right-leg row
-            if (k >= nf) continue;
-            a[k] -= a[j] * RL(a[j], k);
+            a[k] -= a[j] * readlane_f(a[j], k);
+          }
+        } else {
+#pragma unroll
+          for (int k = j + 1; k < nf; k++) {
+            if (j < 6 && k >= 6 && k < 12) continue;
+            a[k] -= a[j] * readlane_f(a[j], 32 + k);
           }
         }
       }
@@ -440,7 +455,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       if (l < 18) {
 #pragma unroll
         for (int k = 0; k < 18; k++) E.u.fac.M[l][k] = a[k];
-        E.u.fac.invd[l] = myinv;
+        // 1 / L_ll from the lane's own row (same-lane LDS write then read: no barrier needed)
+        E.u.fac.invd[l] = __builtin_amdgcn_rcpf(E.u.fac.M[l][l < 18 ? l : 0]);
       }
       if (l == 0 && nonpd) E.bad = 1;
     }
@@ -820,8 +836,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   for (int i = l; i < HG_LAMW; i += 32) S.lambda[i * np + e] = E.lamst[i];
 }
 
-extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream) {
+extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
+                               hipStream_t stream) {
   const int grid = (S->n + 1) / 2;
-  hipLaunchKernelGGL(k_step2, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);
+  if (fixed_base)
+    hipLaunchKernelGGL(k_step2<true>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);
+  else
+    hipLaunchKernelGGL(k_step2<false>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
