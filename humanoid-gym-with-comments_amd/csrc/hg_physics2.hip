@@ -272,14 +272,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   __syncthreads();
   const float scale0 = E.mass0 / M->mass[0];
+  // PD constants of this lane's joint in registers for all substeps (one global load each per
+  // launch instead of per substep); the position target is constant over the policy step
+  float pd_kp = 0.f, pd_kd = 0.f, pd_lim = 0.f, pd_tgt = 0.f;
+  if (l < 12) {
+    pd_kp = cfg->kp[l];
+    pd_kd = cfg->kd[l];
+    pd_lim = cfg->torque_limit[l];
+    pd_tgt = E.act[l] * cfg->action_scale + cfg->default_dof_pos[l];
+  }
+  const int decimation = cfg->decimation;
 
-
-  for (int sub = 0; sub < cfg->decimation; sub++) {
+  for (int sub = 0; sub < decimation; sub++) {
     STAMP(0);
     // ---- A1: torques (_compute_torques, humanoid_env.py:910-925), generalized velocity
     if (l < 12) {
-      float t = cfg->kp[l] * (E.act[l] * cfg->action_scale + cfg->default_dof_pos[l] - E.q[l]) - cfg->kd[l] * E.qd[l];
-      E.tau[l] = fminf(fmaxf(t, -cfg->torque_limit[l]), cfg->torque_limit[l]);
+      float t = pd_kp * (pd_tgt - E.q[l]) - pd_kd * E.qd[l];
+      E.tau[l] = fminf(fmaxf(t, -pd_lim), pd_lim);
       E.nu[6 + l] = E.qd[l];
     }
     if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
