@@ -52,6 +52,11 @@ constexpr int RMAX = 32;
 #ifndef HG_REP_MFMA
 #define HG_REP_MFMA 1
 #endif
+// Cholesky column broadcast: 1 = through LDS (one FMA per trailing entry for both envs),
+// 0 = v_readlane per half-wave
+#ifndef HG_CHOL_LDS
+#define HG_CHOL_LDS 1
+#endif
 
 struct RowC {  // per-row constants of the PGS, one 16-byte broadcast read
   float tgt, invD, invD2;  // target velocity, 1/W_rr, 1/W_(r+1)(r+1) (tangent pair partner)
@@ -61,6 +66,7 @@ struct RowC {  // per-row constants of the PGS, one 16-byte broadcast read
 struct __align__(16) EnvSh {
   float root[16];
   float q[12], qd[12], act[12], tau[12];
+  float pd_kp[12], pd_kd[12], pd_lim[12], pd_tgt[12];  // PD constants / position target per joint
   float nu[20];
   float h[20];
   float lamst[64];
@@ -272,14 +278,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   __syncthreads();
   const float scale0 = E.mass0 / M->mass[0];
-  // PD constants of this lane's joint in registers for all substeps (one global load each per
+  // PD constants of this lane's joint staged in LDS for all substeps (one global load each per
   // launch instead of per substep); the position target is constant over the policy step
-  float pd_kp = 0.f, pd_kd = 0.f, pd_lim = 0.f, pd_tgt = 0.f;
   if (l < 12) {
-    pd_kp = cfg->kp[l];
-    pd_kd = cfg->kd[l];
-    pd_lim = cfg->torque_limit[l];
-    pd_tgt = E.act[l] * cfg->action_scale + cfg->default_dof_pos[l];
+    E.pd_kp[l] = cfg->kp[l];
+    E.pd_kd[l] = cfg->kd[l];
+    E.pd_lim[l] = cfg->torque_limit[l];
+    E.pd_tgt[l] = E.act[l] * cfg->action_scale + cfg->default_dof_pos[l];
   }
   const int decimation = cfg->decimation;
 
@@ -287,8 +292,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     STAMP(0);
     // ---- A1: torques (_compute_torques, humanoid_env.py:910-925), generalized velocity
     if (l < 12) {
-      float t = pd_kp * (pd_tgt - E.q[l]) - pd_kd * E.qd[l];
-      E.tau[l] = fminf(fmaxf(t, -pd_lim), pd_lim);
+      float t = E.pd_kp[l] * (E.pd_tgt[l] - E.q[l]) - E.pd_kd[l] * E.qd[l];
+      E.tau[l] = fminf(fmaxf(t, -E.pd_lim[l]), E.pd_lim[l]);
       E.nu[6 + l] = E.qd[l];
     }
     if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
@@ -434,6 +439,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         a[k] = (l < 18) ? (ol >= ok ? E.u.fac.M[l < 18 ? ol : 0][ok] : E.u.fac.M[ok][l < 18 ? ol : 0]) : 0.f;
       }
       asm volatile("" ::: "memory");
+#if HG_CHOL_LDS
+      // column broadcast through LDS: every lane writes its (unscaled) column-j entry, then reads
+      // the pivot and the trailing entries back as half-wave broadcasts; the rank-1 update is then
+      // ONE FMA per trailing entry for both envs of the wave.  Same-wave LDS accesses complete in
+      // order, so no barrier.  Y (written only in A12) holds the scratch column.
+      float* colbuf = &E.Y[0][0];
+#pragma unroll
+      for (int j = 0; j < nf; j++) {
+        if (l < 18) colbuf[l] = a[j];
+        const float d = colbuf[j];
+        nonpd |= !(d > 0.f);
+        const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));  // 1 ulp, see the readlane form
+        const float t = a[j] * (inv * inv);  // L[l][j] / L[j][j]
+        a[j] = (lane_opaque(l) >= j) ? a[j] * inv : a[j];
+#pragma unroll
+        for (int k = j + 1; k < nf; k++) {
+          if (j < 6 && k >= 6 && k < 12) continue;  // structural zero: left-leg pivot, right-leg row
+          a[k] -= t * colbuf[k];  // L[l][j] L[k][j] = (a_lj / d) a_kj
+        }
+      }
+#else
 #pragma unroll
       for (int j = 0; j < nf; j++) {
         const float d = RL(a[j], j);
@@ -460,6 +486,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           }
         }
       }
+#endif
       }
       if (l < 18) {
 #pragma unroll

@@ -146,3 +146,75 @@ extern "C" int hg_rollout_env(const float* rewards, const uint8_t* reset, const 
                      time_outs, values, num_envs, gamma, rewards_out, dones_out, time_outs_out);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Minibatch gather (RolloutStorage.mini_batch_generator, rollout_storage.py:153-191:
+// observations[batch_idx], critic_observations[batch_idx], ... ): one launch copies row idx[i]
+// of up to three row-major tables into row i of their minibatch buffers.  One wave per output
+// row, lanes along the row with 4 independent element loads in flight per lane; 4-byte or
+// 2-byte elements (the 705-wide fp32 observation rows are not 16-byte aligned, fp16 storage
+// rows not 4-byte aligned).  torch's index kernel ran these at ~2.2 TB/s with per-element 64-bit
+// index arithmetic.
+namespace {
+
+struct GatherTab {
+  const void* src;
+  void* dst;
+  int64_t width;  // elements per row
+  int es;         // element bytes: 4 or 2
+};
+struct GatherArgs {
+  GatherTab t[3];
+  int ntab;
+};
+
+template <typename E>
+__device__ inline void gather_row(const E* __restrict__ src, E* __restrict__ dst, int64_t w, int lane) {
+  int64_t j = lane;
+  for (; j + 192 < w; j += 256) {
+    const E a = src[j], b = src[j + 64], c = src[j + 128], d = src[j + 192];
+    dst[j] = a;
+    dst[j + 64] = b;
+    dst[j + 128] = c;
+    dst[j + 192] = d;
+  }
+  for (; j < w; j += 64) dst[j] = src[j];
+}
+
+__global__ void __launch_bounds__(TPB) k_gather_rows(const int64_t* __restrict__ idx, int64_t rows,
+                                                     int64_t src_rows, GatherArgs A) {
+  const int64_t i = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= rows) return;
+  int64_t s = idx[i];
+  s = s < 0 ? 0 : (s >= src_rows ? src_rows - 1 : s);  // never read out of bounds
+  for (int t = 0; t < A.ntab; t++) {
+    const GatherTab& T = A.t[t];
+    if (T.es == 4)
+      gather_row<uint32_t>((const uint32_t*)T.src + s * T.width, (uint32_t*)T.dst + i * T.width, T.width, lane);
+    else
+      gather_row<uint16_t>((const uint16_t*)T.src + s * T.width, (uint16_t*)T.dst + i * T.width, T.width, lane);
+  }
+}
+
+}  // namespace
+
+extern "C" int hg_gather_rows(const int64_t* idx, int64_t rows, int64_t src_rows, const void* src0, void* dst0,
+                              int64_t width0, int es0, const void* src1, void* dst1, int64_t width1, int es1,
+                              const void* src2, void* dst2, int64_t width2, int es2, void* stream) {
+  if (!idx || rows <= 0 || src_rows <= 0 || !src0 || !dst0) return HG_ERR_ARG;
+  GatherArgs A;
+  A.ntab = 0;
+  const void* src[3] = {src0, src1, src2};
+  void* dst[3] = {dst0, dst1, dst2};
+  const int64_t w[3] = {width0, width1, width2};
+  const int es[3] = {es0, es1, es2};
+  for (int t = 0; t < 3; t++) {
+    if (!src[t]) continue;
+    if (!dst[t] || w[t] <= 0 || (es[t] != 4 && es[t] != 2)) return HG_ERR_ARG;
+    A.t[A.ntab++] = GatherTab{src[t], dst[t], w[t], es[t]};
+  }
+  const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(TPB), 0, (hipStream_t)stream, idx, rows, src_rows, A);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

@@ -28,7 +28,7 @@ from .actor_critic import ActorCritic, _DiagGaussian
 from .hg_adam import HgAdam
 from . import hg_mlp
 from .hg_loss import ppo_loss
-from .rollout_storage import RolloutStorage
+from .rollout_storage import RolloutStorage, gather_rows
 
 
 def _world():
@@ -477,13 +477,21 @@ class PPO:
         torch.cuda.synchronize(dev)
         if self._flat_grad is None:
             self.optimizer.zero_grad(set_to_none=True)  # backward allocates the grads in the graph pool
+        # minibatch rows land in static buffers: the three row gathers are one HIP launch
+        self._mb_obs = torch.empty(mb, obs.shape[1], dtype=obs.dtype, device=dev)
+        self._mb_critic = (torch.empty(mb, critic.shape[1], dtype=critic.dtype, device=dev)
+                           if critic is not obs else self._mb_obs)
+        self._mb_packed = torch.empty(mb, self._packed.shape[1], dtype=torch.float32, device=dev)
+        tables = [(obs, self._mb_obs), (self._packed, self._mb_packed)]
+        if critic is not obs:
+            tables.insert(1, (critic, self._mb_critic))
         with torch.cuda.graph(ga):
             if self._flat_grad is not None:
                 self._flat_grad.zero_()
-            i = self._idx
-            crit_b = critic[i]
-            b = {"obs": obs[i], "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
-            pk = self._packed[i]
+            gather_rows(self._idx, tables)
+            crit_b = self._mb_critic
+            b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
+            pk = self._mb_packed
             for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma"),
                                   pk.split(widths, dim=1)):
                 b[name] = part

@@ -234,6 +234,15 @@ int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* ti
                    int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
                    void* stream);
 
+/* ---- minibatch gather (replaces the `observations.view(-1, ...)[batch_idx]` row gathers of
+ * RolloutStorage.mini_batch_generator, rollout_storage.py:153-191) ----
+ * dst_t[i, :] = src_t[idx[i], :] for up to three row-major tables (src1/src2 may be NULL) of
+ * width_t elements of es_t bytes (4 or 2); idx values outside [0, src_rows) are clamped (the
+ * caller's indices come from randperm).  One launch on `stream`, no host synchronisation. */
+int hg_gather_rows(const int64_t* idx, int64_t rows, int64_t src_rows, const void* src0, void* dst0,
+                   int64_t width0, int es0, const void* src1, void* dst1, int64_t width1, int es1,
+                   const void* src2, void* dst2, int64_t width2, int es2, void* stream);
+
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----
  * A list of float32 device tensors (param, grad, Adam exp_avg / exp_avg_sq, per-tensor step

@@ -911,3 +911,25 @@ def test_fused_mlp_backward_matches_torch():
     for (name, _), a, b in zip([(n, p) for n, p in ac.named_parameters() if n != "std"], g_f, g_t):
         torch.testing.assert_close(a, b, rtol=2e-4, atol=2e-5, msg=lambda m: f"{name}: {m}")
     torch.testing.assert_close(gx_f, gx_t, rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_gather_rows_matches_torch_indexing(dtype):
+    """hg_gather_rows vs table[idx] (the reference generator's gathers, rollout_storage.py:153-191):
+    bitwise, for the 705-wide observation rows (not 16-byte aligned), the 219-wide critic rows,
+    a narrow per-sample table, and a ragged row count."""
+    _need_gpu()
+    from humanoid.algo.ppo.rollout_storage import gather_rows
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    R = 24 * 96
+    obs = torch.randn(R, 705, device="cuda:0", generator=g).to(dtype)
+    crit = torch.randn(R, 219, device="cuda:0", generator=g).to(dtype)
+    pk = torch.randn(R, 40, device="cuda:0", generator=g)
+    for rows in (R // 4, 1, 333):
+        idx = torch.randperm(R, device="cuda:0", generator=g)[:rows]
+        d0, d1, d2 = (torch.empty(rows, t.shape[1], dtype=t.dtype, device="cuda:0") for t in (obs, crit, pk))
+        gather_rows(idx, [(obs, d0), (crit, d1), (pk, d2)])
+        torch.cuda.synchronize()
+        assert torch.equal(d0, obs[idx]) and torch.equal(d1, crit[idx]) and torch.equal(d2, pk[idx])
+    with pytest.raises(RuntimeError):
+        gather_rows(idx, [(obs, torch.empty(rows, 705, dtype=torch.float64, device="cuda:0"))])
