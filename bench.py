@@ -34,10 +34,11 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) dense peak
 HBM_PEAK_GBS = 8000.0
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_v5", "pmc_summary.json")
+PROFILE_DIR = "r1_v6"  # the committed rocprofv3 summaries of the current kernels
+PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
 
-def sq_issue(kernel_file=os.path.join(REPO, "profiles", "r1_v5", "sq_counters_k_step2.json")):
+def sq_issue(kernel_file=os.path.join(REPO, "profiles", PROFILE_DIR, "sq_counters_k_step2.json")):
     """SIMD VALU issue utilisation of K_step from the committed SQ counter passes (None if absent)."""
     try:
         with open(kernel_file) as f:
@@ -269,7 +270,7 @@ def main():
                 "hbm_achieved_GBs": round(1808 * args.envs / (ms_step * 1e-3) / 1e9, 1),
                 "hbm_frac": round(1808 * args.envs / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                 "valu_issue_util": sq_issue(),
-                "valu_issue_source": "profiles/r1_v5/sq_counters_k_step2.json (2 x SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES)",
+                "valu_issue_source": f"profiles/{PROFILE_DIR}/sq_counters_k_step2.json (2 x SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES)",
                 "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
                 "launch_sampling": f"HIP events on 1 in {timer.every} launches of the timed region",
                 "flops_per_launch": flops, "active_rows_per_env": round(rows, 2),

@@ -57,6 +57,12 @@ constexpr int RMAX = 32;
 #ifndef HG_CHOL_LDS
 #define HG_CHOL_LDS 1
 #endif
+#ifndef HG_LANE_OPAQUE
+#define HG_LANE_OPAQUE 1
+#endif
+#ifndef HG_CHOL_SB
+#define HG_CHOL_SB 0
+#endif
 
 struct RowC {  // per-row constants of the PGS, one 16-byte broadcast read
   float tgt, invD, invD2;  // target velocity, 1/W_rr, 1/W_(r+1)(r+1) (tangent pair partner)
@@ -232,8 +238,16 @@ __device__ __forceinline__ int lane_opaque(int l) {
 template <bool FIXED>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_step2(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
   __shared__ EnvSh shm[2];
+#if HG_LANE_OPAQUE > 1
+  int half = threadIdx.x >> 5;
+#else
   const int half = threadIdx.x >> 5;
+#endif
+#if HG_LANE_OPAQUE
+  int l = threadIdx.x & 31;
+#else
   const int l = threadIdx.x & 31;
+#endif
   // XCD-aware env mapping: workgroups are dispatched round-robin over the 8 XCDs (block b ->
   // XCD b % 8), each with its own L2.  Giving every XCD a contiguous range of env pairs keeps the
   // 16 envs of one 64-byte SoA line on one L2, so their 4-byte state stores merge there instead of
@@ -289,6 +303,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int decimation = cfg->decimation;
 
   for (int sub = 0; sub < decimation; sub++) {
+#if HG_LANE_OPAQUE
+    // lane masks are rebuilt per substep (v_cmp) instead of living across the loop in SGPR pairs
+    asm volatile("" : "+v"(l));
+#endif
+#if HG_LANE_OPAQUE > 1
+    asm volatile("" : "+v"(half));
+#endif
     STAMP(0);
     // ---- A1: torques (_compute_torques, humanoid_env.py:910-925), generalized velocity
     if (l < 12) {
@@ -458,6 +479,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           if (j < 6 && k >= 6 && k < 12) continue;  // structural zero: left-leg pivot, right-leg row
           a[k] -= t * colbuf[k];  // L[l][j] L[k][j] = (a_lj / d) a_kj
         }
+#if HG_CHOL_SB
+        __builtin_amdgcn_sched_barrier(0);
+#endif
       }
 #else
 #pragma unroll

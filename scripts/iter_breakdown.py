@@ -6,7 +6,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-ks = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_step2")]
+ks = [i for i, r in enumerate(rows) if "k_step2" in r["Kernel_Name"][:24]]
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 24
 # last full iteration: from the first K_step of the last group of T to the first K_step of... the end
 first = ks[-T]

@@ -14,7 +14,7 @@ def main():
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if not r["Kernel_Name"].startswith("k_step2"):
+                if "k_step2" not in r["Kernel_Name"][:24]:
                     continue
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
                 launches[r["Counter_Name"]].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
