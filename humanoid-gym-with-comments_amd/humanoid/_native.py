@@ -90,7 +90,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
            "hg_rollout_act", "hg_rollout_env", "hg_gather_rows", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
-           "hg_mlp_act_backward", "hg_mlp_act_backward_scratch", "hg_linear_skinny_supported",
+           "hg_mlp_act_backward", "hg_mlp_act_backward_scratch", "hg_colsum_jobs", "hg_linear_skinny_supported",
            "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch", "hg_version"]
 
 _LIB = None
@@ -162,6 +162,9 @@ def load_library(path=LIB_PATH):
     L.hg_ppo_loss_backward.argtypes = [vp, ctypes.c_int64, ctypes.c_int] + [vp] * 5
     L.hg_mlp_act_backward.restype = ctypes.c_int
     L.hg_mlp_act_backward.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp]
+    L.hg_colsum_jobs.restype = ctypes.c_int
+    L.hg_colsum_jobs.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                 ctypes.POINTER(ctypes.c_int), ctypes.c_int, vp]
     L.hg_mlp_act_backward_scratch.restype = ctypes.c_int64
     L.hg_mlp_act_backward_scratch.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.hg_linear_skinny_supported.restype = ctypes.c_int

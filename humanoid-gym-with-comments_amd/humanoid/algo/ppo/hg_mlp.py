@@ -11,6 +11,7 @@ pre-activation) is kept for the backward: elu'(h) = y + 1 for h <= 0.  Parameter
 nn.Sequential (state_dict keys unchanged).  Device float32 only.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -35,17 +36,46 @@ def fusable(net):
     return True
 
 
-def _act_backward(gy, y, rows, width, gb):
-    """gh = gy * elu'(from y) (y None: gh = gy) and gb = gh.sum(0), in one fused pass."""
+class _Reductions:
+    """The column sums of one MLP backward (bias-gradient tile partials, split-K weight-gradient
+    chunks), deferred and launched together as ONE hg_colsum_jobs kernel at the end of the
+    backward instead of one reduction launch per layer."""
+
+    def __init__(self):
+        self.jobs = []  # (src [parts, width], dst [width], width, parts)
+
+    def add(self, src, dst, width, parts):
+        self.jobs.append((src, dst, int(width), int(parts)))
+
+    def launch(self, dev):
+        n = len(self.jobs)
+        if n == 0:
+            return
+        vp = ctypes.c_void_p
+        src = (vp * n)(*[j[0].data_ptr() for j in self.jobs])
+        dst = (vp * n)(*[j[1].data_ptr() for j in self.jobs])
+        width = (ctypes.c_int64 * n)(*[j[2] for j in self.jobs])
+        parts = (ctypes.c_int * n)(*[j[3] for j in self.jobs])
+        rc = N.lib().hg_colsum_jobs(src, dst, width, parts, n, _stream(dev))
+        if rc != 0:
+            raise RuntimeError(f"hg_colsum_jobs failed ({rc})")
+        self.jobs = []
+
+
+def _act_backward(gy, y, rows, width, gb, red=None):
+    """gh = gy * elu'(from y) (y None: gh = gy) and gb = gh.sum(0), in one fused pass (the final
+    column sum of gb deferred to ``red`` when given)."""
     L = N.lib()
     scratch = torch.empty(int(L.hg_mlp_act_backward_scratch(rows, width)), dtype=torch.float32, device=gy.device)
     gh = torch.empty_like(gy) if y is not None else gy
     s = ctypes.c_void_p(torch.cuda.current_stream(gy.device).cuda_stream)
     rc = L.hg_mlp_act_backward(gy.data_ptr(), y.data_ptr() if y is not None else None,
-                               gh.data_ptr() if y is not None else None, rows, width, gb.data_ptr(),
-                               scratch.data_ptr(), s)
+                               gh.data_ptr() if y is not None else None, rows, width,
+                               gb.data_ptr() if red is None else None, scratch.data_ptr(), s)
     if rc != 0:
         raise RuntimeError(f"hg_mlp_act_backward failed ({rc})")
+    if red is not None:
+        red.add(scratch, gb, width, scratch.numel() // width)
     return gh
 
 
@@ -71,17 +101,19 @@ def _skinny_forward(h, W, b, out=None):
     return y
 
 
-def _skinny_backward(g, h, W, need_dx):
+def _skinny_backward(g, h, W, need_dx, red=None):
     rows, (n, k) = g.shape[0], W.shape
     L = N.lib()
     wb = torch.empty(n * k + n, dtype=torch.float32, device=g.device)
     dx = torch.empty(rows, k, dtype=torch.float32, device=g.device) if need_dx else None
     scratch = torch.empty(int(L.hg_linear_skinny_backward_scratch(rows, n, k)), dtype=torch.float32, device=g.device)
     rc = L.hg_linear_skinny_backward(g.data_ptr(), h.data_ptr(), h.stride(0), W.data_ptr(),
-                                     dx.data_ptr() if need_dx else None, wb.data_ptr(), rows, n, k,
-                                     scratch.data_ptr(), _stream(g.device))
+                                     dx.data_ptr() if need_dx else None, wb.data_ptr() if red is None else None,
+                                     rows, n, k, scratch.data_ptr(), _stream(g.device))
     if rc != 0:
         raise RuntimeError(f"hg_linear_skinny_backward failed ({rc})")
+    if red is not None:
+        red.add(scratch, wb, n * k + n, scratch.numel() // (n * k + n))
     return wb[: n * k].view(n, k), wb[n * k:], dx
 
 
@@ -95,13 +127,22 @@ _DW_SPLIT = {(128, 256): 8, (128, 128): 4, (256, 512): 4, (128, 705): 8, (512, 7
              (256, 768): 4}
 
 
-def _weight_grad(gh, x):
+def _weight_grad(gh, x, red=None):
     rows, n = gh.shape
     k = x.shape[1]
     S = _DW_SPLIT.get((n, k), 1) if rows >= 8192 else 1
     if S == 1 or rows % S or not (gh.is_contiguous() and x.is_contiguous()):
         return torch.mm(gh.t(), x)
-    return torch.bmm(gh.view(S, rows // S, n).transpose(1, 2), x.view(S, rows // S, k)).sum(0)
+    chunks = torch.bmm(gh.view(S, rows // S, n).transpose(1, 2), x.view(S, rows // S, k))
+    if red is None:
+        return chunks.sum(0)
+    dw = torch.empty(n, k, dtype=torch.float32, device=gh.device)
+    red.add(chunks, dw, n * k, S)  # chunk sum p = 0 .. S-1, in the batched end-of-backward launch
+    return dw
+
+
+# the per-layer column sums of the backward run as one batched launch at its end (hg_colsum_jobs)
+DEFER_REDUCTIONS = os.environ.get("HG_DEFER_REDUCTIONS", "1") != "0"
 
 
 class _MLP(torch.autograd.Function):
@@ -132,24 +173,27 @@ class _MLP(torch.autograd.Function):
         grads = [None] * (2 * n)
         g = g.contiguous()
         gx = None
+        red = _Reductions() if DEFER_REDUCTIONS else None
         for i in range(n - 1, -1, -1):
             need_dx = i > 0 or ctx.needs_input_grad[0]
             if i == n - 1 and _skinny_ok(ins[i], Ws[i]):
                 # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
-                grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx)
+                grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx, red)
             else:
                 rows, width = g.shape
                 gb = torch.empty(width, dtype=torch.float32, device=g.device)
                 # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
-                gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb)
+                gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb, red)
                 grads[2 * i + 1] = gb
-                grads[2 * i] = _weight_grad(gh, ins[i])
+                grads[2 * i] = _weight_grad(gh, ins[i], red)
                 gnext = torch.mm(gh, Ws[i]) if need_dx else None
             if i > 0:
                 # the next (lower) layer's incoming gradient goes through its ELU backward
                 g = gnext
             else:
                 gx = gnext
+        if red is not None:
+            red.launch(g.device)
         return (gx, *grads)
 
 

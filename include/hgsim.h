@@ -319,15 +319,17 @@ int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int num_actions, 
  * Linear(+ELU) layer of actor_critic.py:36-149, torch's ELU backward and grad_bias = gh.sum(0))
  * gh = gy * elu'(h) with elu'(h) = 1 for y > 0, y + 1 otherwise (y = the layer's ELU output);
  * y == NULL: identity activation, gh is gy (gh not written).  grad_bias[width] = column sums of
- * gh, deterministic (per-128-row tile partials in scratch, fixed-order column sums).
- * [rows, width] contiguous row-major float32; two launches. */
+ * gh, deterministic (per-32-row tile partials in scratch, fixed-order column sums).
+ * [rows, width] contiguous row-major float32; two launches.  grad_bias == NULL: one launch, the
+ * [ceil(rows/32), width] partials are left in scratch for hg_colsum_jobs. */
 int hg_mlp_act_backward(const float* gy, const float* y, float* gh, int64_t rows, int width, float* grad_bias,
                         float* scratch /* >= hg_mlp_act_backward_scratch() floats */, void* stream);
 int64_t hg_mlp_act_backward_scratch(int64_t rows, int width);
 /* Skinny output layers (n in {1,2,3,4,6,8,12,16}, k == 128): the last Linear of
  * each policy MLP (12 actions, 3 lin-vel, 1 value).  forward: y[rows, n] = x W^T + b, x rows of
  * stride ldx (16-byte aligned); backward: grad_wb = [dW (n x k row-major), db (n)] as
- * deterministic column sums over 64-row tiles, dx[rows, k] = gh W (dx may be NULL). */
+ * deterministic column sums over 64-row tiles, dx[rows, k] = gh W (dx may be NULL).  grad_wb ==
+ * NULL: the [ceil(rows/64), n*k + n] partials are left in scratch for hg_colsum_jobs. */
 int hg_linear_skinny_supported(int n, int k);
 int hg_linear_skinny_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y, int64_t rows,
                              int n, int k, void* stream);
@@ -335,6 +337,12 @@ int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, cons
                               float* grad_wb, int64_t rows, int n, int k,
                               float* scratch /* >= hg_linear_skinny_backward_scratch() floats */, void* stream);
 int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k);
+/* Batched column sums (the deferred reductions of one MLP backward in one launch: bias-gradient
+ * tile partials and split-K weight-gradient chunks, replacing per-layer grad.sum(0) launches):
+ * dst[j][c] = sum over p < parts[j] of src[j][p * width[j] + c], fixed order, for j < njobs <= 16.
+ * parts > 16 uses hg_mlp_act_backward's own final reduction (identical bits). */
+int hg_colsum_jobs(const float* const* src, float* const* dst, const int64_t* width, const int* parts, int njobs,
+                   void* stream);
 
 /* library build info */
 const char* hg_version(void);

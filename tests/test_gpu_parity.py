@@ -933,3 +933,47 @@ def test_gather_rows_matches_torch_indexing(dtype):
         assert torch.equal(d0, obs[idx]) and torch.equal(d1, crit[idx]) and torch.equal(d2, pk[idx])
     with pytest.raises(RuntimeError):
         gather_rows(idx, [(obs, torch.empty(rows, 705, dtype=torch.float64, device="cuda:0"))])
+
+
+def test_deferred_mlp_reductions_match():
+    """The batched end-of-backward column sums (hg_colsum_jobs) at the 24576-row minibatch, where
+    the weight gradients run split-K: bias gradients bitwise those of the per-layer reductions,
+    weight gradients equal to the per-layer chunk sums up to summation order, and both within
+    tolerance of torch's nn.Sequential backward."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic
+    from humanoid.algo.ppo import hg_mlp
+    torch.manual_seed(4)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     base_lin_vel_hidden_dims=[128, 128]).cuda()
+    B = 24576
+    obs = torch.randn(B, 705, device="cuda:0")
+    critic = torch.randn(B, 219, device="cuda:0")
+    w_mu, w_v, w_lv = (torch.randn(B, 12, device="cuda:0"), torch.randn(B, 1, device="cuda:0"),
+                       torch.randn(B, 3, device="cuda:0"))
+
+    def run(fused, defer):
+        ac.fused_mlp = fused
+        hg_mlp.DEFER_REDUCTIONS = defer
+        for p in ac.parameters():
+            p.grad = None
+        mu = ac._mlp(ac.actor, obs)
+        v = ac._mlp(ac.critic, critic)
+        lv = ac._mlp(ac.base_lin_vel, obs)
+        ((mu * w_mu).sum() + (v * w_v).sum() + (lv * w_lv).sum()).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.clone() for n, p in ac.named_parameters() if p.grad is not None}
+
+    try:
+        g_t = run(False, False)
+        g_i = run(True, False)
+        g_d = run(True, True)
+    finally:
+        hg_mlp.DEFER_REDUCTIONS = True
+    assert g_d.keys() == g_i.keys() == g_t.keys()
+    for n in g_d:
+        if n.endswith("bias"):
+            assert torch.equal(g_d[n], g_i[n]), n
+        else:
+            torch.testing.assert_close(g_d[n], g_i[n], rtol=1e-5, atol=1e-5, msg=lambda m: f"{n}: {m}")
+        torch.testing.assert_close(g_d[n], g_t[n], rtol=2e-4, atol=2e-4, msg=lambda m: f"{n}: {m}")
