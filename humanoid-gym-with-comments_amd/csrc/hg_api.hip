@@ -15,7 +15,7 @@ extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t 
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
                               float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
                               float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
-                              hipStream_t stream);
+                              int ep_slot, hipStream_t stream);
 
 namespace {
 
@@ -78,7 +78,9 @@ Layout make_layout(const hg_cfg* c) {
   for (int id = 0; id < HG_T_COUNT; id++) {
     L.off[id] = o;
     if (id == HG_T_OBS_BUF || id == HG_T_PRIV_BUF) continue;  // below
-    if (id == HG_T_EP_STATS) { o += align256(48 * sizeof(float)); continue; }
+    // EP_STATS region: [24] stats, [24] accumulators, then the [HG_EP_RING, 24] snapshot ring
+    if (id == HG_T_EP_STATS) { o += align256((48 + HG_EP_RING * 24) * sizeof(float)); continue; }
+    if (id == HG_T_EP_STATS_RING) { L.off[id] = L.off[HG_T_EP_STATS] + 48 * sizeof(float); continue; }
     o += align256((size_t)soa_rows(id) * np * esize(dtype_of(id)));
   }
   const size_t ob = (size_t)n * c->frame_stack * HG_OBS1 * 4, pb = (size_t)n * c->c_frame_stack * HG_PRIV1 * 4;
@@ -104,6 +106,8 @@ struct Sim {
   Layout L;
   HgState S;
   int parity;  // which obs/priv buffer holds the latest stack
+  uint64_t post_seq = 0;  // post/reset launches so far: EP_STATS ring row of the next one
+  int ep_slot = 0;        // ring row written by the latest one
   int physics_version;  // 2 (lane-parallel, default) or 1 (lane-per-env reference kernel)
   std::string err;
 };
@@ -265,6 +269,9 @@ int hg_tensor(void* sim, int id, hg_desc* d) {
     case HG_T_EP_STATS:
       d->ndim = 1; d->shape[0] = 24; d->strides[0] = 1;
       return HG_OK;
+    case HG_T_EP_STATS_RING:
+      d->ndim = 2; d->shape[0] = HG_EP_RING; d->shape[1] = 24; d->strides[0] = 24; d->strides[1] = 1;
+      return HG_OK;
     case HG_T_CONTACT_FORCES:  // AoS [N,13,3], contiguous like the reference's net_contact_force view
       d->ndim = 3; d->shape[0] = n; d->shape[1] = HG_NB; d->shape[2] = 3;
       d->strides[0] = HG_NB * 3; d->strides[1] = 3; d->strides[2] = 1;
@@ -301,12 +308,20 @@ static int do_post(Sim* s, uint64_t counter, int mode, const uint8_t* mask, void
   float* pb0 = (float*)(s->arena + s->L.priv_buf[p]);
   float* pb1 = (float*)(s->arena + s->L.priv_buf[1 - p]);
   const float inv_len_s = 1.0f / ((float)s->cfg.max_episode_length * s->cfg.dt);
+  const int slot = (int)(s->post_seq % HG_EP_RING);
   int rc = hg_launch_post(&s->S, &s->cfg, counter, mode, mask, (float*)(s->arena + s->L.frame_obs),
                           (float*)(s->arena + s->L.frame_priv), ob0, ob1, pb0, pb1, s->cfg.frame_stack,
-                          s->cfg.c_frame_stack, inv_len_s, (hipStream_t)stream);
+                          s->cfg.c_frame_stack, inv_len_s, slot, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_post launch failed");
+  s->ep_slot = slot;
+  s->post_seq++;
   s->parity = 1 - p;
   return HG_OK;
+}
+
+int hg_ep_stats_slot(void* sim) {
+  Sim* s = (Sim*)sim;
+  return s ? s->ep_slot : -1;
 }
 
 int hg_post(void* sim, uint64_t common_step_counter, void* stream) {

@@ -818,15 +818,20 @@ struct StackT {
   int width, frames;
 };
 __global__ void __launch_bounds__(256) k_stack_stats(StackT A, StackT B, const uint8_t* __restrict__ reset, int n,
-                                                     float* ep_stats, float inv_len_s) {
+                                                     float* ep_stats, float inv_len_s, int ring_slot) {
   if (blockIdx.x == gridDim.x - 1) {
     const int k = threadIdx.x;
     float* acc = ep_stats + 24;
     const float cnt = acc[22];
     __syncthreads();
-    if (k < HG_NUM_REWARDS && cnt > 0.f) ep_stats[k] = acc[k] / cnt * inv_len_s;
-    if (k == 22) ep_stats[22] = cnt;
-    if (k == 23) ep_stats[23] = cnt > 0.f ? 1.f : 0.f;
+    float v = k < 24 ? ep_stats[k] : 0.f;
+    if (k < HG_NUM_REWARDS && cnt > 0.f) v = acc[k] / cnt * inv_len_s;
+    if (k == 22) v = cnt;
+    if (k == 23) v = cnt > 0.f ? 1.f : 0.f;
+    if (k < 24) {
+      ep_stats[k] = v;
+      ep_stats[48 + ring_slot * 24 + k] = v;  // this launch's snapshot (HG_T_EP_STATS_RING)
+    }
     __syncthreads();
     if (k < 24) acc[k] = 0.f;
     return;
@@ -851,7 +856,7 @@ __global__ void __launch_bounds__(256) k_stack_stats(StackT A, StackT B, const u
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
                               float* frame_obs, float* frame_priv, const float* obs_src, float* obs_dst,
                               const float* priv_src, float* priv_dst, int frame_stack, int c_frame_stack,
-                              float inv_len_s, hipStream_t stream) {
+                              float inv_len_s, int ep_slot, hipStream_t stream) {
   const int n = S->n;
   if (mode == 0)
     hipLaunchKernelGGL(k_post_step, dim3((n + 63) / 64), dim3(64), 0, stream, *S, *hcfg, counter, frame_obs,
@@ -863,6 +868,7 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
   const int g = (int)std::min<int64_t>((tot + 255) / 256, 4096) + 1;  // + the statistics block
   const StackT A = {obs_src, obs_dst, frame_obs, HG_OBS1, frame_stack};
   const StackT B = {priv_src, priv_dst, frame_priv, HG_PRIV1, c_frame_stack};
-  hipLaunchKernelGGL(k_stack_stats, dim3(g), dim3(256), 0, stream, A, B, S->reset_buf, n, S->ep_stats, inv_len_s);
+  hipLaunchKernelGGL(k_stack_stats, dim3(g), dim3(256), 0, stream, A, B, S->reset_buf, n, S->ep_stats, inv_len_s,
+                     ep_slot);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

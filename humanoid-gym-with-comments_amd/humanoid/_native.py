@@ -81,12 +81,14 @@ TENSOR_IDS = [
     "FEET_AIR_TIME", "LAST_CONTACTS", "FEET_HEIGHT", "LAST_FEET_Z", "ENV_FRICTION", "BODY_MASS",
     "PUSH_FORCE", "PUSH_TORQUE", "BASE_LIN_VEL", "BASE_ANG_VEL", "PROJ_GRAVITY", "BASE_EULER",
     "REF_DOF_POS", "ENV_ORIGINS", "EP_STATS", "CONTACT_LAMBDA", "NONFINITE", "TERRAIN_LEVEL", "TERRAIN_TYPE",
+    "EP_STATS_RING",
 ]
+EP_RING = 64  # HG_EP_RING
 T = {name: i for i, name in enumerate(TENSOR_IDS)}
 
 # every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
-           "hg_post", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
+           "hg_post", "hg_ep_stats_slot", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
            "hg_rollout_act", "hg_rollout_env", "hg_gather_rows", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
@@ -146,6 +148,8 @@ def load_library(path=LIB_PATH):
     L.hg_rollout_act.restype = ctypes.c_int
     L.hg_rollout_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                  vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+    L.hg_ep_stats_slot.restype = ctypes.c_int
+    L.hg_ep_stats_slot.argtypes = [vp]
     L.hg_gather_rows.restype = ctypes.c_int
     L.hg_gather_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int64] + [vp, vp, ctypes.c_int64, ctypes.c_int] * 3 + [vp]
     L.hg_rollout_env.restype = ctypes.c_int

@@ -286,6 +286,7 @@ class XBotLFreeEnv(BaseTask):
         self.ref_dof_pos = self._view(T["REF_DOF_POS"])
         self.env_origins = self._view(T["ENV_ORIGINS"])
         self._ep_stats = self._view(T["EP_STATS"])
+        self._ep_ring = self._view(T["EP_STATS_RING"])
         self.nonfinite_count = self._view(T["NONFINITE"])
 
     def _get_env_origins(self):
@@ -415,7 +416,9 @@ class XBotLFreeEnv(BaseTask):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _publish_extras(self):
-        stats = self._ep_stats.clone()
+        # the latest post/reset launch left its EP_STATS snapshot in ring row hg_ep_stats_slot: a
+        # view, intact for the next EP_RING - 1 launches (no copy kernel per step)
+        stats = self._ep_ring[self.hg.hg_ep_stats_slot(self.sim)]
         self.extras = {
             "episode": {"rew_" + n: stats[REWARD_NAMES.index(n)] for n in self.reward_names},
             "time_outs": self.time_out_buf,

@@ -123,6 +123,7 @@ typedef struct hg_desc {
   int64_t strides[4];   /* in elements */
 } hg_desc;
 
+#define HG_EP_RING 64
 /* tensor ids for hg_tensor() */
 enum hg_tensor_id {
   HG_T_ROOT_STATE = 0,   /* [N,13] pos3 quat(xyzw)4 linvel3 angvel3, world   (actor_root_state) */
@@ -150,6 +151,9 @@ enum hg_tensor_id {
   HG_T_NONFINITE,        /* [N] int32 count of non-finite recoveries */
   HG_T_TERRAIN_LEVEL,    /* [N] int32 curriculum level (row of terrain_origins) */
   HG_T_TERRAIN_TYPE,     /* [N] int32 terrain type (column of terrain_origins) */
+  HG_T_EP_STATS_RING,    /* [HG_EP_RING, 24] EP_STATS as left by each post/reset launch, launch k in row
+                            k % HG_EP_RING (hg_ep_stats_slot): the per-step extras["episode"] snapshot
+                            without a copy launch */
   HG_T_COUNT
 };
 
@@ -173,6 +177,9 @@ int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream
 /* replaces post_physics_step minus the refreshes (humanoid_env.py:780-806) and the obs clip
  * (:654-657): derived state, commands, push, termination, rewards, masked reset, observations.
  * common_step_counter is the reference's host-side counter (:781). */
+/* ring row of HG_T_EP_STATS_RING written by the latest hg_post / hg_reset_masked launch (host-side
+ * bookkeeping, no device access) */
+int hg_ep_stats_slot(void* sim);
 int hg_post(void* sim, uint64_t common_step_counter, void* stream);
 /* Runtime parameter update (curricula, e.g. the push-recovery ramp of config 5): copies *cfg into
  * the handle and, stream-ordered, into the device copy the kernels read.  Fields that size or

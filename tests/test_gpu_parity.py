@@ -977,3 +977,25 @@ def test_deferred_mlp_reductions_match():
         else:
             torch.testing.assert_close(g_d[n], g_i[n], rtol=1e-5, atol=1e-5, msg=lambda m: f"{n}: {m}")
         torch.testing.assert_close(g_d[n], g_t[n], rtol=2e-4, atol=2e-4, msg=lambda m: f"{n}: {m}")
+
+
+def test_episode_extras_ring_snapshots():
+    """extras["episode"] (reset_idx's episode reward means, humanoid_env.py:1109-1163) is a view of
+    the EP_STATS snapshot ring: each step's dict holds the EP_STATS values as they were after that
+    step, and stays intact while later steps run (up to the ring length)."""
+    _need_gpu()
+    env = _make_env(N_ENVS)
+    snaps, dicts = [], []
+    for t in range(40):
+        if t % 7 == 3:  # force resets so the statistics change
+            env.reset_buf[: N_ENVS // 4] = True
+            env.reset_idx(torch.arange(N_ENVS // 4, device="cuda:0"))
+        env.step(torch.randn(N_ENVS, 12, device="cuda:0") * 0.3)
+        torch.cuda.synchronize()
+        snaps.append(env._ep_stats.clone())
+        dicts.append(env.extras["episode"])
+    from humanoid.envs.custom.humanoid_env import REWARD_NAMES
+    for t, (snap, d) in enumerate(zip(snaps, dicts)):
+        for name, v in d.items():
+            assert torch.equal(v, snap[REWARD_NAMES.index(name[4:])]), (t, name)
+    assert any(not torch.equal(snaps[0], s) for s in snaps[1:])
