@@ -118,12 +118,13 @@ def _skinny_backward(g, h, W, need_dx, red=None):
 
 
 # Split-K factors for the weight gradients dW[n, k] = gh[R, n]^T x[R, k] at the 24576-row
-# minibatch: the reduction over R is cut into S row chunks computed as one batched GEMM and summed
-# in a fixed order.  Small outputs (128 x 256, 256 x 512, ...) expose too few output tiles to fill
-# 256 CUs, so BLAS runs them at 30-90 TFLOP/s; measured on MI355X with TunableOp-tuned kernels for
-# every variant (scripts/dw_probe.py): 128x256 51 -> 25 us (S=8), 256x512 80 -> 58 us (S=4),
-# 768x219 105 -> 92 us (S=4), 256x768 106 -> 86 us (S=4).
-_DW_SPLIT = {(128, 256): 8, (128, 128): 4, (256, 512): 4, (128, 705): 8, (512, 705): 2, (768, 219): 4,
+# minibatch: the reduction over R is cut into S row chunks computed as one batched GEMM; the chunk
+# sum runs in the batched end-of-backward column-sum launch.  Small outputs (128 x 256, 256 x 512,
+# ...) expose too few output tiles to fill 256 CUs, so BLAS runs them at 25-80 TFLOP/s; measured on
+# MI355X, bmm only, TunableOp-tuned kernels for every variant (scripts/dw_probe.py): 128x128
+# 31 -> 17 us (S=16), 128x256 52 -> 20 us (S=32), 256x512 79 -> 55 us (S=4), 768x219 105 -> 78 us
+# (S=32), 256x768 106 -> 86 us (S=4).
+_DW_SPLIT = {(128, 256): 32, (128, 128): 16, (256, 512): 4, (128, 705): 8, (512, 705): 2, (768, 219): 32,
              (256, 768): 4}
 
 

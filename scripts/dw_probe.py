@@ -26,17 +26,20 @@ def t_us(f, n=50):
     return a.elapsed_time(b) * 1e3 / n
 
 
-for n, k in ((128, 256), (128, 128), (256, 512), (128, 705), (512, 705), (768, 219), (256, 768)):
+SHAPES = [tuple(int(v) for v in s.split('x')) for s in os.environ.get('DW_SHAPES', '').split(',') if s] or \
+    [(128, 256), (128, 128), (256, 512), (128, 705), (512, 705), (768, 219), (256, 768)]
+SPLITS = [int(v) for v in os.environ.get('DW_SPLITS', '2,4,8').split(',')]
+for n, k in SHAPES:
     gh = torch.randn(R, n, device=dev)
     x = torch.randn(R, k, device=dev)
     base = t_us(lambda: torch.mm(gh.t(), x))
     ref = torch.mm(gh.t(), x)
     line = f"dW {n}x{k}: mm {base:7.1f} us ({2 * R * n * k / base / 1e6:6.1f} TF/s)"
-    for S in (2, 4, 8):
+    for S in SPLITS:
         ghs = gh.view(S, R // S, n).transpose(1, 2)
         xs = x.view(S, R // S, k)
         f = lambda: torch.bmm(ghs, xs).sum(0)  # noqa: E731
-        t = t_us(f)
+        t = t_us(lambda: torch.bmm(ghs, xs))  # the chunk sum runs in the batched end-of-backward launch
         err = (f() - ref).abs().max().item() / ref.abs().max().item()
         line += f" | S={S} {t:7.1f} us (rel err {err:.1e})"
     print(line, flush=True)
