@@ -807,8 +807,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 }
 
 // history stacking: dst[e] = [src[e][W:], frame[e]] (src zeroed for reset envs), for the
-// observation and the privileged tables in one launch; one thread per output element so both the
-// reads and the writes are contiguous.  The last block also folds the episode statistics
+// observation and the privileged tables in one launch; one block per (env, table) row, threads
+// along the row so both the reads and the writes are contiguous.  The last block also folds the episode statistics
 // (ep_stats[k] = acc[k] / n_reset / episode_length_s when any env reset) and clears the
 // accumulators.
 struct StackT {
@@ -836,21 +836,19 @@ __global__ void __launch_bounds__(256) k_stack_stats(StackT A, StackT B, const u
     if (k < 24) acc[k] = 0.f;
     return;
   }
-  const int rowA = A.frames * A.width, rowB = B.frames * B.width;
-  const int64_t totA = (int64_t)n * rowA, total = totA + (int64_t)n * rowB;
-  const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const bool a = i < totA;
-    const StackT& T = a ? A : B;
-    const int row = a ? rowA : rowB;
-    const int64_t j = a ? i : i - totA;
-    const int e = (int)(j / row);
-    const int k = (int)(j - (int64_t)e * row);
-    float v;
-    if (k >= row - T.width) v = T.frame[(size_t)e * T.width + (k - (row - T.width))];
-    else v = reset[e] ? 0.f : T.src[(size_t)e * row + k + T.width];
-    T.dst[j] = v;
-  }
+  // one block per (env, table) row: no per-element index division (the former flat one-thread-
+  // per-element form spent its time in 64-bit divides), contiguous reads and writes along the row
+  const int b = blockIdx.x;
+  const bool a = b < n;
+  const StackT& T = a ? A : B;
+  const int e = a ? b : b - n;
+  const int row = T.frames * T.width;
+  const int cut = row - T.width;
+  const bool rs = reset[e] != 0;
+  const float* __restrict__ src = T.src + (size_t)e * row + T.width;
+  const float* __restrict__ fr = T.frame + (size_t)e * T.width - cut;
+  float* __restrict__ dst = T.dst + (size_t)e * row;
+  for (int k = threadIdx.x; k < row; k += blockDim.x) dst[k] = k >= cut ? fr[k] : (rs ? 0.f : src[k]);
 }
 
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
@@ -864,8 +862,7 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
   else
     hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
                        frame_priv);
-  const int64_t tot = (int64_t)n * (frame_stack * HG_OBS1 + c_frame_stack * HG_PRIV1);
-  const int g = (int)std::min<int64_t>((tot + 255) / 256, 4096) + 1;  // + the statistics block
+  const int g = 2 * n + 1;  // one block per (env, table) row + the statistics block
   const StackT A = {obs_src, obs_dst, frame_obs, HG_OBS1, frame_stack};
   const StackT B = {priv_src, priv_dst, frame_priv, HG_PRIV1, c_frame_stack};
   hipLaunchKernelGGL(k_stack_stats, dim3(g), dim3(256), 0, stream, A, B, S->reset_buf, n, S->ep_stats, inv_len_s,
