@@ -92,6 +92,11 @@ class OnPolicyRunner:
         cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
         cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
         tot_iter = self.current_learning_iteration + num_learning_iterations
+        # without a log writer nothing in the loop needs the iteration's numbers on the host: its
+        # phase events and loss means are read one iteration later (after the next iteration's
+        # work is queued) and at the end, so the GPU never idles at the iteration boundary
+        lazy = self.log_dir is None
+        pending = None
         for it in range(self.current_learning_iteration, tot_iter):
             if hasattr(self.env, "update_push_curriculum"):
                 self.env.update_push_curriculum(it)
@@ -128,6 +133,14 @@ class OnPolicyRunner:
                 course_gain = self.env.course_gain
                 start = stop
                 self.alg.compute_returns(critic_obs)
+            if on_gpu and lazy:
+                losses = self.alg.update(sync=False)
+                ev[2].record()
+                if pending is not None:
+                    self._resolve_stats(*pending)
+                pending = (ev, losses)
+                ep_infos.clear()
+                continue
             mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss = self.alg.update()
             stop = time.time()
             learn_time = stop - start
@@ -144,9 +157,20 @@ class OnPolicyRunner:
                 if it % self.save_interval == 0:
                     self.save(os.path.join(self.log_dir, "model_{}.pt".format(it)))
             ep_infos.clear()
+        if pending is not None:
+            self._resolve_stats(*pending)
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, "model_{}.pt".format(self.current_learning_iteration)))
+
+    def _resolve_stats(self, ev, losses):
+        """last_iteration_stats from an iteration's phase events and device loss means (waits for
+        that iteration's end only)."""
+        ev[2].synchronize()
+        v, s, _, lv = [float(x) for x in losses]
+        self.last_iteration_stats = dict(collection_time=ev[0].elapsed_time(ev[1]) * 1e-3,
+                                         learn_time=ev[1].elapsed_time(ev[2]) * 1e-3,
+                                         value_loss=v, surrogate_loss=s, lin_vel_loss=lv)
 
     def log(self, locs, width=90, pad=45):
         self.tot_timesteps += self.num_steps_per_env * self.env.num_envs

@@ -389,10 +389,13 @@ class PPO:
             nn.utils.clip_grad_norm_(self._params, self.max_grad_norm)
             self.optimizer.step()
 
-    def update(self):
+    def update(self, sync=True):
+        """ppo.py:140-226.  Returns the mean value / surrogate / sym / lin-vel losses as floats; with
+        sync=False (device path) the means stay on the device (0-d tensors; no host wait)."""
         if self._on_device and self.use_graphs:
-            return self._update_graphed()
-        return self._update_eager()
+            return self._update_graphed(sync)
+        out = self._update_eager()
+        return out
 
     def _update_eager(self):
         mean_value_loss = 0.0
@@ -521,7 +524,7 @@ class PPO:
             self._clip_and_step()
         self._graphs = (ga, gb, mb, self._storage_key())
 
-    def _update_graphed(self):
+    def _update_graphed(self, sync=True):
         st = self.storage
         nmb = self.num_mini_batches
         batch = st.num_envs * st.num_transitions_per_env
@@ -550,6 +553,9 @@ class PPO:
                     dist.all_reduce(self._flat_grad)  # gradients + the KL slot
                 gb.replay()
         num_updates = self.num_learning_epochs * nmb
-        v, s, lv = (self._sums / num_updates).tolist()  # the one host read of the update
+        means = self._sums / num_updates
         st.clear()
+        if not sync:
+            return means[0], means[1], 0, means[2]
+        v, s, lv = means.tolist()  # the one host read of the update
         return v, s, 0, lv

@@ -999,3 +999,25 @@ def test_episode_extras_ring_snapshots():
         for name, v in d.items():
             assert torch.equal(v, snap[REWARD_NAMES.index(name[4:])]), (t, name)
     assert any(not torch.equal(snaps[0], s) for s in snaps[1:])
+
+
+def test_runner_lazy_stats_are_last_iteration():
+    """OnPolicyRunner.learn without a log writer reads each iteration's phase events and loss means
+    one iteration late (no host wait at the iteration boundary); after learn() the stats are
+    those of the last iteration: its loss means exactly as the update accumulated them."""
+    _need_gpu()
+    from humanoid.envs import XBotLCfgPPO  # noqa: F401  (registers humanoid_ppo)
+    from humanoid.utils import get_args, task_registry
+    args = get_args(["--num_envs", "64", "--headless", "--run_name", "t"])
+    env, _ = task_registry.make_env("humanoid_ppo", args=args)
+    _, tcfg = task_registry.get_cfgs("humanoid_ppo")
+    tcfg.runner.num_steps_per_env = 8
+    runner, _ = task_registry.make_alg_runner(env, args=args, train_cfg=tcfg, log_root=None)
+    assert runner.log_dir is None
+    runner.learn(4, init_at_random_ep_len=True)
+    st = runner.last_iteration_stats
+    assert st["collection_time"] > 0 and st["learn_time"] > 0
+    alg = runner.alg
+    v, s_, lv = (alg._sums / (alg.num_learning_epochs * alg.num_mini_batches)).tolist()
+    assert (st["value_loss"], st["surrogate_loss"], st["lin_vel_loss"]) == (v, s_, lv)
+    assert all(math.isfinite(x) for x in (v, s_, lv))
