@@ -488,41 +488,66 @@ class PPO:
         tables = [(obs, self._mb_obs), (self._packed, self._mb_packed)]
         if critic is not obs:
             tables.insert(1, (critic, self._mb_critic))
+        self._mb_tables, self._mb_widths = tables, widths
+        # world size 1: the whole update (epochs x minibatches, each with its LR rule and Adam step)
+        # is ONE graph reading its row indices from a static permutation buffer; with ranks to
+        # all-reduce between the backward and the step, two graphs per minibatch
+        self._whole = self.world_size == 1 and self._flat_grad is None
+        if self._whole:
+            nmb = self.num_mini_batches
+            self._perm = torch.zeros(nmb * mb, dtype=torch.int64, device=dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.num_learning_epochs):
+                    for i in range(nmb):
+                        self.optimizer.zero_grad(set_to_none=True)  # fresh gradients from each backward
+                        self._mb_backward(self._perm[i * mb:(i + 1) * mb])
+                        self._mb_step()
+            self._graphs = (g, None, mb, self._storage_key())
+            return
         with torch.cuda.graph(ga):
-            if self._flat_grad is not None:
-                self._flat_grad.zero_()
-            gather_rows(self._idx, tables)
-            crit_b = self._mb_critic
-            b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
-            pk = self._mb_packed
-            for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma"),
-                                  pk.split(widths, dim=1)):
-                b[name] = part
-            if self._fused_loss:
-                loss = self._losses_fused(b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"],
-                                          b["adv"], b["returns"], b["logp"], b["mu"], b["sigma"],
-                                          stats_out=self._stats4)
-            else:
-                loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
-                    b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"],
-                    b["logp"])
-                if self._adaptive:
-                    ac = self.actor_critic
-                    self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
-                self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
-            if self.world_size > 1 and self._adaptive:
-                self._kl_slot.copy_(self._kl)
-            loss.backward()
+            self._mb_backward(self._idx)
         with torch.cuda.graph(gb, pool=ga.pool()):
-            kl = self._kl
-            if self.world_size > 1:
-                # gradients and the KL mean were summed over ranks in ONE all-reduce
-                self._flat_grad.div_(self.world_size)
-                kl = self._kl_slot
-            if self._adaptive:
-                self._lr_rule_device(kl)
-            self._clip_and_step()
+            self._mb_step()
         self._graphs = (ga, gb, mb, self._storage_key())
+
+    def _mb_backward(self, idx):
+        """Captured minibatch body: gather rows -> losses -> backward (+ KL mean, loss sums)."""
+        if self._flat_grad is not None:
+            self._flat_grad.zero_()
+        gather_rows(idx, self._mb_tables)
+        crit_b = self._mb_critic
+        b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
+        pk = self._mb_packed
+        for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma"),
+                              pk.split(self._mb_widths, dim=1)):
+            b[name] = part
+        if self._fused_loss:
+            loss = self._losses_fused(b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"],
+                                      b["adv"], b["returns"], b["logp"], b["mu"], b["sigma"],
+                                      stats_out=self._stats4)
+        else:
+            loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
+                b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"],
+                b["logp"])
+            if self._adaptive:
+                ac = self.actor_critic
+                self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
+            self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
+        if self.world_size > 1 and self._adaptive:
+            self._kl_slot.copy_(self._kl)
+        loss.backward()
+
+    def _mb_step(self):
+        """Captured minibatch step: adaptive learning rate, global-norm clip, fused Adam."""
+        kl = self._kl
+        if self.world_size > 1:
+            # gradients and the KL mean were summed over ranks in ONE all-reduce
+            self._flat_grad.div_(self.world_size)
+            kl = self._kl_slot
+        if self._adaptive:
+            self._lr_rule_device(kl)
+        self._clip_and_step()
 
     def _update_graphed(self, sync=True):
         st = self.storage
@@ -542,16 +567,21 @@ class PPO:
         if self._graphs is None or self._graphs[2] != mb or self._graphs[3] != self._storage_key():
             self._capture(mb)
         ga, gb = self._graphs[0], self._graphs[1]
-        indices = torch.randperm(nmb * mb, requires_grad=False, device=st.observations.device)
+        dev = st.observations.device
         torch.cat([t.flatten(0, 1) for t in self._pack_src], dim=1, out=self._packed)
         self._sums.zero_()
-        for _ in range(self.num_learning_epochs):
-            for i in range(nmb):
-                self._idx.copy_(indices[i * mb:(i + 1) * mb])
-                ga.replay()
-                if self.world_size > 1:
-                    dist.all_reduce(self._flat_grad)  # gradients + the KL slot
-                gb.replay()
+        if gb is None:  # the whole update as one graph
+            torch.randperm(nmb * mb, out=self._perm, device=dev)
+            ga.replay()
+        else:
+            indices = torch.randperm(nmb * mb, requires_grad=False, device=dev)
+            for _ in range(self.num_learning_epochs):
+                for i in range(nmb):
+                    self._idx.copy_(indices[i * mb:(i + 1) * mb])
+                    ga.replay()
+                    if self.world_size > 1:
+                        dist.all_reduce(self._flat_grad)  # gradients + the KL slot
+                    gb.replay()
         num_updates = self.num_learning_epochs * nmb
         means = self._sums / num_updates
         st.clear()
