@@ -60,6 +60,10 @@ constexpr int RMAX = 32;
 #ifndef HG_LANE_OPAQUE
 #define HG_LANE_OPAQUE 1
 #endif
+// forward kinematics as a DPP prefix scan over each leg (1) or the serial 2-lane chains (0)
+#ifndef HG_KIN_SCAN
+#define HG_KIN_SCAN 1
+#endif
 #ifndef HG_CHOL_SB
 #define HG_CHOL_SB 0
 #endif
@@ -133,6 +137,7 @@ __device__ void ground(const hg_cfg* cfg, float x, float y, float* h, f3* n) {
   *n = mk(-dhdx * inv, -dhdy * inv, inv);
 }
 
+#if !HG_KIN_SCAN
 // ---- kinematics: local rotations (lanes 1..12) + base frame (lane 0); then leg chains (lanes 0,1)
 __device__ void kin_local(EnvSh& E, const hg_model* M, int l) {
   if (l >= 1 && l <= 12) {
@@ -188,6 +193,125 @@ __device__ void kin_chain(EnvSh& E, const hg_model* M, int leg, float gz, bool b
 #pragma unroll
     for (int i = 0; i < 9; i++) Rp[i] = Rb[i];
     op = ob; vp = vb; wp = wb;
+  }
+}
+
+#endif
+
+// ---- kinematics as a parallel scan over each leg (lanes 1..6 left leg, 7..12 right leg; every
+// lane of the env runs it, lanes 0 and 13..31 on clamped indices, so the DPP exchanges never
+// read a disabled lane).  A body's world transform is the base frame composed with the prefix
+// product of its leg's local transforms (Lr_j, jp_j), and every velocity/acceleration recursion
+// of kin_chain is a prefix sum of per-body terms:
+//   w_b   = w_0 + sum_j qd_j a_j                 v_b   = v_0 + sum_j w_p(j) x r_j
+//   alp_b =       sum_j w_p(j) x qd_j a_j        acc_b = acc_0 + sum_j alp_p(j) x r_j + w_p(j) x (w_p(j) x r_j)
+// Hillis-Steele steps 1, 2, 4 with DPP row_shr (the leg lies inside one 16-lane DPP row), so the
+// 6-link chains take 3 dependent steps per quantity instead of 6, with no LDS round trips.
+template <int N>
+__device__ __forceinline__ float shr(float x) {  // lane i <- lane i - N within the 16-lane row
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x110 | N, 0xF, 0xF, true));
+}
+// the DPP reads must run with every lane of the row active (a disabled source lane reads as 0):
+// each step computes unconditionally and keeps or drops the result with a select, never a branch
+// the compiler could sink the DPP into
+__device__ __forceinline__ float keep_dpp(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+template <int N>
+__device__ __forceinline__ void scan_step(f3& v, int k) {
+  const f3 u = mk(keep_dpp(shr<N>(v.x)), keep_dpp(shr<N>(v.y)), keep_dpp(shr<N>(v.z)));
+  const bool take = k >= N;
+  v = mk(take ? u.x + v.x : v.x, take ? u.y + v.y : v.y, take ? u.z + v.z : v.z);
+}
+__device__ __forceinline__ void scan3(f3& v, int k) {
+  scan_step<1>(v, k);
+  scan_step<2>(v, k);
+  scan_step<4>(v, k);
+}
+template <int N>
+__device__ __forceinline__ void tf_step(float* P, f3& t, int k) {
+  float Q[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) Q[i] = keep_dpp(shr<N>(P[i]));
+  const f3 u = mk(keep_dpp(shr<N>(t.x)), keep_dpp(shr<N>(t.y)), keep_dpp(shr<N>(t.z)));
+  // (Q, u) o (P, t) = (Q P, u + Q t), kept where the partner is in the same leg
+  float QP[9];
+  mm3(Q, P, QP);
+  const f3 tn = u + mv3(Q, t);
+  const bool take = k >= N;
+#pragma unroll
+  for (int i = 0; i < 9; i++) P[i] = take ? QP[i] : P[i];
+  t = mk(take ? tn.x : t.x, take ? tn.y : t.y, take ? tn.z : t.z);
+}
+__device__ __forceinline__ f3 shr1_or(f3 v, int k, f3 base) {  // parent's value (base for link 0)
+  const f3 u = mk(keep_dpp(shr<1>(v.x)), keep_dpp(shr<1>(v.y)), keep_dpp(shr<1>(v.z)));
+  return k == 0 ? base : u;
+}
+
+__device__ void kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool bias) {
+  const bool body = l >= 1 && l <= 12;
+  const int b = body ? l : 1;
+  const int k = (b - 1) % 6;  // link index within the leg
+  // base frame (every lane, from the root quaternion)
+  float R0[9];
+  {
+    const float x = E.root[3], y = E.root[4], z = E.root[5], w = E.root[6];
+    R0[0] = 1 - 2 * (y * y + z * z); R0[1] = 2 * (x * y - z * w);     R0[2] = 2 * (x * z + y * w);
+    R0[3] = 2 * (x * y + z * w);     R0[4] = 1 - 2 * (x * x + z * z); R0[5] = 2 * (y * z - x * w);
+    R0[6] = 2 * (x * z - y * w);     R0[7] = 2 * (y * z + x * w);     R0[8] = 1 - 2 * (x * x + y * y);
+  }
+  const f3 v0 = mk(E.nu[0], E.nu[1], E.nu[2]), w0 = mk(E.nu[3], E.nu[4], E.nu[5]);
+  // local transform of body b: Lr = jrot * rot(axis, q), origin jp (parent frame)
+  const f3 ax = ld3(M->axis[b]);
+  float P[9];
+  {
+    float Rq[9], s, c;
+    sincosf(E.q[b - 1], &s, &c);
+    const float vv = 1 - c;
+    Rq[0] = c + ax.x * ax.x * vv;        Rq[1] = ax.x * ax.y * vv - ax.z * s; Rq[2] = ax.x * ax.z * vv + ax.y * s;
+    Rq[3] = ax.y * ax.x * vv + ax.z * s; Rq[4] = c + ax.y * ax.y * vv;        Rq[5] = ax.y * ax.z * vv - ax.x * s;
+    Rq[6] = ax.z * ax.x * vv - ax.y * s; Rq[7] = ax.z * ax.y * vv + ax.x * s; Rq[8] = c + ax.z * ax.z * vv;
+    mm3(M->joint_rot[b], Rq, P);
+  }
+  f3 t = ld3(M->joint_pos[b]);
+  tf_step<1>(P, t, k);
+  tf_step<2>(P, t, k);
+  tf_step<4>(P, t, k);
+  float Rb[9];
+  mm3(R0, P, Rb);
+  const f3 ob = mv3(R0, t);
+  const f3 ab = mv3(Rb, ax);  // R_b axis = R_parent jrot axis (the joint rotation fixes its axis)
+  const float qd = E.nu[5 + b];
+  const f3 qa = qd * ab;
+  f3 wb = qa;
+  scan3(wb, k);
+  wb = w0 + wb;
+  const f3 op = shr1_or(ob, k, mk(0, 0, 0));
+  const f3 wp = shr1_or(wb, k, w0);
+  const f3 r = ob - op;
+  f3 vb = cross(wp, r);
+  scan3(vb, k);
+  vb = v0 + vb;
+  f3 alb = mk(0, 0, 0), acb = mk(0, 0, 0);
+  if (bias) {
+    alb = cross(wp, qa);
+    scan3(alb, k);
+    const f3 alp = shr1_or(alb, k, mk(0, 0, 0));
+    acb = cross(alp, r) + cross(wp, cross(wp, r));
+    scan3(acb, k);
+    acb = mk(0, 0, -gz) + acb;
+  }
+  if (body) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) E.R[b][i] = Rb[i];
+    st3(E.o[b], ob); st3(E.a[b], ab); st3(E.w[b], wb); st3(E.v[b], vb);
+    if (bias) { st3(E.u.kin.al[b], alb); st3(E.u.kin.ac[b], acb); }
+  } else if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) E.R[0][i] = R0[i];
+    st3(E.o[0], mk(0, 0, 0)); st3(E.v[0], v0); st3(E.w[0], w0);
+    if (bias) { st3(E.u.kin.al[0], mk(0, 0, 0)); st3(E.u.kin.ac[0], mk(0, 0, -gz)); }
   }
 }
 
@@ -322,10 +446,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     STAMP(1);
     // ---- A2/A3: kinematics + RNEA forward
     for (int rep = 0; rep < HG_REP_KIN; rep++) {
+#if HG_KIN_SCAN
+      kin_scan(E, M, l, gz, true);
+#else
       kin_local(E, M, l);
       __syncthreads();
       if (l < 2) kin_chain(E, M, l, gz, true);
       if (l == 2) { st3(E.u.kin.al[0], mk(0, 0, 0)); st3(E.u.kin.ac[0], mk(0, 0, -gz)); }
+#endif
       __syncthreads();
     }
     STAMP(2);
@@ -849,9 +977,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   if (l < 6) E.nu[l] = E.root[7 + l];
   if (l < 12) E.nu[6 + l] = E.qd[l];
   __syncthreads();
+#if HG_KIN_SCAN
+  kin_scan(E, M, l, gz, false);
+#else
   kin_local(E, M, l);
   __syncthreads();
   if (l < 2) kin_chain(E, M, l, gz, false);
+#endif
   __syncthreads();
   // stage the [13][13] rigid states and [13][3] contact forces in LDS, then store each env's
   // rows as one contiguous run (AoS, the reference's tensor layout)
