@@ -64,6 +64,10 @@ constexpr int RMAX = 32;
 #ifndef HG_KIN_SCAN
 #define HG_KIN_SCAN 1
 #endif
+// RNEA backward recursions + composite inertias as DPP suffix sums in registers (needs KIN_SCAN)
+#ifndef HG_RNEA_SCAN
+#define HG_RNEA_SCAN 1
+#endif
 #ifndef HG_CHOL_SB
 #define HG_CHOL_SB 0
 #endif
@@ -249,7 +253,12 @@ __device__ __forceinline__ f3 shr1_or(f3 v, int k, f3 base) {  // parent's value
   return k == 0 ? base : u;
 }
 
-__device__ void kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool bias) {
+struct KinLane {  // one lane's body after kin_scan (lane 0: the base; lanes 13..31: don't-care)
+  float R[9];
+  f3 o, w, al, ac;
+};
+
+__device__ KinLane kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool bias) {
   const bool body = l >= 1 && l <= 12;
   const int b = body ? l : 1;
   const int k = (b - 1) % 6;  // link index within the leg
@@ -302,6 +311,7 @@ __device__ void kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool bias
     scan3(acb, k);
     acb = mk(0, 0, -gz) + acb;
   }
+  KinLane K;
   if (body) {
 #pragma unroll
     for (int i = 0; i < 9; i++) E.R[b][i] = Rb[i];
@@ -312,6 +322,85 @@ __device__ void kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool bias
     for (int i = 0; i < 9; i++) E.R[0][i] = R0[i];
     st3(E.o[0], mk(0, 0, 0)); st3(E.v[0], v0); st3(E.w[0], w0);
     if (bias) { st3(E.u.kin.al[0], mk(0, 0, 0)); st3(E.u.kin.ac[0], mk(0, 0, -gz)); }
+  }
+  const bool base = l == 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) K.R[i] = base ? R0[i] : Rb[i];
+  K.o = base ? mk(0, 0, 0) : ob;
+  K.w = base ? w0 : wb;
+  K.al = base ? mk(0, 0, 0) : alb;
+  K.ac = base ? mk(0, 0, -gz) : acb;
+  return K;
+}
+
+// ---- A4 + A5 in registers after kin_scan: per-body inertia / RNEA forces / composite seeds (lane
+// b), then the leg's backward recursions as suffix sums with DPP row_shl (partner lane b + N in the
+// same 16-lane row, kept where link k + N stays in the leg):
+//   F_k = sum_{j>=k} f_j,  N_k = sum_{j>=k} n_j + sum_{j>=k} o_j x f_j - o_k x F_k
+//   (= kin_chain's n_k + N_{k+1} + (o_{k+1} - o_k) x F_{k+1} unrolled), composite mass / first /
+//   second moments as plain suffix sums; h_k = a_k . N_k.
+template <int N>
+__device__ __forceinline__ float shl(float x) {  // lane i <- lane i + N within the 16-lane row
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x100 | N, 0xF, 0xF, true));
+}
+template <int N>
+__device__ __forceinline__ void sfx_step(float* v, int n, int k) {
+  const bool take = k + N <= 5;
+  for (int i = 0; i < n; i++) {
+    const float u = keep_dpp(shl<N>(v[i]));
+    v[i] = take ? v[i] + u : v[i];
+  }
+}
+
+__device__ void rnea_scan(EnvSh& E, const hg_model* M, int l, const KinLane& K, float scale0) {
+  const int b = l < 13 ? l : 0;
+  const bool leg = l >= 1 && l <= 12;
+  const int k = leg ? (l - 1) % 6 : 6;  // lanes outside the legs take no partner
+  const f3 o = K.o;
+  const f3 cb = o + mv3(K.R, ld3(M->com[b]));
+  float Iw[6];
+  {
+    const float* I = M->inertia[b];
+    const float* Rm = K.R;
+    float Im[9] = {I[0], I[3], I[4], I[3], I[1], I[5], I[4], I[5], I[2]};
+    float T9[9];
+    mm3(Rm, Im, T9);
+    float W9[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) W9[i * 3 + j] = T9[i * 3] * Rm[j * 3] + T9[i * 3 + 1] * Rm[j * 3 + 1] + T9[i * 3 + 2] * Rm[j * 3 + 2];
+    Iw[0] = W9[0]; Iw[1] = W9[4]; Iw[2] = W9[8]; Iw[3] = W9[1]; Iw[4] = W9[2]; Iw[5] = W9[5];
+  }
+  float mb = M->mass[b];
+  if (b == 0) {
+    mb = E.mass0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) Iw[i] *= scale0;
+  }
+  const f3 wb = K.w, alb = K.al, acb = K.ac;
+  const f3 d = cb - o;
+  const f3 acc = acb + cross(alb, d) + cross(wb, cross(wb, d));
+  const f3 fb = mb * acc;
+  const f3 nb = symv(Iw, alb) + cross(wb, symv(Iw, wb)) + cross(d, fb);
+  const float cc = dot(cb, cb);
+  const f3 of = cross(o, fb);
+  // [F(3), S_n(3), S_of(3), m, m c(3), J(6)]
+  float v[19] = {fb.x, fb.y, fb.z, nb.x, nb.y, nb.z, of.x, of.y, of.z, mb, mb * cb.x, mb * cb.y, mb * cb.z,
+                 Iw[0] + mb * (cc - cb.x * cb.x), Iw[1] + mb * (cc - cb.y * cb.y), Iw[2] + mb * (cc - cb.z * cb.z),
+                 Iw[3] - mb * cb.x * cb.y, Iw[4] - mb * cb.x * cb.z, Iw[5] - mb * cb.y * cb.z};
+  sfx_step<1>(v, 19, k);
+  sfx_step<2>(v, 19, k);
+  sfx_step<4>(v, 19, k);
+  const f3 F = mk(v[0], v[1], v[2]);
+  const f3 Nk = mk(v[3], v[4], v[5]) + mk(v[6], v[7], v[8]) - cross(o, F);
+  if (l < 13) {
+    st3(E.u.kin.f[b], F); st3(E.u.kin.n[b], Nk);
+    E.cm[b] = v[9];
+    st3(E.cs[b], mk(v[10], v[11], v[12]));
+#pragma unroll
+    for (int i = 0; i < 6; i++) E.cJ[b][i] = v[13 + i];
+    if (leg) E.h[5 + b] = dot(ld3(E.a[b]), Nk);
   }
 }
 
@@ -445,6 +534,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     STAMP(1);
     // ---- A2/A3: kinematics + RNEA forward
+#if HG_KIN_SCAN && HG_RNEA_SCAN
+    // one register-resident pass over the legs: kinematics (prefix scans), then the per-body
+    // forces and the backward recursions (suffix scans) — no barrier until the base totals
+    const KinLane K = kin_scan(E, M, l, gz, true);
+    STAMP(2);
+    rnea_scan(E, M, l, K, scale0);
+    STAMP(3);
+#else
     for (int rep = 0; rep < HG_REP_KIN; rep++) {
 #if HG_KIN_SCAN
       kin_scan(E, M, l, gz, true);
@@ -525,6 +622,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         for (int i = 0; i < 6; i++) cJch[i] = cJb[i];
       }
     }
+#endif
     __syncthreads();
     // base totals (lane 0) — read the kinematics scratch before M overwrites it
     if (l == 0) {
