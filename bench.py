@@ -236,13 +236,13 @@ def main():
     env = make_env(args.envs, device, seed=5 + rank, terrain=args.terrain, push_curriculum=c5)
     runner = OnPolicyRunner(env, train_cfg(args.T, "bf16" if c5 else "fp32", "fp16" if c5 else "fp32"),
                             log_dir=None, device=device)
-    timer = KernelTimer()
+    timer = KernelTimer(every=int(os.environ.get("HG_TIMER_EVERY", "4")))
     env.kernel_timer = timer
     runner.learn(args.warmup, init_at_random_ep_len=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.enabled = True
+    timer.enabled = timer.every > 0
     t0 = time.time()
     runner.learn(args.steps)
     torch.cuda.synchronize()

@@ -36,7 +36,7 @@ struct Layout {
   size_t off[HG_T_COUNT + 8];
   size_t bytes;
   // extra regions
-  size_t obs_buf[2], priv_buf[2], frame_obs, frame_priv, cfg, model;
+  size_t obs_buf[2], priv_buf[2], frame_obs, frame_priv, cfg, model, obs_noise, noise_counter;
 };
 
 enum { X_OBS0 = HG_T_COUNT, X_OBS1, X_PRIV0, X_PRIV1, X_FOBS, X_FPRIV, X_CFG, X_MODEL };
@@ -92,6 +92,8 @@ Layout make_layout(const hg_cfg* c) {
   L.frame_priv = o; o += align256((size_t)n * HG_PRIV1 * 4);
   L.cfg = o; o += align256(sizeof(hg_cfg));
   L.model = o; o += align256(sizeof(hg_model));
+  L.obs_noise = o; o += align256((size_t)48 * np * 4);
+  L.noise_counter = o; o += align256(sizeof(uint64_t));
   L.off[HG_T_OBS_BUF] = L.obs_buf[0];
   L.off[HG_T_PRIV_BUF] = L.priv_buf[0];
   L.bytes = o;
@@ -226,10 +228,13 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   S.terrain_type = (int32_t*)P(HG_T_TERRAIN_TYPE);
   S.cfg = (const hg_cfg*)(s->arena + s->L.cfg);
   S.model = (const hg_model*)(s->arena + s->L.model);
+  S.obs_noise = (float*)(s->arena + s->L.obs_noise);
+  S.noise_counter = (uint64_t*)(s->arena + s->L.noise_counter);
   // zero the arena, upload cfg/model, initial state (synchronous: creation is not on the hot path)
   if (hipMemset(arena, 0, s->L.bytes) != hipSuccess ||
       hipMemcpy((void*)S.cfg, &s->cfg, sizeof(hg_cfg), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy((void*)S.model, &s->model, sizeof(hg_model), hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy((void*)S.model, &s->model, sizeof(hg_model), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(S.noise_counter, 0xFF, sizeof(uint64_t)) != hipSuccess) {
     delete s;
     return fail(nullptr, HG_ERR_HIP, "hip memset/memcpy failed (is the arena device memory?)");
   }

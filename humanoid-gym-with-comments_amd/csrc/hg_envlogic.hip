@@ -773,7 +773,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     P[69] = go.stance[0]; P[70] = go.stance[1];
     P[71] = cm0; P[72] = cm1;
     float z[48];
-    if (C.add_noise) {
+    if (C.add_noise && *S.noise_counter == counter) {
+      // drawn by the K_step epilogue for this counter (same Philox keys, same values)
+#pragma unroll
+      for (int i = 0; i < 48; i++) z[i] = S.obs_noise[i * np + e];
+    } else if (C.add_noise) {
 #pragma unroll
       for (int b = 0; b < 12; b++) normals4(rng4(cfg, e, counter, b, RNG_OBS_NOISE), z + 4 * b);
     } else {

@@ -1071,6 +1071,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
 
   // ---------------- epilogue: rigid-body states (refresh_rigid_body_state_tensor) + store
+  // observation noise of the post launch that follows this step (env.step passes it
+  // step_counter + 1): 12 lanes per env draw one Philox block each here, where lanes are idle,
+  // instead of one K_post thread drawing all twelve in sequence.  K_post checks the counter.
+  if (cfg->add_noise && l < 12 && valid) {
+    float z4[4];
+    normals4(rng4(cfg, e, step_counter + 1, l, RNG_OBS_NOISE), z4);
+#pragma unroll
+    for (int i = 0; i < 4; i++) S.obs_noise[(4 * l + i) * np + e] = z4[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *S.noise_counter = step_counter + 1;
   const bool bad = E.bad != 0;
   if (l < 6) E.nu[l] = E.root[7 + l];
   if (l < 12) E.nu[6 + l] = E.qd[l];

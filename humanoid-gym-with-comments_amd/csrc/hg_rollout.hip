@@ -21,6 +21,7 @@ namespace {
 
 constexpr int TPB = 256;
 constexpr uint32_t RNG_ACTION_SAMPLE = 9;
+constexpr int ACT_LANES = 16;  // lanes per env in the sampling blocks (num_actions <= 16)
 
 __device__ inline u4 philox_key(uint64_t seed, uint32_t env, uint64_t step, uint32_t block) {
   u4 c = {env, (uint32_t)step, (block & 0xFFFFu) | ((uint32_t)(step >> 32) << 16), RNG_ACTION_SAMPLE};
@@ -55,9 +56,37 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
                                             OT* __restrict__ cobs_out, uint64_t seed, uint64_t counter,
                                             int env_blocks, int vec) {
   if ((int)blockIdx.x < env_blocks) {
+    const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
+    if (A <= ACT_LANES) {
+      // one 16-lane group per env, one lane per action (its Philox block computed by each of the
+      // block's lanes); the log-prob terms are summed in action order by every lane of the group
+      // (the same additions as the one-thread-per-env loop below)
+      const int e = (int)(((int64_t)blockIdx.x * TPB + threadIdx.x) / ACT_LANES);
+      const int j = threadIdx.x % ACT_LANES;
+      if (e >= n) return;  // whole groups leave together
+      float term = 0.f;
+      if (j < A) {
+        float z4[4];
+        normals4(philox_key(seed, (uint32_t)e, counter, (uint32_t)(j >> 2)), z4);
+        const float z = (j & 3) == 0 ? z4[0] : (j & 3) == 1 ? z4[1] : (j & 3) == 2 ? z4[2] : z4[3];
+        const float m = mean[(size_t)e * A + j], s = std[j];
+        const float a = m + s * z;
+        const float d = a - m;
+        term = -(d * d) / (2.0f * (s * s)) - logf(s) - c;
+        act_out[(size_t)e * A + j] = a;
+        mu_out[(size_t)e * A + j] = m;
+        sigma_out[(size_t)e * A + j] = s;
+      }
+      float lp = 0.f;
+      for (int jj = 0; jj < A; jj++) lp += __shfl(term, jj, ACT_LANES);
+      if (j == 0) {
+        logp_out[e] = lp;
+        if (value) value_out[e] = value[e];
+      }
+      return;
+    }
     const int e = blockIdx.x * TPB + threadIdx.x;
     if (e >= n) return;
-    const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
     float lp = 0.f;
     float z4[4];
     for (int j = 0; j < A; j++) {
@@ -122,7 +151,8 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
   const uintptr_t in_al = (uintptr_t)obs | (critic_obs_width > 0 ? (uintptr_t)critic_obs : 0);
   const uintptr_t out_al = (uintptr_t)obs_out | (critic_obs_width > 0 ? (uintptr_t)critic_obs_out : 0);
   const int vec = in_al % 16 == 0 && out_al % (obs_fp16 ? 8 : 16) == 0;
-  const int env_blocks = (num_envs + TPB - 1) / TPB;
+  const int64_t env_threads = (int64_t)num_envs * (num_actions <= ACT_LANES ? ACT_LANES : 1);
+  const int env_blocks = (int)((env_threads + TPB - 1) / TPB);
   const int copy_blocks = 512;
   hipStream_t s = (hipStream_t)stream;
   if (obs_fp16)
