@@ -34,7 +34,11 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) dense peak
 HBM_PEAK_GBS = 8000.0
-PROFILE_DIR = "r1_v6"  # the committed rocprofv3 summaries of the current kernels
+# K_step algorithmic HBM bytes per env and launch: 492 B read (state, actions,
+# warm-start impulses) + 1316 B written (rigid 13x13, contacts 13x3, root, dofs, torques, actions,
+# warm-start) + 192 B of next-step observation noise (48 floats)
+KSTEP_BYTES_PER_ENV = 492 + 1316 + 192
+PROFILE_DIR = "r1_v7"  # the committed rocprofv3 summaries of the current kernels
 PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
 
@@ -266,9 +270,9 @@ def main():
                 "achieved": round(achieved_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": 1808 * args.envs,
-                "hbm_achieved_GBs": round(1808 * args.envs / (ms_step * 1e-3) / 1e9, 1),
-                "hbm_frac": round(1808 * args.envs / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "algorithmic_bytes_per_launch": KSTEP_BYTES_PER_ENV * args.envs,
+                "hbm_achieved_GBs": round(KSTEP_BYTES_PER_ENV * args.envs / (ms_step * 1e-3) / 1e9, 1),
+                "hbm_frac": round(KSTEP_BYTES_PER_ENV * args.envs / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                 "valu_issue_util": sq_issue(),
                 "valu_issue_source": f"profiles/{PROFILE_DIR}/sq_counters_k_step2.json (2 x SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES)",
                 "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
