@@ -56,7 +56,8 @@ struct HgState {
   int32_t* nonfinite;     // [np]
   int32_t* terrain_level; // [np]
   int32_t* terrain_type;  // [np]
-  float* obs_noise;       // [48][np] N(0,1) observation noise of the next post launch (K_step epilogue)
+  float* obs_noise;       // [np][48] N(0,1) observation noise of the next post launch (K_step epilogue;
+                          // per-env rows, so each wave writes whole cache lines)
   uint64_t* noise_counter;// [1] the post counter obs_noise was drawn for (~0: none)
   const hg_cfg* cfg;      // device copy
   const hg_model* model;  // device copy

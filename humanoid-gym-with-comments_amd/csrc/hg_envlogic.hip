@@ -775,8 +775,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     float z[48];
     if (C.add_noise && *S.noise_counter == counter) {
       // drawn by the K_step epilogue for this counter (same Philox keys, same values)
+      const float4* zr = reinterpret_cast<const float4*>(S.obs_noise + (size_t)e * 48);
 #pragma unroll
-      for (int i = 0; i < 48; i++) z[i] = S.obs_noise[i * np + e];
+      for (int q = 0; q < 12; q++) {
+        const float4 v = zr[q];
+        z[4 * q] = v.x; z[4 * q + 1] = v.y; z[4 * q + 2] = v.z; z[4 * q + 3] = v.w;
+      }
     } else if (C.add_noise) {
 #pragma unroll
       for (int b = 0; b < 12; b++) normals4(rng4(cfg, e, counter, b, RNG_OBS_NOISE), z + 4 * b);

@@ -1077,8 +1077,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   if (cfg->add_noise && l < 12 && valid) {
     float z4[4];
     normals4(rng4(cfg, e, step_counter + 1, l, RNG_OBS_NOISE), z4);
-#pragma unroll
-    for (int i = 0; i < 4; i++) S.obs_noise[(4 * l + i) * np + e] = z4[i];
+    // per-env rows [e][48]: lanes 0..11 of the wave's two envs store 384 contiguous bytes (whole
+    // cache lines; the former [48][np] columns were 8-byte pieces the L2 fetched lines for)
+    *reinterpret_cast<float4*>(S.obs_noise + (size_t)e * 48 + 4 * l) = make_float4(z4[0], z4[1], z4[2], z4[3]);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *S.noise_counter = step_counter + 1;
   const bool bad = E.bad != 0;
