@@ -196,6 +196,7 @@ struct GatherTab {
 struct GatherArgs {
   GatherTab t[3];
   int ntab;
+  int short_rows;  // every table 4-byte elements and <= 1024 wide: the all-loads-first path
 };
 
 template <typename E>
@@ -211,6 +212,26 @@ __device__ inline void gather_row(const E* __restrict__ src, E* __restrict__ dst
   for (; j < w; j += 64) dst[j] = src[j];
 }
 
+// rows up to 16 x 64 elements: every load of the row's three tables is issued before the first
+// store (up to 48 loads in flight per lane instead of 4)
+constexpr int GK = 16;
+template <typename E>
+__device__ inline void gather_load(const E* __restrict__ src, int64_t w, int lane, E* v) {
+#pragma unroll
+  for (int k = 0; k < GK; k++) {
+    const int64_t j = lane + 64 * k;
+    v[k] = j < w ? src[j] : E(0);
+  }
+}
+template <typename E>
+__device__ inline void gather_store(E* __restrict__ dst, int64_t w, int lane, const E* v) {
+#pragma unroll
+  for (int k = 0; k < GK; k++) {
+    const int64_t j = lane + 64 * k;
+    if (j < w) dst[j] = v[k];
+  }
+}
+
 __global__ void __launch_bounds__(TPB) k_gather_rows(const int64_t* __restrict__ idx, int64_t rows,
                                                      int64_t src_rows, GatherArgs A) {
   const int64_t i = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
@@ -218,6 +239,16 @@ __global__ void __launch_bounds__(TPB) k_gather_rows(const int64_t* __restrict__
   if (i >= rows) return;
   int64_t s = idx[i];
   s = s < 0 ? 0 : (s >= src_rows ? src_rows - 1 : s);  // never read out of bounds
+  if (A.short_rows) {
+    uint32_t v[3][GK];
+#pragma unroll
+    for (int t = 0; t < 3; t++)
+      if (t < A.ntab) gather_load<uint32_t>((const uint32_t*)A.t[t].src + s * A.t[t].width, A.t[t].width, lane, v[t]);
+#pragma unroll
+    for (int t = 0; t < 3; t++)
+      if (t < A.ntab) gather_store<uint32_t>((uint32_t*)A.t[t].dst + i * A.t[t].width, A.t[t].width, lane, v[t]);
+    return;
+  }
   for (int t = 0; t < A.ntab; t++) {
     const GatherTab& T = A.t[t];
     if (T.es == 4)
@@ -244,6 +275,8 @@ extern "C" int hg_gather_rows(const int64_t* idx, int64_t rows, int64_t src_rows
     if (!dst[t] || w[t] <= 0 || (es[t] != 4 && es[t] != 2)) return HG_ERR_ARG;
     A.t[A.ntab++] = GatherTab{src[t], dst[t], w[t], es[t]};
   }
+  A.short_rows = 1;
+  for (int t = 0; t < A.ntab; t++) A.short_rows &= (A.t[t].es == 4 && A.t[t].width <= 64 * GK);
   const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
   hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(TPB), 0, (hipStream_t)stream, idx, rows, src_rows, A);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
