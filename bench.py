@@ -42,7 +42,7 @@ PROFILE_DIR = "r1_v8"  # the committed rocprofv3 summaries of the current kernel
 PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
 
-def sq_issue(kernel_file=os.path.join(REPO, "profiles", PROFILE_DIR, "sq_counters_k_step2.json")):
+def sq_issue(kernel_file=os.path.join(REPO, "profiles", PROFILE_DIR, "sq_counters_k_step.json")):
     """SIMD VALU issue utilisation of K_step from the committed SQ counter passes (None if absent)."""
     try:
         with open(kernel_file) as f:
@@ -51,7 +51,7 @@ def sq_issue(kernel_file=os.path.join(REPO, "profiles", PROFILE_DIR, "sq_counter
         return None
 
 
-def pmc_traffic(kernel="k_step2"):
+def pmc_traffic(kernel="k_step"):
     """HBM bytes per launch of `kernel` from the committed PMC summary (None if absent)."""
     try:
         with open(PMC_SUMMARY) as f:
@@ -261,7 +261,7 @@ def main():
     env_steps = args.envs * args.T * args.steps * world
     value = env_steps / elapsed
     rows = active_rows(env)
-    traffic, traffic_src = (pmc_traffic("k_step2") if args.envs == 4096 and args.terrain == "plane" and not c5
+    traffic, traffic_src = (pmc_traffic("k_step") if args.envs == 4096 and args.terrain == "plane" and not c5
                             else (None, None))
     ms_step = timer.mean_ms("k_step")
     flops = physics_flops_per_env_step(rows) * args.envs
@@ -274,7 +274,7 @@ def main():
                 "hbm_achieved_GBs": round(KSTEP_BYTES_PER_ENV * args.envs / (ms_step * 1e-3) / 1e9, 1),
                 "hbm_frac": round(KSTEP_BYTES_PER_ENV * args.envs / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                 "valu_issue_util": sq_issue(),
-                "valu_issue_source": f"profiles/{PROFILE_DIR}/sq_counters_k_step2.json (2 x SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES)",
+                "valu_issue_source": f"profiles/{PROFILE_DIR}/sq_counters_k_step.json (2 x SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES)",
                 "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
                 "launch_sampling": f"HIP events on 1 in {timer.every} launches of the timed region",
                 "flops_per_launch": flops, "active_rows_per_env": round(rows, 2),

@@ -9,8 +9,7 @@
 
 #include "hg_common.h"
 
-extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, hipStream_t stream);
-extern "C" int hg_launch_step2(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
+extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
                                hipStream_t stream);
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
                               float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
@@ -110,7 +109,6 @@ struct Sim {
   int parity;  // which obs/priv buffer holds the latest stack
   uint64_t post_seq = 0;  // post/reset launches so far: EP_STATS ring row of the next one
   int ep_slot = 0;        // ring row written by the latest one
-  int physics_version;  // 2 (lane-parallel, default) or 1 (lane-per-env reference kernel)
   std::string err;
 };
 
@@ -179,10 +177,6 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   s->arena = (char*)arena;
   s->bytes = arena_bytes;
   s->parity = 0;
-  {
-    const char* pv = getenv("HG_PHYSICS");
-    s->physics_version = (pv && strcmp(pv, "v1") == 0) ? 1 : 2;
-  }
   const int n = cfg->num_envs;
   HgState& S = s->S;
   S.n = n;
@@ -300,8 +294,7 @@ int hg_tensor(void* sim, int id, hg_desc* d) {
 int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream) {
   Sim* s = (Sim*)sim;
   if (!s || !actions) return fail(s, HG_ERR_ARG, "null argument");
-  const int rc = s->physics_version == 1 ? hg_launch_step(&s->S, actions, step_counter, (hipStream_t)stream)
-                                         : hg_launch_step2(&s->S, actions, step_counter, s->cfg.fix_base_link, (hipStream_t)stream);
+  const int rc = hg_launch_step(&s->S, actions, step_counter, s->cfg.fix_base_link, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_step launch failed");
   return HG_OK;
 }
@@ -461,4 +454,4 @@ extern "C" int hg_set_env_props(void* sim, const float* friction, const float* b
   return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_props launch failed");
 }
 
-extern "C" const char* hg_version(void) { return "hg_sim 0.2 (gfx950, physics v2: 32 lanes/env, LDS-resident, Delassus PGS)"; }
+extern "C" const char* hg_version(void) { return "hg_sim 0.3 (gfx950, K_step: 32 lanes/env, LDS-resident, MFMA Delassus, register PGS)"; }

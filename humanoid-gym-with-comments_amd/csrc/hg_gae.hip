@@ -6,7 +6,9 @@
 // [t, :] row it touches is a contiguous 4*N-byte stream, so the wave's loads/stores coalesce.
 // The op order of the reference is kept and FMA contraction is disabled (clang fp contract(off);
 // plus -ffp-contract=off for this file), so returns match the reference bitwise.
-// Per-block (sum A, sum A^2) partials are reduced in fp64 and added to stats[0..1].
+// Per-block (sum A, sum A^2) partials are written in fp64 to stats[2 + 2b .. 3 + 2b] and a
+// one-wave final kernel adds them to stats[0..1] in block order: the statistics, and so the
+// normalised advantages, are bitwise reproducible run to run (no atomics).
 // Pass 2 (k_gae_norm): A = (A - mean) / (std_unbiased + 1e-8), elementwise, float4-vectorised.
 // Roofline: HBM.  Algorithmic bytes: 17 B per (t, env) in pass 1 (r 4 + done 1 + V 4 + R 4 +
 // A 4) + 8 B per env (last V read) ; 8 B per element in pass 2.
@@ -42,7 +44,7 @@ __global__ void __launch_bounds__(256) k_gae_scan(const float* __restrict__ rewa
       next_v = v;
     }
   }
-  // wave reduction then one atomic pair per block
+  // wave reduction, then the block's partial pair (fixed order, no atomics)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s1 += __shfl_down(s1, off, 64);
@@ -55,8 +57,24 @@ __global__ void __launch_bounds__(256) k_gae_scan(const float* __restrict__ rewa
   if (threadIdx.x == 0) {
     double a = 0.0, b = 0.0;
     for (int w = 0; w < (int)(blockDim.x >> 6); w++) { a += red[0][w]; b += red[1][w]; }
-    atomicAdd(&stats[0], a);
-    atomicAdd(&stats[1], b);
+    stats[2 + 2 * blockIdx.x] = a;
+    stats[3 + 2 * blockIdx.x] = b;
+  }
+}
+
+// fixed-order sum of the block partials: lane i sums blocks i, i+64, ... in order, then a
+// fixed butterfly over the 64 lanes; added to stats[0..1] (zeroed first when zero_stats)
+__global__ void __launch_bounds__(64) k_gae_stats_final(double* __restrict__ stats, int nblocks, int zero_stats) {
+  double a = 0.0, b = 0.0;
+  for (int k = threadIdx.x; k < nblocks; k += 64) { a += stats[2 + 2 * k]; b += stats[3 + 2 * k]; }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = (zero_stats ? 0.0 : stats[0]) + a;
+    stats[1] = (zero_stats ? 0.0 : stats[1]) + b;
   }
 }
 
@@ -82,11 +100,14 @@ extern "C" int hg_gae_scan(const float* rewards, const uint8_t* dones, const flo
                            int zero_stats, void* stream) {
   if (T <= 0 || N <= 0 || !rewards || !dones || !values || !last_values || !returns || !advantages || !stats) return 1;
   hipStream_t s = (hipStream_t)stream;
-  if (zero_stats && hipMemsetAsync(stats, 0, 2 * sizeof(double), s) != hipSuccess) return 2;
-  hipLaunchKernelGGL(k_gae_scan, dim3((N + 255) / 256), dim3(256), 0, s, rewards, dones, values, last_values, returns,
+  const int nblocks = (N + 255) / 256;
+  hipLaunchKernelGGL(k_gae_scan, dim3(nblocks), dim3(256), 0, s, rewards, dones, values, last_values, returns,
                      advantages, stats, T, N, gamma, lam);
+  hipLaunchKernelGGL(k_gae_stats_final, dim3(1), dim3(64), 0, s, stats, nblocks, zero_stats);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
+
+extern "C" int64_t hg_gae_stats_len(int N) { return N > 0 ? 2 + 2 * (int64_t)((N + 255) / 256) : 0; }
 
 extern "C" int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int64_t n_local, void* stream) {
   if (!advantages || !stats || count < 2 || n_local <= 0) return 1;

@@ -90,7 +90,7 @@ T = {name: i for i, name in enumerate(TENSOR_IDS)}
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
            "hg_post", "hg_ep_stats_slot", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_set_root_state", "hg_set_env_props",
-           "hg_measure_heights", "hg_gae_scan", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
+           "hg_measure_heights", "hg_gae_scan", "hg_gae_stats_len", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
            "hg_rollout_act", "hg_rollout_env", "hg_gather_rows", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
            "hg_mlp_act_backward", "hg_mlp_act_backward_scratch", "hg_colsum_jobs", "hg_linear_skinny_supported",
            "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch", "hg_version"]
@@ -139,6 +139,8 @@ def load_library(path=LIB_PATH):
     L.hg_gae_scan.restype = ctypes.c_int
     L.hg_gae_scan.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                               ctypes.c_float, ctypes.c_int, vp]
+    L.hg_gae_stats_len.restype = ctypes.c_int64
+    L.hg_gae_stats_len.argtypes = [ctypes.c_int]
     L.hg_gae_normalize.restype = ctypes.c_int
     L.hg_gae_normalize.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64, vp]
     L.hg_kl_mean.restype = ctypes.c_int

@@ -52,8 +52,24 @@ class HgAdam(torch.optim.Optimizer):
                 st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
 
     def load_state_dict(self, state_dict):
+        # the group's lr is the live device scalar the PPO adaptive-KL rule writes (PPO._lr_f32);
+        # torch's loader would replace it by the checkpoint's value and cut that link, so the
+        # update graph would keep a stale constant.  The reference re-assigns param_group['lr']
+        # from PPO.learning_rate before every step (ppo.py:173-174), so the loaded lr is never
+        # used there either: keep the live tensor.
+        lr = self.param_groups[0]["lr"]
         super().load_state_dict(state_dict)
+        if torch.is_tensor(lr):
+            self.param_groups[0]["lr"] = lr
         self.version += 1
+
+    def state_dict(self):
+        # lr as a Python float, as torch.optim.Adam writes it (reference checkpoints stay loadable both ways)
+        sd = super().state_dict()
+        for g in sd["param_groups"]:
+            if torch.is_tensor(g.get("lr")):
+                g["lr"] = float(g["lr"].item())
+        return sd
 
     def _lr_tensor(self, device):
         lr = self.param_groups[0]["lr"]

@@ -116,7 +116,12 @@ class OnPolicyRunner:
                     self.alg.process_env_step(rewards, dones, infos)
                     if self.log_dir is not None:
                         if "episode" in infos:
-                            ep_infos.append(infos["episode"])
+                            # hg_sim publishes views into a ring of episode_snapshot_rows launches:
+                            # rollouts at least that long keep a copy instead
+                            ep = infos["episode"]
+                            if self.num_steps_per_env >= getattr(self.env, "episode_snapshot_rows", float("inf")):
+                                ep = {k: v.clone() if torch.is_tensor(v) else v for k, v in ep.items()}
+                            ep_infos.append(ep)
                         cur_reward_sum += rewards
                         cur_episode_length += 1
                         new_ids = (dones > 0).nonzero(as_tuple=False)

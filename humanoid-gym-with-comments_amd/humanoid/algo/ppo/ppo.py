@@ -37,6 +37,15 @@ def _world():
     return 1
 
 
+
+def _as_u8(x):
+    """0/1 byte mask for the HIP kernels: bool/uint8 reinterpreted in place, any other dtype (the
+    reference's int64 reset_buf) converted."""
+    x = x.contiguous()
+    if x.dtype in (torch.bool, torch.uint8):
+        return x.view(torch.uint8)
+    return (x != 0).to(torch.uint8)
+
 class PPO:
     actor_critic: ActorCritic
 
@@ -214,8 +223,7 @@ class PPO:
             p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
             to = infos.get("time_outs")
             r = rewards.contiguous().float()
-            d = dones.contiguous().view(torch.uint8)
-            to = to.contiguous().view(torch.uint8) if to is not None else None
+            d, to = _as_u8(dones), (_as_u8(to) if to is not None else None)
             s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
             if self._defer_values():
                 # time-out bootstrap deferred to the batched value pass in compute_returns

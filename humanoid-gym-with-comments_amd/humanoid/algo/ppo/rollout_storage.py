@@ -68,6 +68,7 @@ class RolloutStorage:
         self.gae_fn = None  # optional override (tests); default: HIP kernel
         self.time_outs = None  # [T, N, 1] u8, only when PPO defers the value pass (device path)
         self.values_deferred = False
+        self._stats_buf = None  # [hg_gae_stats_len(N)] f64: (sum A, sum A^2) + the kernel's block partials
         self._stats = torch.zeros(2, dtype=torch.float64, device=device)
 
     def add_transitions(self, transition: Transition):
@@ -109,6 +110,11 @@ class RolloutStorage:
         from humanoid import _native as N
         L = N.lib()
         lv = last_values.detach().reshape(-1).contiguous().float()
+        if self._stats_buf is None:
+            L.hg_gae_stats_len.restype = ctypes.c_int64
+            L.hg_gae_stats_len.argtypes = [ctypes.c_int]
+            self._stats_buf = torch.zeros(int(L.hg_gae_stats_len(Nn)), dtype=torch.float64, device=self.rewards.device)
+            self._stats = self._stats_buf[:2]
         s = ctypes.c_void_p(torch.cuda.current_stream(self.rewards.device).cuda_stream)
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         N.check(L.hg_gae_scan(p(self.rewards), p(self.dones), p(self.values), p(lv), p(self.returns),

@@ -349,6 +349,8 @@ class XBotLFreeEnv(BaseTask):
             self.height_points = self._init_height_points()
             self._height_xy = self.height_points[0, :, :2].contiguous()
             self.measured_heights = torch.zeros(self.num_envs, self.num_height_points, device=self.device)
+        # extras["episode"] entries are views into a ring of this many post/reset snapshots
+        self.episode_snapshot_rows = N.EP_RING
         self.course_gain = 1.0   # read by OnPolicyRunner.learn (on_policy_runner.py:160-162)
         self.course_ratio = 1.0
 

@@ -211,12 +211,14 @@ int hg_measure_heights(void* sim, const float* points_xy, int num_points, float*
 /* ---- rollout storage: fused GAE (replaces RolloutStorage.compute_returns,
  * humanoid/algo/ppo/rollout_storage.py:122-143) ---- */
 /* Pass 1: reverse-time scan.  rewards/values/returns/advantages [T,N] f32, dones [T,N] u8,
- * last_values [N].  Writes returns and raw advantages, and accumulates (sum A, sum A^2) in
- * float64 into stats[0..1] (stats must be zeroed by the caller or by hg_gae_scan when
- * zero_stats != 0). */
+ * last_values [N].  Writes returns and raw advantages, and adds (sum A, sum A^2) in float64 to
+ * stats[0..1] (set instead of added when zero_stats != 0).  stats holds hg_gae_stats_len(N)
+ * doubles: stats[2..] is scratch for the per-block partials, which are summed in a fixed order
+ * (bitwise reproducible; no atomics).  Two launches. */
 int hg_gae_scan(const float* rewards, const uint8_t* dones, const float* values,
                 const float* last_values, float* returns, float* advantages, double* stats,
                 int T, int N, float gamma, float lam, int zero_stats, void* stream);
+int64_t hg_gae_stats_len(int N);
 /* Pass 2: advantages = (A - mean) / (std_unbiased + 1e-8) with mean/std from stats over
  * `count` elements (count = T*N*world_size after an all-reduce of stats). */
 int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int64_t n_local,

@@ -6,7 +6,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-ks = [i for i, r in enumerate(rows) if "k_step2" in r["Kernel_Name"][:24]]
+ks = [i for i, r in enumerate(rows) if "k_step" in r["Kernel_Name"][:24]]
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 24
 # last full iteration: from the first K_step of the last group of T to the first K_step of... the end
 first = ks[-T]
@@ -17,7 +17,7 @@ seg = rows[prev_first:first]  # the second-to-last iteration (collection + learn
 def cls(n):
     if n.startswith("Cijk") or "gemm" in n.lower():
         return "gemm"
-    for k in ("k_step2", "elu_kernel", "k_act_bwd", "k_colsum", "index_elementwise", "reduce_kernel", "k_post",
+    for k in ("k_step", "elu_kernel", "k_act_bwd", "k_colsum", "index_elementwise", "reduce_kernel", "k_post",
               "k_stack", "k_skinny", "k_adam", "k_sqnorm", "k_ppo_loss", "k_kl", "copyBuffer", "FillFunctor",
               "gather", "k_act", "k_env", "k_gae", "k_lr"):
         if k in n:

@@ -11,7 +11,7 @@ import csv, glob, sys, collections
 tot = collections.Counter(); n = collections.Counter()
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "k_step2" in r["Kernel_Name"][:24]:
+        if "k_step" in r["Kernel_Name"][:24]:
             tot[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
 print({k: round(v / n[k]) for k, v in tot.items()})
 PY

@@ -7,7 +7,7 @@ done
 python3 - "$R/gpurun_out" <<'PY'
 import csv, glob, sys, collections
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    for k in ("k_step2", "k_post_step"):
+    for k in ("k_step", "k_post_step"):
         v = [float(r["Counter_Value"]) for f in glob.glob(f"{sys.argv[1]}/pmck_{c}/**/*counter_collection.csv", recursive=True)
              for r in csv.DictReader(open(f)) if k in r["Kernel_Name"][:30]]
         print(c, k, round(sum(v) / max(len(v), 1)), "KB/launch", len(v))

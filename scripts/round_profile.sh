@@ -6,7 +6,7 @@ cd "$R"
 bash scripts/profile.sh || exit $?
 python scripts/pmc_summary.py gpurun_out/prof gpurun_out/prof/pmc_summary.json gpurun_out/prof/trace/run_kernel_stats.csv > /dev/null || exit $?
 bash scripts/pmc_sq.sh || exit $?
-python scripts/sq_summary.py gpurun_out/pmc_sq gpurun_out/pmc_sq/sq_counters_k_step2.json || exit $?
+python scripts/sq_summary.py gpurun_out/pmc_sq gpurun_out/pmc_sq/sq_counters_k_step.json || exit $?
 cd "$R"
 timeout -k 10 700 python scripts/trajectory_curve.py > gpurun_out/traj.log 2>&1 || exit $?
 timeout -k 10 600 python bench.py > gpurun_out/bench_round.log 2>&1 || exit $?

@@ -1,4 +1,4 @@
-"""Summarise the two SQ counter passes of scripts/pmc_sq.sh for k_step2 into per-wave figures.
+"""Summarise the two SQ counter passes of scripts/pmc_sq.sh for k_step into per-wave figures.
 Usage: python scripts/sq_summary.py <pmc_sq dir> <out.json>"""
 import csv
 import glob
@@ -14,7 +14,7 @@ def main():
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if "k_step2" not in r["Kernel_Name"][:24]:
+                if "k_step" not in r["Kernel_Name"][:24]:
                     continue
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
                 launches[r["Counter_Name"]].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
@@ -30,7 +30,7 @@ def main():
         "active_valu": round(pw["SQ_ACTIVE_INST_VALU"] / wc, 3)}
     # two waves share each SIMD: the SIMD's VALU is busy ~2x one wave's VALU-active fraction
     res["simd_valu_busy_est"] = round(2 * pw["SQ_ACTIVE_INST_VALU"] / wc, 3)
-    res["_note"] = ("k_step2, 4096 envs, 5 PGS sweeps, random actions; 2 waves per SIMD; SQ cycle counters in "
+    res["_note"] = ("k_step, 4096 envs, 5 PGS sweeps, random actions; 2 waves per SIMD; SQ cycle counters in "
                     "quad-cycles; two --pmc passes with --kernel-trace only (scripts/pmc_sq.sh)")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)

@@ -24,12 +24,10 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def _make_env(n, version="v2", **over):
-    import os
+def _make_env(n, **over):
     from humanoid.envs import XBotLCfg
     from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
     from humanoid.utils.helpers import SimParams
-    os.environ["HG_PHYSICS"] = version
     torch.manual_seed(5)
     np.random.seed(5)
     cfg = XBotLCfg()
@@ -38,16 +36,13 @@ def _make_env(n, version="v2", **over):
     for k, v in over.items():
         sec, name = k.split("__")
         setattr(getattr(cfg, sec), name, v)
-    try:
-        return XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
-    finally:
-        os.environ.pop("HG_PHYSICS", None)
+    return XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
 
 
-@pytest.fixture(scope="module", params=["v2", "v1"])
-def physics_env(request):
+@pytest.fixture(scope="module")
+def physics_env():
     _need_gpu()
-    return _make_env(N_ENVS, request.param)
+    return _make_env(N_ENVS)
 
 
 @pytest.fixture(scope="module")
@@ -132,6 +127,29 @@ def test_gae_kernel_large_properties():
     ret, _ = E.gae(st.rewards[..., 0].cpu().numpy(), st.dones[..., 0].cpu().numpy(), st.values[..., 0].cpu().numpy(),
                    last[:, 0].cpu().numpy(), 0.994, 0.9)
     np.testing.assert_array_equal(st.returns[..., 0].cpu().numpy(), ret)
+
+
+def test_gae_deterministic():
+    """Two identical compute_returns calls give bitwise-identical normalised advantages: the
+    (sum A, sum A^2) statistics are block partials summed in a fixed order (no float atomics)."""
+    _need_gpu()
+    from humanoid.algo.ppo import RolloutStorage
+    T, N = 24, 4096
+    gen = torch.Generator(device="cuda:0").manual_seed(11)
+    r = torch.randn(T, N, 1, device="cuda:0", generator=gen)
+    v = torch.randn(T, N, 1, device="cuda:0", generator=gen)
+    d = (torch.rand(T, N, 1, device="cuda:0", generator=gen) < 0.05).to(torch.uint8)
+    last = torch.randn(N, 1, device="cuda:0", generator=gen)
+    outs = []
+    for _ in range(2):
+        st = RolloutStorage(N, T, [1], [1], [1], device="cuda:0")
+        st.rewards.copy_(r)
+        st.values.copy_(v)
+        st.dones.copy_(d)
+        st.compute_returns(last, 0.994, 0.9)
+        outs.append((st.advantages.clone(), st._stats.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
 
 
 def _oracle_cfg(env):
@@ -233,8 +251,7 @@ def _step_only(env, actions, counter):
 
 
 def test_step_physics_parity(physics_env):
-    """One K_step (prologue + 10 substeps + rigid states) vs the C reference simulator, for the
-    lane-parallel kernel (v2, default) and the lane-per-env kernel (v1)."""
+    """One K_step (prologue + 10 substeps + rigid states) vs the C reference simulator."""
     import pipeline_ref as PR
     env = physics_env
     for _ in range(5):
@@ -260,29 +277,27 @@ def test_step_physics_parity(physics_env):
         assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
 
 
-@pytest.mark.parametrize("version", ["v2", "v1"])
-def test_trajectory_1000_steps_fixed_base(version):
+def test_trajectory_1000_steps_fixed_base():
     """SURVEY §8d parity trajectory, variant A (fix_base_link): joint angles / torques of the HIP
     path vs the f64 reference simulator over 1000 policy steps (10,000 substeps)."""
     _need_gpu()
-    err_q, err_tau = _run_trajectory(fixed=True, steps=1000, version=version)
+    err_q, err_tau = _run_trajectory(fixed=True, steps=1000)
     assert err_q.max() < 2e-3, err_q.max()
     assert err_tau.max() < 0.5, err_tau.max()
 
 
-@pytest.mark.parametrize("version", ["v2", "v1"])
-def test_trajectory_floating_base(version):
+def test_trajectory_floating_base():
     """Variant B (floating base on the plane): tight agreement over the first 100 steps; the
     contact dynamics then diverge chaotically (fp32 vs fp64), so the rest is reported."""
     _need_gpu()
-    err_q, err_tau = _run_trajectory(fixed=False, steps=300, version=version)
+    err_q, err_tau = _run_trajectory(fixed=False, steps=300)
     assert err_q[:100].max() < 5e-2, err_q[:100].max()
     print("floating-base |dq| max at steps 100/200/300:", err_q[99], err_q[199], err_q[299])
 
 
-def _run_trajectory(fixed, steps, version="v2"):
+def _run_trajectory(fixed, steps):
     import pipeline_ref as PR
-    env = _make_env(16, version, asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
+    env = _make_env(16, asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
                     domain_rand__push_robots=False, noise__add_noise=False)
     S, _, _ = snapshot(env)
     oc = _oracle_cfg(env)
