@@ -429,7 +429,7 @@ def test_ppo_graphed_update_matches_eager():
 @pytest.fixture(scope="module")
 def terrain_env():
     _need_gpu()
-    return _make_env(N_ENVS, "v2", terrain__mesh_type="heightfield", terrain__measure_heights=True)
+    return _make_env(N_ENVS, terrain__mesh_type="heightfield", terrain__measure_heights=True)
 
 
 def test_step_physics_parity_heightfield(terrain_env):
@@ -510,7 +510,7 @@ def test_terrain_curriculum_parity():
     (humanoid_env.py:1075-1095); against the numpy pipeline on the same state."""
     _need_gpu()
     import pipeline_ref as PR
-    env = _make_env(N_ENVS, "v2", terrain__mesh_type="heightfield", terrain__curriculum=True)
+    env = _make_env(N_ENVS, terrain__mesh_type="heightfield", terrain__curriculum=True)
     assert env._hgcfg.curriculum == 1
     for _ in range(3):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
@@ -614,7 +614,7 @@ def test_config5_bf16_policy_fp16_storage_push_curriculum():
     import pipeline_ref as PR
     from humanoid.algo.ppo import OnPolicyRunner
     import bench
-    env = _make_env(N_ENVS, "v2", domain_rand__push_curriculum=True)
+    env = _make_env(N_ENVS, domain_rand__push_curriculum=True)
     env.update_push_curriculum(0)
     assert abs(env._hgcfg.max_push_vel_xy - 0.2) < 1e-6
     env.update_push_curriculum(10 ** 6)
@@ -762,7 +762,7 @@ def test_initial_state_parity():
     step 0) vs pipeline_ref.initial_state: root/dof state, commands, first observation stacks."""
     _need_gpu()
     import pipeline_ref as PR
-    env = _make_env(N_ENVS, "v2")
+    env = _make_env(N_ENVS)
     g = lambda t: t.detach().cpu().numpy()  # noqa: E731
     S, obs, priv = PR.initial_state(_oracle_cfg(env), g(env.env_origins), g(env.body_mass)[:, 0],
                                     g(env.env_frictions)[:, 0])
@@ -782,7 +782,7 @@ def test_reset_idx_and_indexed_writes():
     import ctypes as C
     import pipeline_ref as PR
     from humanoid import _native as N
-    env = _make_env(N_ENVS, "v2")
+    env = _make_env(N_ENVS)
     for _ in range(4):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
     torch.cuda.synchronize()
