@@ -103,7 +103,7 @@ __device__ void reset_env(const hg_cfg* cfg, HgState& S, int e, uint64_t step, i
     uint32_t u[4] = {r.x, r.y, r.z, r.w};
     for (int i = 0; i < 4; i++) {
       int j = b * 4 + i;
-      S.dof_pos[j * np + e] = cfg->default_dof_pos[j] + (0.1f - (-0.1f)) * u01(u[i]) + (-0.1f);
+      S.dof_pos[j * np + e] = cfg->default_dof_pos[j] + ((0.1f - (-0.1f)) * u01(u[i]) + (-0.1f));  // default + torch_rand_float(-0.1, 0.1)
       S.dof_vel[j * np + e] = 0.f;
     }
   }

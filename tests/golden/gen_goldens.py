@@ -14,7 +14,8 @@ Recipe:
     the stubs below restate Isaac Gym Preview 4's published definitions.  Values depending only
     on them are "parity unpinned" (see DESIGN.md).
 
-Usage:  python tests/golden/gen_goldens.py   (writes tests/golden/*.npz)
+Usage:  python tests/golden/gen_goldens.py [name ...]   (writes tests/golden/*.npz; names: gae actor_critic
+        ppo_update env math pipeline heights terrain)
 """
 import importlib.util
 import os
@@ -103,6 +104,7 @@ def install_stubs():
         m = types.ModuleType("isaacgym." + sub)
         sys.modules["isaacgym." + sub] = m
         setattr(ig, sub, m)
+    sys.modules["isaacgym.gymtorch"].unwrap_tensor = lambda t: None
     tu = _torch_utils_module()
     sys.modules["isaacgym.torch_utils"] = tu
     ig.torch_utils = tu
@@ -406,18 +408,340 @@ def gen_math(he):
     np.savez_compressed(os.path.join(OUT, "quat.npz"), q=q, v=v, rot_inv=rot_inv, apply=app, euler=eul)
 
 
-def main():
+# ----------------------------------------------------------------------------------------------
+# reference-pinned pipeline (injected draws): the reference's own step() / post_physics_step /
+# reset_idx / curriculum / _get_heights / HumanoidTerrain, with torch's RNG calls intercepted and
+# the raw draws recorded, so oracle/pipeline_ref.py can be run on the same draws
+# ----------------------------------------------------------------------------------------------
+class _NoGym:
+    """gym stub: every call (refresh_*, simulate, set_*_tensor*) is a no-op; physics is frozen."""
+
+    def __getattr__(self, name):
+        return lambda *a, **k: None
+
+
+class DrawRecorder:
+    """Intercepts torch.rand / torch.randn_like / torch.randint_like and the env module's
+    torch_rand_float while the reference runs; records the RAW draws (uniforms before scaling,
+    normals, integers) under a purpose key derived from the calling reference method."""
+
+    KEYS = {("rand", "step"): "step:rand", ("randn_like", "step"): "step:randn_like",
+            ("randn_like", "compute_observations"): "obs:randn_like",
+            ("randint_like", "_update_terrain_curriculum"): "curriculum:randint",
+            ("rf", "_push_robots"): "push", ("rf", "_reset_dofs"): "reset:dof",
+            ("rf", "_reset_root_states"): "reset:root"}
+
+    def __init__(self, he, seed):
+        self.he = he
+        self.g = torch.Generator().manual_seed(seed)
+        self.rec = {}
+
+    def _key(self, kind, depth):
+        f = sys._getframe(depth)
+        name = f.f_code.co_name
+        if kind == "rf" and name == "_resample_commands":
+            outer = f.f_back.f_code.co_name
+            return {"_post_physics_step_callback": "callback:cmd", "reset_idx": "reset:cmd"}[outer]
+        return self.KEYS[(kind, name)]
+
+    def _add(self, key, t):
+        self.rec.setdefault(key, []).append(t.detach().clone().numpy())
+
+    def __enter__(self):
+        self.saved = (torch.rand, torch.randn_like, torch.randint_like, self.he.torch_rand_float)
+        rand0, randn_like0, randint_like0, _ = self.saved
+        rec = self
+
+        def rand(*shape, **kw):
+            if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
+                shape = tuple(shape[0])
+            kw.pop("device", None)
+            u = rand0(*shape, generator=rec.g, **kw)
+            rec._add(rec._key("rand", 2), u)
+            return u
+
+        def randn_like(x, **kw):
+            z = torch.randn(x.shape, generator=rec.g, dtype=x.dtype)
+            rec._add(rec._key("randn_like", 2), z)
+            return z
+
+        def randint_like(x, high, **kw):
+            r = torch.randint(0, int(high), x.shape, generator=rec.g, dtype=x.dtype)
+            rec._add(rec._key("randint_like", 2), r)
+            return r
+
+        def torch_rand_float(lower, upper, shape, device):
+            u = rand0(*shape, generator=rec.g)
+            rec._add(rec._key("rf", 2), u)
+            return (upper - lower) * u + lower   # isaacgym.torch_utils.torch_rand_float
+
+        torch.rand, torch.randn_like, torch.randint_like = rand, randn_like, randint_like
+        self.he.torch_rand_float = torch_rand_float
+        return self
+
+    def __exit__(self, *exc):
+        torch.rand, torch.randn_like, torch.randint_like, self.he.torch_rand_float = self.saved
+        return False
+
+
+STATE_KEYS = ("dof_pos", "dof_vel", "actions", "last_actions", "last_last_actions", "torques", "last_dof_vel",
+              "root_states", "last_root_vel", "rigid_state", "contact_forces", "commands", "feet_air_time",
+              "last_contacts", "feet_height", "last_feet_z", "rand_push_force", "rand_push_torque", "env_frictions",
+              "body_mass", "episode_length_buf", "base_lin_vel", "base_ang_vel", "projected_gravity",
+              "base_euler_xyz", "env_origins", "default_dof_pos", "ref_dof_pos")
+
+
+def _cfg_record(E, N, terrain_type, curriculum):
+    """The hg_cfg fields oracle/pipeline_ref.Cfg reads, from the reference's XBotLCfg."""
+    c = E.cfg
+    rg = c.commands.ranges
+    dt = E.dt
+    scales = {k: v for k, v in E.reward_scales.items()}   # already x dt, zero scales dropped
+    REWARDS = ["action_smoothness", "base_acc", "base_height", "collision", "default_joint_pos", "dof_acc",
+               "dof_vel", "feet_air_time", "feet_clearance", "feet_contact_forces", "feet_contact_number",
+               "feet_distance", "foot_slip", "joint_pos", "knee_distance", "low_speed", "orientation", "torques",
+               "track_vel_hard", "tracking_ang_vel", "tracking_lin_vel", "vel_mismatch_exp"]
+    r = dict(num_envs=N, seed=0, dt=dt, cycle_time=c.rewards.cycle_time,
+             target_joint_pos_scale=c.rewards.target_joint_pos_scale, target_feet_height=c.rewards.target_feet_height,
+             base_height_target=c.rewards.base_height_target, min_dist=c.rewards.min_dist, max_dist=c.rewards.max_dist,
+             tracking_sigma=c.rewards.tracking_sigma, max_contact_force=c.rewards.max_contact_force,
+             max_episode_length=float(E.max_episode_length), only_positive_rewards=int(c.rewards.only_positive_rewards),
+             obs_lin_vel=c.normalization.obs_scales.lin_vel, obs_ang_vel=c.normalization.obs_scales.ang_vel,
+             obs_dof_pos=c.normalization.obs_scales.dof_pos, obs_dof_vel=c.normalization.obs_scales.dof_vel,
+             obs_quat=c.normalization.obs_scales.quat, noise_dof_pos=c.noise.noise_scales.dof_pos,
+             noise_dof_vel=c.noise.noise_scales.dof_vel, noise_ang_vel=c.noise.noise_scales.ang_vel,
+             noise_quat=c.noise.noise_scales.quat, noise_level=c.noise.noise_level,
+             clip_observations=c.normalization.clip_observations, clip_actions=c.normalization.clip_actions,
+             dynamic_randomization=c.domain_rand.dynamic_randomization,
+             cmd_lin_x=list(rg.lin_vel_x), cmd_lin_y=list(rg.lin_vel_y), cmd_ang_yaw=list(rg.ang_vel_yaw),
+             cmd_heading=list(rg.heading), heading_command=int(c.commands.heading_command),
+             resample_interval=int(c.commands.resampling_time / dt),
+             push_interval=int(np.ceil(c.domain_rand.push_interval_s / dt)), push_robots=int(c.domain_rand.push_robots),
+             max_push_vel_xy=c.domain_rand.max_push_vel_xy, max_push_ang_vel=c.domain_rand.max_push_ang_vel,
+             add_noise=int(E.add_noise), init_pos=list(c.init_state.pos), init_rot=list(c.init_state.rot),
+             init_lin_vel=list(c.init_state.lin_vel), init_ang_vel=list(c.init_state.ang_vel),
+             terrain_type=terrain_type, fix_base_link=int(c.asset.fix_base_link), curriculum=int(curriculum),
+             terrain_rows=int(getattr(E, "max_terrain_level", 0)), terrain_env_length=float(c.terrain.terrain_length),
+             max_episode_length_s=float(E.max_episode_length_s),
+             reward_scale=[float(scales.get(n, 0.0)) for n in REWARDS])
+    return r
+
+
+def _pipeline_env(he, N, seed, curriculum):
+    from collections import deque
+    import types as _t
+    XB = he.XBotLFreeEnv
+    E = XB.__new__(XB)
+    g = make_env_state(E, he, N, seed=seed)
+    c = E.cfg
+    E.gym, E.sim, E.viewer = _NoGym(), None, None
+    E.dof_state = torch.zeros(N * 18, 2)
+    E.common_step_counter = 0
+    E.extras = {}
+    E.max_episode_length_s = c.env.episode_length_s
+    E.command_ranges = he.class_to_dict(c.commands.ranges)
+    E.reward_scales = he.class_to_dict(c.rewards.scales)
+    E.rew_buf = torch.zeros(N)
+    E.reset_buf = torch.zeros(N, dtype=torch.bool)
+    E.time_out_buf = torch.zeros(N, dtype=torch.bool)
+    E._prepare_reward_function()
+    for n in E.episode_sums:
+        E.episode_sums[n][:] = torch.rand(N, generator=g) - 0.3
+    E.p_gains = torch.rand(N, 18, generator=g) * 300
+    E.d_gains = torch.rand(N, 18, generator=g) * 10
+    E.torque_limits = torch.rand(18, generator=g) * 150 + 20
+    E.forward_vec = torch.tensor([[1.0, 0.0, 0.0]]).repeat(N, 1)
+    E.base_init_state = torch.tensor(c.init_state.pos + c.init_state.rot + c.init_state.lin_vel + c.init_state.ang_vel)
+    E.last_rigid_state = torch.zeros_like(E.rigid_state)
+    E.ref_dof_pos = (torch.rand(N, 18, generator=g) - 0.5) * 0.6   # left by the previous observation pass
+    E.add_noise = True
+    E.noise_scale_vec = E._get_noise_scale_vec(c)
+    E.env_origins = torch.zeros(N, 3)
+    E.env_origins[:, :2] = (torch.rand(N, 2, generator=g) - 0.5) * 20
+    E.init_done = True
+    c.domain_rand.push_robots = True
+    c.domain_rand.push_interval = np.ceil(c.domain_rand.push_interval_s / E.dt)   # _parse_cfg
+    if curriculum:
+        rows, cols = 5, 4
+        c.terrain.curriculum = True
+        c.terrain.mesh_type = "trimesh"
+        E.custom_origins = True
+        E.terrain = _t.SimpleNamespace(env_length=c.terrain.terrain_length)
+        E.max_terrain_level = rows
+        E.terrain_origins = torch.rand(rows, cols, 3, generator=g) * torch.tensor([40.0, 32.0, 0.3])
+        E.terrain_levels = torch.randint(0, rows, (N,), generator=g)
+        E.terrain_levels[::4] = rows - 1          # some at the top level: move up -> random level
+        E.terrain_types = torch.randint(0, cols, (N,), generator=g)
+        E.env_origins[:] = E.terrain_origins[E.terrain_levels, E.terrain_types]
+        # walked far (move up) / not far (move down) / in between
+        E.root_states[:, :2] = E.env_origins[:, :2] + (torch.rand(N, 2, generator=g) - 0.5) * 12
+    else:
+        c.terrain.curriculum = False
+        E.custom_origins = False
+    E.obs_history = deque(maxlen=c.env.frame_stack)
+    E.critic_history = deque(maxlen=c.env.c_frame_stack)
+    for _ in range(c.env.frame_stack):
+        E.obs_history.append(torch.randn(N, c.env.num_single_obs, generator=g))
+    for _ in range(c.env.c_frame_stack):
+        E.critic_history.append(torch.randn(N, c.env.single_num_privileged_obs, generator=g))
+    # force the branches: base contact (reset), time-outs, command resampling, a push step
+    E.contact_forces[:, 0, :] = 0
+    E.contact_forces[0:3, 0, 2] = 40.0
+    E.episode_length_buf[3:6] = int(E.max_episode_length)        # +1 -> time-out
+    E.episode_length_buf[6:10] = int(c.commands.resampling_time / E.dt) - 1
+    E.episode_length_buf[10:] = E.episode_length_buf[10:] % 2000
+    E.common_step_counter = int(np.ceil(c.domain_rand.push_interval_s / E.dt)) * 3 - 1  # +1 -> push
+    return E, g
+
+
+def gen_pipeline(he):
+    """pipeline18.npz: the reference's step() with gym.simulate a no-op, at the fork's 18-DOF
+    layout, twice: 'plane' (resample, push, base-contact and time-out resets, observation noise)
+    and 'curriculum' (custom origins, terrain curriculum incl. the top-level random draw, root xy
+    randomisation).  Inputs, every recorded draw and the outputs."""
+    out = {}
+    for tag, curriculum, seed in (("plane", False, 31), ("curriculum", True, 32)):
+        N = 24
+        E, g = _pipeline_env(he, N, seed, curriculum)
+        cfgr = _cfg_record(E, N, 1 if curriculum else 0, curriculum)
+        for k, v in cfgr.items():
+            out[f"{tag}/cfg/{k}"] = np.asarray(v)
+        for k in STATE_KEYS:
+            v = getattr(E, k)
+            out[f"{tag}/in/{k}"] = v.numpy().copy() if torch.is_tensor(v) else np.asarray(v)
+        for n in E.episode_sums:
+            out[f"{tag}/in/sum/{n}"] = E.episode_sums[n].numpy().copy()
+        out[f"{tag}/in/obs_history"] = torch.cat(list(E.obs_history), 1).numpy().copy()
+        out[f"{tag}/in/critic_history"] = torch.cat(list(E.critic_history), 1).numpy().copy()
+        out[f"{tag}/in/p_gains"] = E.p_gains.numpy().copy()
+        out[f"{tag}/in/d_gains"] = E.d_gains.numpy().copy()
+        out[f"{tag}/in/torque_limits"] = E.torque_limits.numpy().copy()
+        out[f"{tag}/in/action_scale"] = np.float64(E.cfg.control.action_scale)
+        out[f"{tag}/in/common_step_counter"] = np.int64(E.common_step_counter)
+        if curriculum:
+            out[f"{tag}/in/terrain_levels"] = E.terrain_levels.numpy().copy()
+            out[f"{tag}/in/terrain_types"] = E.terrain_types.numpy().copy()
+            out[f"{tag}/in/terrain_origins"] = E.terrain_origins.numpy().copy()
+        acts = (torch.rand(N, 18, generator=g) - 0.5) * 6
+        out[f"{tag}/in/policy_actions"] = acts.numpy().copy()
+        with DrawRecorder(he, seed + 100) as rec:
+            obs, priv, rew, reset, extras = E.step(acts.clone())
+        for k, lst in rec.rec.items():
+            for i, a in enumerate(lst):
+                out[f"{tag}/draw/{k}/{i}"] = a
+        for k in STATE_KEYS + ("rew_buf", "reset_buf", "time_out_buf", "obs_buf", "privileged_obs_buf"):
+            v = getattr(E, k)
+            out[f"{tag}/out/{k}"] = v.numpy().copy() if torch.is_tensor(v) else np.asarray(v)
+        for n in E.episode_sums:
+            out[f"{tag}/out/sum/{n}"] = E.episode_sums[n].numpy().copy()
+        for k, v in extras.get("episode", {}).items():
+            out[f"{tag}/out/episode/{k}"] = np.float32(v)
+        if curriculum:
+            out[f"{tag}/out/terrain_levels"] = E.terrain_levels.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "pipeline18.npz"), **out)
+
+
+def gen_heights(he):
+    """heights.npz: the reference's _get_heights on a random heightfield at random base poses
+    (yaw-rotated 17 x 11 grid, border offset, truncation, edge clipping, min of 3 neighbours)."""
+    import types as _t
+    XB = he.XBotLFreeEnv
+    E = XB.__new__(XB)
+    from humanoid.envs.custom.humanoid_config import XBotLCfg
+    c = XBotLCfg()
+    c.terrain.mesh_type = "trimesh"
+    c.terrain.border_size = 2.0
+    E.cfg = c
+    E.device = "cpu"
+    N = 16
+    E.num_envs = N
+    g = torch.Generator().manual_seed(41)
+    rows, cols = 140, 120
+    E.height_samples = torch.randint(-200, 300, (rows, cols), generator=g, dtype=torch.int16)
+    E.terrain = _t.SimpleNamespace(cfg=c.terrain)
+    y = torch.tensor(c.terrain.measured_points_y)
+    x = torch.tensor(c.terrain.measured_points_x)
+    gx, gy = torch.meshgrid(x, y, indexing="ij")
+    E.num_height_points = gx.numel()
+    hp = torch.zeros(N, E.num_height_points, 3)
+    hp[:, :, 0] = gx.flatten()
+    hp[:, :, 1] = gy.flatten()
+    E.height_points = hp
+    q = torch.randn(N, 4, generator=g)
+    q = q / q.norm(dim=1, keepdim=True)
+    E.root_states = torch.zeros(N, 13)
+    E.root_states[:, 0] = torch.rand(N, generator=g) * (rows * 0.1 - 2.0) - 1.0   # some near/over the edges
+    E.root_states[:, 1] = torch.rand(N, generator=g) * (cols * 0.1 - 2.0) - 1.0
+    E.root_states[:, 2] = 0.9
+    E.root_states[:, 3:7] = q
+    E.base_quat = E.root_states[:, 3:7]
+    h = E._get_heights()
+    np.savez_compressed(os.path.join(OUT, "heights.npz"), heightfield=E.height_samples.numpy(),
+                        root_states=E.root_states.numpy(), points_xy=hp[0, :, :2].numpy().copy(),
+                        heights=h.numpy(), border_size=np.float64(c.terrain.border_size),
+                        horizontal_scale=np.float64(c.terrain.horizontal_scale),
+                        vertical_scale=np.float64(c.terrain.vertical_scale))
+
+
+def gen_terrain():
+    """terrain.npz: the reference's HumanoidTerrain (utils/terrain.py:38-231; proportions, choice
+    and difficulty sequence, border, sub-terrain placement, env origins) with the BUILD's
+    terrain_utils standing in for the third-party isaacgym.terrain_utils, on a reduced map."""
+    import types as _t
+    tu_path = os.path.join(os.path.dirname(os.path.dirname(OUT)), "humanoid-gym-with-comments_amd", "humanoid", "utils",
+                           "terrain_utils.py")
+    tspec = importlib.util.spec_from_file_location("build_terrain_utils", tu_path)
+    ours_tu = importlib.util.module_from_spec(tspec)
+    tspec.loader.exec_module(ours_tu)
+    sys.modules["isaacgym.terrain_utils"] = ours_tu
+    sys.modules["isaacgym"].terrain_utils = ours_tu
+    spec = importlib.util.spec_from_file_location("ref_terrain", os.path.join(REF, "humanoid", "utils", "terrain.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    from humanoid.envs.custom.humanoid_config import XBotLCfg
+    out = {}
+    for tag, seed, (rows, cols) in (("a", 5, (4, 5)), ("b", 9, (3, 3))):
+        tc = XBotLCfg.terrain()
+        tc.mesh_type = "heightfield"
+        tc.num_rows, tc.num_cols = rows, cols
+        tc.border_size = 2.0
+        tc.curriculum = False
+        np.random.seed(seed)
+        t = mod.HumanoidTerrain(tc, 64)
+        out[f"{tag}/heightsamples"] = t.heightsamples.copy()
+        out[f"{tag}/env_origins"] = t.env_origins.copy()
+        out[f"{tag}/seed"] = np.int64(seed)
+        out[f"{tag}/rows"] = np.int64(rows)
+        out[f"{tag}/cols"] = np.int64(cols)
+    out["proportions"] = np.asarray(XBotLCfg.terrain.terrain_proportions, np.float64)
+    np.savez_compressed(os.path.join(OUT, "terrain.npz"), **out)
+
+
+def main(only=None):
+    """only: names of the generators to run (default: all)."""
     torch.set_num_threads(1)
+    run = (lambda name: only is None or name in only)
     mods = load_ref_ppo()
-    gen_gae(mods)
-    gen_actor_critic(mods)
-    gen_ppo_update(mods)
+    if run("gae"):
+        gen_gae(mods)
+    if run("actor_critic"):
+        gen_actor_critic(mods)
+    if run("ppo_update"):
+        gen_ppo_update(mods)
     install_stubs()
     from humanoid.envs.custom import humanoid_env as he
-    gen_env(he)
-    gen_math(he)
+    if run("env"):
+        gen_env(he)
+    if run("math"):
+        gen_math(he)
+    if run("pipeline"):
+        gen_pipeline(he)
+    if run("heights"):
+        gen_heights(he)
+    if run("terrain"):
+        gen_terrain()
     print("goldens written to", OUT)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -470,32 +470,15 @@ def test_step_physics_parity_heightfield(terrain_env):
     assert np.isfinite(g(env.root_states)).all()
 
 
-def _heights_ref(root, hs_samples, pts_xy, border, hscale, vscale):
-    """torch-CPU restatement of _get_heights (humanoid_env.py:949-985) + quat_apply_yaw."""
-    q = root[:, 3:7].clone()
-    q[:, :2] = 0.0
-    q = q / q.norm(dim=-1, keepdim=True).clamp(min=1e-9)
-    P = pts_xy.shape[0]
-    v = torch.cat([pts_xy, torch.zeros(P, 1)], dim=1).unsqueeze(0).expand(root.shape[0], P, 3).reshape(-1, 3)
-    qq = q.repeat_interleave(P, dim=0)
-    xyz = qq[:, :3]
-    t = torch.cross(xyz, v, dim=-1) * 2
-    pts = (v + qq[:, 3:] * t + torch.cross(xyz, t, dim=-1)).view(root.shape[0], P, 3) + root[:, :3].unsqueeze(1)
-    pts = pts + border
-    pts = (pts / hscale).long()
-    px = pts[:, :, 0].reshape(-1).clip(0, hs_samples.shape[0] - 2)
-    py = pts[:, :, 1].reshape(-1).clip(0, hs_samples.shape[1] - 2)
-    h = torch.min(torch.min(hs_samples[px, py], hs_samples[px + 1, py]), hs_samples[px, py + 1])
-    return h.view(root.shape[0], -1).float() * vscale
-
-
 def test_measured_heights(terrain_env):
     env = terrain_env
     for _ in range(5):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    import pipeline_ref as PR
     h = env._get_heights().cpu()
-    ref = _heights_ref(env.root_states.cpu(), env.height_samples.cpu().long(), env._height_xy.cpu(),
-                       env.cfg.terrain.border_size, env.cfg.terrain.horizontal_scale, env.cfg.terrain.vertical_scale)
+    # oracle: pipeline_ref.heights, pinned against the reference's _get_heights (tests/golden/heights.npz)
+    ref = torch.from_numpy(PR.heights(_oracle_cfg(env), env.root_states.cpu().numpy(), env._height_xy.cpu().numpy(),
+                                      env.height_samples.cpu().numpy()))
     assert h.shape == (env.num_envs, 187)
     exact = (h == ref).float().mean().item()
     assert exact > 0.999, exact  # cell-boundary float ties aside, bit-exact
