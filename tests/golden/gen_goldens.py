@@ -15,7 +15,7 @@ Recipe:
     on them are "parity unpinned" (see DESIGN.md).
 
 Usage:  python tests/golden/gen_goldens.py [name ...]   (writes tests/golden/*.npz; names: gae actor_critic
-        ppo_update env math pipeline heights terrain)
+        ppo_update env math pipeline heights terrain mjcf)
 """
 import importlib.util
 import os
@@ -717,6 +717,49 @@ def gen_terrain():
     np.savez_compressed(os.path.join(OUT, "terrain.npz"), **out)
 
 
+def gen_mjcf():
+    """mjcf_xbotl.json: the body tree of the reference's MuJoCo description of the same robot
+    (resources/robots/XBot/mjcf/XBot-L.xml) as plain data — per body: parent, pos, quat (w x y z),
+    inertial (pos, quat, mass, diaginertia) and hinge joints (name, axis, range, class
+    armature/frictionloss).  tests/test_model_mjcf.py collapses it like collapse_fixed_joints
+    and cross-checks model/xbotl_model.json (compiled from the URDF) against it."""
+    import json
+    import xml.etree.ElementTree as ET
+    path = os.path.join(REF, "resources", "robots", "XBot", "mjcf", "XBot-L.xml")
+    root = ET.parse(path).getroot()
+    classes = {}
+    for d in root.find("default").iter("default"):
+        cls = d.get("class")
+        j = d.find("joint")
+        if cls and j is not None:
+            classes[cls] = {k: float(v) for k, v in j.attrib.items()}
+    fl = lambda s: [float(x) for x in s.split()]  # noqa: E731
+    bodies = []
+
+    def walk(el, parent):
+        for b in el.findall("body"):
+            rec = dict(name=b.get("name"), parent=parent, pos=fl(b.get("pos", "0 0 0")),
+                       quat=fl(b.get("quat", "1 0 0 0")), joints=[])
+            inn = b.find("inertial")
+            if inn is not None:
+                rec["inertial"] = dict(pos=fl(inn.get("pos", "0 0 0")), quat=fl(inn.get("quat", "1 0 0 0")),
+                                       mass=float(inn.get("mass")), diaginertia=fl(inn.get("diaginertia")))
+            for j in b.findall("joint"):
+                jr = dict(name=j.get("name"), type=j.get("type", "hinge"), axis=fl(j.get("axis", "0 0 1")))
+                if j.get("range"):
+                    jr["range"] = fl(j.get("range"))
+                c = classes.get(j.get("class"), {})
+                jr["armature"] = float(j.get("armature", c.get("armature", 0.0)))
+                jr["frictionloss"] = float(j.get("frictionloss", c.get("frictionloss", 0.0)))
+                rec["joints"].append(jr)
+            bodies.append(rec)
+            walk(b, rec["name"])
+
+    walk(root.find("worldbody"), None)
+    with open(os.path.join(OUT, "mjcf_xbotl.json"), "w") as f:
+        json.dump(dict(source="resources/robots/XBot/mjcf/XBot-L.xml", bodies=bodies), f, indent=0)
+
+
 def main(only=None):
     """only: names of the generators to run (default: all)."""
     torch.set_num_threads(1)
@@ -740,6 +783,8 @@ def main(only=None):
         gen_heights(he)
     if run("terrain"):
         gen_terrain()
+    if run("mjcf"):
+        gen_mjcf()
     print("goldens written to", OUT)
 
 

@@ -1,0 +1,133 @@
+"""Cross-check of the physics model input against the reference's independent robot description.
+
+model/xbotl_model.json is compiled from the URDF (tools/urdf_compile.py, collapse_fixed_joints as
+humanoid_config.py:93).  The reference also ships a MuJoCo description of the same robot
+(resources/robots/XBot/mjcf/XBot-L.xml), written separately; tests/golden/mjcf_xbotl.json holds its
+body tree as plain data.  Collapsing every joint-less MJCF body into its parent gives the same 13
+bodies; their masses, COMs, inertias, joint frames, axes and ranges must agree with the compiled
+model.  This is the only reference-held pin the physics input has (PhysX itself is absent).
+
+Documented differences (asserted as such, not hidden by a tolerance):
+  * the trunk (base_link after the collapse): the MJCF leaves the neck-base, arm-base and hand
+    link masses out of its base body (geoms with density 0, no inertial), so its trunk is 0.95 kg
+    lighter (28.95 vs 29.90 kg) with a COM 1-2 cm off; the build follows the URDF, which is what
+    Isaac Gym loads.  The twelve leg bodies agree to the MJCF's printed precision.
+  * armature / frictionloss: the MJCF gives armature 0.01 and frictionloss 0.01 on the leg joints,
+    0.05 on the ankles; the Isaac Gym asset uses armature 0 (humanoid_config.py:118) and the URDF's
+    joint friction (0.1 N m on the four ankle joints, XBot-L.urdf:1675-1677,1745-1747,2472-2473,
+    2533-2534), which is what the build simulates.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODEL = os.path.join(REPO, "humanoid-gym-with-comments_amd", "model", "xbotl_model.json")
+
+
+def _qmat(q):  # MuJoCo quaternion (w, x, y, z)
+    w, x, y, z = np.asarray(q, float) / np.linalg.norm(q)
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _collapse(bodies):
+    """MJCF tree -> {jointed body: dict(mass, com, I (about COM, body frame), T_parent (4x4 in the
+    parent jointed body's frame), parent, joint)}, merging joint-less bodies into their ancestor."""
+    by = {b["name"]: b for b in bodies}
+    T_world = {}
+    for b in bodies:  # bodies are listed parents first
+        T = np.eye(4)
+        T[:3, :3] = _qmat(b["quat"])
+        T[:3, 3] = b["pos"]
+        T_world[b["name"]] = T if b["parent"] is None else T_world[b["parent"]] @ T
+
+    def owner(name):
+        while not by[name]["joints"]:
+            name = by[name]["parent"]
+        return name
+    out = {}
+    for b in bodies:
+        if b["joints"]:
+            par = owner(b["parent"]) if b["parent"] else None
+            Tp = np.linalg.inv(T_world[par]) @ T_world[b["name"]] if par else np.eye(4)
+            out[b["name"]] = dict(parent=par, T=Tp, joint=b["joints"][0], items=[])
+    for b in bodies:
+        inn = b.get("inertial")
+        if inn is None:
+            continue
+        o = owner(b["name"])
+        T = np.linalg.inv(T_world[o]) @ T_world[b["name"]]
+        R = T[:3, :3] @ _qmat(inn["quat"])
+        c = T[:3, :3] @ np.asarray(inn["pos"]) + T[:3, 3]
+        out[o]["items"].append((inn["mass"], c, R @ np.diag(inn["diaginertia"]) @ R.T))
+    for rec in out.values():
+        m = sum(i[0] for i in rec["items"])
+        com = sum(i[0] * i[1] for i in rec["items"]) / m
+        I = np.zeros((3, 3))
+        for mi, ci, Ii in rec["items"]:
+            d = ci - com
+            I += Ii + mi * (d @ d * np.eye(3) - np.outer(d, d))
+        rec.update(mass=m, com=com, I=I)
+    return out
+
+
+@pytest.fixture(scope="module")
+def models(golden):
+    with open(os.path.join(os.path.dirname(MODEL), "xbotl_model.json")) as f:
+        ours = json.load(f)
+    with open(os.path.join(REPO, "tests", "golden", "mjcf_xbotl.json")) as f:
+        mj = _collapse(json.load(f)["bodies"])
+    return ours, mj
+
+
+def test_same_bodies_and_mass(models):
+    ours, mj = models
+    names = [b["name"] for b in ours["bodies"]]
+    assert sorted(names) == sorted(mj)
+    for b in ours["bodies"][1:]:
+        assert b["mass"] == pytest.approx(mj[b["name"]]["mass"], rel=1e-4), b["name"]
+    dm = ours["bodies"][0]["mass"] - mj["base_link"]["mass"]
+    assert dm == pytest.approx(0.951, abs=0.01)   # documented trunk difference
+    total_mj = sum(r["mass"] for r in mj.values())
+    assert ours["total_mass"] - total_mj == pytest.approx(dm, abs=1e-6)
+
+
+def test_com_and_inertia(models):
+    ours, mj = models
+    for b in ours["bodies"][1:]:
+        r = mj[b["name"]]
+        np.testing.assert_allclose(b["com"], r["com"], atol=1e-5, err_msg=b["name"])
+        I = b["inertia"]
+        Io = np.array([[I[0], I[3], I[4]], [I[3], I[1], I[5]], [I[4], I[5], I[2]]])
+        scale = max(np.abs(r["I"]).max(), 1e-6)
+        np.testing.assert_allclose(Io, r["I"], atol=1e-4 * scale, err_msg=b["name"])
+    # the trunk: documented difference (module docstring)
+    np.testing.assert_allclose(ours["bodies"][0]["com"], mj["base_link"]["com"], atol=0.03)
+
+
+def test_joint_frames_axes_ranges(models):
+    ours, mj = models
+    for b in ours["bodies"][1:]:
+        r = mj[b["name"]]
+        j = b["joint"]
+        assert r["joint"]["name"] == j["name"]
+        assert r["parent"] == ours["bodies"][b["parent"]]["name"]
+        np.testing.assert_allclose(j["origin_pos"], r["T"][:3, 3], atol=1e-4, err_msg=j["name"])
+        np.testing.assert_allclose(np.asarray(j["origin_rot"]), r["T"][:3, :3], atol=2e-5, err_msg=j["name"])
+        np.testing.assert_allclose(j["axis"], r["joint"]["axis"], atol=1e-9, err_msg=j["name"])
+        np.testing.assert_allclose([j["lower"], j["upper"]], r["joint"]["range"], atol=1e-9, err_msg=j["name"])
+
+
+def test_documented_joint_parameter_differences(models):
+    """The MJCF's armature/frictionloss are not the Isaac Gym asset's (see module docstring)."""
+    ours, mj = models
+    for b in ours["bodies"][1:]:
+        r = mj[b["name"]]["joint"]
+        assert r["armature"] == pytest.approx(0.01)
+        ankle = "ankle" in b["name"]
+        assert r["frictionloss"] == pytest.approx(0.05 if ankle else 0.01)
+        assert b["joint"]["friction"] == pytest.approx(0.1 if ankle else 0.0)
