@@ -151,7 +151,15 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   if (cfg->num_envs <= 0) return fail(nullptr, HG_ERR_ARG, "num_envs must be > 0");
   if (model->num_bodies != HG_NB || model->num_dof != HG_ND)
     return fail(nullptr, HG_ERR_ARG, "model must have 13 bodies / 12 dofs (XBot-L profile)");
-  if (model->num_contacts <= 0 || model->num_contacts > HG_NC) return fail(nullptr, HG_ERR_ARG, "bad contact count");
+  if (model->num_contacts <= 0 || model->num_contacts > HG_MAX_CONTACTS) return fail(nullptr, HG_ERR_ARG, "bad contact count");
+  if (model->num_pairs < 0 || model->num_pairs > HG_MAX_PAIRS || model->num_capsules < 0 ||
+      model->num_capsules > HG_MAX_CAPSULES || model->num_contacts + model->num_pairs > 32 ||
+      model->num_leg_contacts < 0 || model->num_leg_contacts > model->num_contacts)
+    return fail(nullptr, HG_ERR_ARG, "bad collision model (<= 32 contact candidates + pairs)");
+  for (int p = 0; p < model->num_pairs; p++)
+    for (int s = 0; s < 2; s++)
+      if (model->pair[p][s] < 0 || model->pair[p][s] >= model->num_capsules)
+        return fail(nullptr, HG_ERR_ARG, "pair names a missing capsule");
   for (int b = 1; b < HG_NB; b++)  // two 6-link leg chains off the base (XBot-L topology)
     if (model->parent[b] != ((b == 1 || b == 7) ? 0 : b - 1))
       return fail(nullptr, HG_ERR_ARG, "model topology must be base + two 6-link leg chains (bodies 1-6, 7-12)");
@@ -364,7 +372,8 @@ __global__ void k_set_dof(HgState S, const int32_t* ids, int n, const float* pos
     if (pos) S.dof_pos[j * S.np + e] = pos[(size_t)i * HG_ND + j];
     if (vel) S.dof_vel[j * S.np + e] = vel[(size_t)i * HG_ND + j];
   }
-  for (int c = HG_NC * 3; c < HG_LAMW; c++) S.lambda[c * S.np + e] = 0.f;
+  // joint limit and friction warm starts
+  for (int c = (HG_MAX_CONTACTS + HG_MAX_PAIRS) * 3; c < HG_LAMW; c++) S.lambda[c * S.np + e] = 0.f;
 }
 __global__ void k_set_root(HgState S, const int32_t* ids, int n, const float* root) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -372,7 +381,7 @@ __global__ void k_set_root(HgState S, const int32_t* ids, int n, const float* ro
   const int e = ids[i];
   if (e < 0 || e >= S.n) return;
   for (int f = 0; f < 13; f++) S.root[f * S.np + e] = root[(size_t)i * 13 + f];
-  for (int c = 0; c < HG_NC * 3; c++) S.lambda[c * S.np + e] = 0.f;
+  for (int c = 0; c < (HG_MAX_CONTACTS + HG_MAX_PAIRS) * 3; c++) S.lambda[c * S.np + e] = 0.f;  // contacts
 }
 
 extern "C" int hg_set_dof_state_indexed(void* sim, const int32_t* env_ids, int n, const float* dof_pos,
@@ -429,7 +438,7 @@ __global__ void k_set_root_all(HgState S, const float* root) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= S.n) return;
   for (int f = 0; f < 13; f++) S.root[f * S.np + e] = root[(size_t)e * 13 + f];
-  for (int c = 0; c < HG_NC * 3; c++) S.lambda[c * S.np + e] = 0.f;
+  for (int c = 0; c < (HG_MAX_CONTACTS + HG_MAX_PAIRS) * 3; c++) S.lambda[c * S.np + e] = 0.f;  // contacts
 }
 __global__ void k_set_props(HgState S, const float* fric, const float* mass) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;

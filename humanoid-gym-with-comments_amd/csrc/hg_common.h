@@ -8,8 +8,6 @@
 #define HG_NB 13
 #define HG_ND 12
 #define HG_NV 18
-#define HG_NC 16
-#define HG_LAMW (HG_NC * 3 + HG_ND)
 #define HG_OBS1 47
 #define HG_PRIV1 73
 
@@ -52,7 +50,7 @@ struct HgState {
   float* ref_dof_pos;     // [12][np]
   float* env_origins;     // [3][np]
   float* ep_stats;        // [24] (+ accumulators [24] after)
-  float* lambda;          // [60][np]
+  float* lambda;          // [HG_LAMW][np] solver warm-start impulses
   int32_t* nonfinite;     // [np]
   int32_t* terrain_level; // [np]
   int32_t* terrain_type;  // [np]

@@ -1,55 +1,75 @@
 // hg_physics.hip — K_step: lane-parallel articulated dynamics for CDNA4 (gfx950).
 //
-// Same algorithm and results as oracle/physics_ref.c, mapped onto the hardware:
-//   * 32 lanes per env, 2 envs per 64-lane wave, block = 1 wave; 4096 envs -> 2048 waves
-//     (8 per CU).  Every per-env working array lives in LDS (~11 KB/env), nothing spills.
-//   * Phases run lane-parallel: 12 joint rotations; the two 6-link leg chains (FK, RNEA forward
-//     and backward) on 2 lanes; 13 bodies' inertia/force terms; 12 mass-matrix columns;
-//     row-parallel Cholesky of M (18 lanes); explicit M^-1 by 18 parallel triangular solves;
-//     one constraint row per lane (<= 32 rows: sole/base contact normals+tangents, joint
-//     limits) with its Jacobian row held in the lane's registers; the Delassus matrix
-//     W = J M^-1 J^T one row per lane.
-//   * Projected Gauss-Seidel entirely in registers: lane r keeps the row velocity v_r = J_r nu
-//     and its Delassus row W[r][0..31]; every lane of an env keeps a copy of the 32 impulses;
-//     a row update reads v_r with v_readlane (no cross-lane reductions) and applies
-//     W[:][r] dlambda as one FMA per lane; the row loop is unrolled so all indices are static.  Gauss-Seidel order (normal, then the tangent pair, row by row) is
-//     the oracle's, so the PGS iterates are the same sequence as physics_ref.c.
-// Replaces humanoid_env.py:620-649 (+ refreshes :776-778), like v1.
+// Replaces the reference's step() preamble + decimation x (_compute_torques, gym.simulate) + the
+// state refreshes (humanoid_env.py:620-649, 776-778).  Same algorithm and results as
+// oracle/physics_ref.c (the build's documented physics), mapped onto the hardware:
+//   * 32 lanes per env, 2 envs per 64-lane wave, block = 1 wave; 4096 envs -> 2048 waves (8 per
+//     CU, 2 per SIMD).  Per-env working arrays live in LDS, the hot per-lane state in registers.
+//   * Kinematics + RNEA as DPP prefix / suffix scans over the two 6-link legs (one lane per
+//     link); composite-rigid-body mass-matrix columns one per lane.
+//   * PD torques with the damping term integrated implicitly on unclipped joints (dt*kd on M's
+//     diagonal; armature 0 as the asset).
+//   * Cholesky of M in registers (lane i = row i, legs-first order, arrow structure skipped), with
+//     g = L^-1 (tau - h) carried along as an extra column; no explicit inverse.
+//   * Contacts: one candidate per lane — sole points / capsule end spheres vs plane or
+//     heightfield, leg-vs-leg capsule pairs (segment closest points) — ranked by ballot/popcount;
+//     at most 9 points (27 rows), then the ankle joint-friction rows, then joint limits (<= 32).
+//   * Lane r owns constraint row r: Jacobian row in registers, z_r = L^-1 J_r^T by a per-lane
+//     forward solve (L broadcast from LDS), the Delassus matrix W = Z^T Z on the matrix cores
+//     (v_mfma_f32_32x32x2f32, 9 per env; the wave's two envs interleaved with v_permlane32_swap).
+//   * Projected Gauss-Seidel in registers over 3-row groups (a contact's normal + tangent pair,
+//     or up to three single rows): one v_readlane round per group, the in-group couplings from
+//     W's 3x3 block, the other rows' velocities updated by one FMA each.  The iterate sequence
+//     is the oracle's row-by-row Gauss-Seidel.
+//   * nu_new = nu + L^-T (dt g + Z^T lambda): one column-oriented back substitution.
 #include "hg_common.h"
-
 
 namespace {
 
-constexpr int RMAX = 32;
+constexpr int RMAX = 32;          // constraint rows per env (one per lane)
+constexpr int NGRP = 11;          // PGS groups of 3 row slots (the 33rd slot is virtual, always empty)
+constexpr int MAX_PTS = 9;        // contact points per env (27 rows)
+constexpr int LAM_PAIR = HG_MAX_CONTACTS * 3;           // warm-start slots (oracle/physics_ref.c)
+constexpr int LAM_LIM = LAM_PAIR + HG_MAX_PAIRS * 3;
+constexpr int LAM_FRIC = LAM_LIM + HG_ND;
+constexpr float BIG = 3.0e38f;
 
-struct RowC {  // per-row constants of the PGS, one 16-byte broadcast read
-  float tgt, invD, invD2;  // target velocity, 1/W_rr, 1/W_(r+1)(r+1) (tangent pair partner)
-  int kind;                // 0 normal, 1 tangent-1 (pair head), 2 tangent-2, 3 joint limit
+struct GroupC {  // PGS constants of one 3-slot group (a, b, c), one broadcast read per field
+  float invD[3];
+  float Wba, Wca, Wcb;     // W[b][a], W[c][a], W[c][b]
+  float tgt[3], lo[3], hi[3];
+  float mu;
+  int contact;             // 1: (a, b, c) = a contact's normal and tangent pair; 0: single rows
+  int pad;
 };
 
 struct __align__(16) EnvSh {
   float root[16];
   float q[12], qd[12], act[12], tau[12];
-  float pd_kp[12], pd_kd[12], pd_lim[12], pd_tgt[12];  // PD constants / position target per joint
+  float pd_kp[12], pd_kd[12], pd_lim[12], pd_tgt[12], madd[12];
   float nu[20];
   float h[20];
-  float lamst[64];
+  float gv[20];            // g = L^-1 (tau - h), legs-first order
+  float invd[20];          // 1 / L_kk
+  float lamst[HG_LAMW];
   float R[13][9];
-  float axp[13][3];  // joint axis in the parent-body frame (jrot * axis)
   float o[13][3], a[13][3], w[13][3], v[13][3];
   float cm[13], cs[13][3], cJ[13][6];
   union {
-    struct { float al[13][3], ac[13][3], f[13][3], n[13][3]; } kin;  // A2..A5 scratch
-    struct { float M[18][20]; float Minv[18][20]; float invd[20]; } fac;                 // A6..A12
-    struct { float rigid[13 * 13]; float cf[13 * 3]; } out;                              // epilogue staging
+    struct { float al[13][3], ac[13][3], f[13][3], n[13][3]; } kin;  // RNEA scratch
+    struct { float xP[RMAX][3], xN[RMAX][3]; } rg;                     // row contact points
+    float Z[RMAX][20];                                                 // z_r rows, legs-first order
+    struct { float rigid[13 * 13]; float cf[13 * 3]; } out;            // epilogue staging
   } u;
-  float Y[RMAX][18];
-  RowC rc[RMAX];
+  float L[18][20];         // M (dof order, lower) then its Cholesky factor (legs-first order)
+  float colbuf[20], bbuf[20];
+  GroupC grp[NGRP];
+  float rd[RMAX][3];       // row direction (contact rows) / sign in rd[r][0] (joint rows)
+  int rbP[RMAX], rbN[RMAX];// contact rows: bodies receiving +/- lambda d; joint rows: rbP = -1 - dof
+  int rlam[RMAX];          // warm-start slot
   float rLam[RMAX];
-  float rx[RMAX][3], rd[RMAX][3];   // row geometry: point (base-centred) and direction
-  int rPt[RMAX], rBody[RMAX];
   float cf[13][3];
-  float base_f[6], base_cm, base_cs[3], base_cJ[6];
+  float base_cm, base_cs[3], base_cJ[6];
   float mass0, fric;
   int nrows, bad;
 };
@@ -334,10 +354,32 @@ __device__ __forceinline__ int lane_opaque(int l) {
   return l;
 }
 
+
+// closest points of the segments [p1,q1], [p2,q2] (Ericson 5.1.9; as oracle/physics_ref.c seg_seg)
+__device__ __forceinline__ void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3& c1, f3& c2) {
+  const f3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
+  const float a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r);
+  const float c = dot(d1, r), b = dot(d1, d2);
+  const float denom = a * e - b * b;
+  float s = denom > 1e-6f * a * e ? fminf(fmaxf((b * f - c * e) / denom, 0.f), 1.f) : 0.f;
+  float t = (b * s + f) / e;
+  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-c / a, 0.f), 1.f); }
+  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((b - c) / a, 0.f), 1.f); }
+  c1 = p1 + s * d1;
+  c2 = p2 + t * d2;
+}
+
+// d . (a_k x (x - o_k)) for every joint k on body b's chain (k in 1..12), 0 elsewhere
+__device__ __forceinline__ float chain_term(const EnvSh& E, int b, int k, f3 x, f3 d) {
+  const int lo = b >= 7 ? 7 : 1;
+  const bool anc = b > 0 && k >= lo && k <= b && (k <= 6) == (b <= 6);
+  return anc ? dot(d, cross(ld3(E.a[k]), x - ld3(E.o[k]))) : 0.f;
+}
+
 }  // namespace
 
 // FIXED = asset.fix_base_link, a compile-time constant so the factorised size and every
-// floating-base branch resolve at compile time (no per-entry scalar branches in the Cholesky)
+// floating-base branch resolve at compile time
 template <bool FIXED>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_step(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
   __shared__ EnvSh shm[2];
@@ -359,6 +401,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const float dt = cfg->sim_dt;
   const float inv_dt = 1.0f / dt;
   constexpr bool fixed = FIXED;
+  constexpr int nf = fixed ? 12 : 18;  // factorised size (legs-first order: left leg, right leg, base)
   const float gz = cfg->gravity_z;
 
   // ---------------- prologue: actions (humanoid_env.py:624-635) + state load
@@ -386,8 +429,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   __syncthreads();
   const float scale0 = E.mass0 / M->mass[0];
-  // PD constants of this lane's joint staged in LDS for all substeps (one global load each per
-  // launch instead of per substep); the position target is constant over the policy step
+  // PD constants of this lane's joint staged in LDS for all substeps; the position target is
+  // constant over the policy step
   if (l < 12) {
     E.pd_kp[l] = cfg->kp[l];
     E.pd_kd[l] = cfg->kd[l];
@@ -399,17 +442,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   for (int sub = 0; sub < decimation; sub++) {
     // lane masks are rebuilt per substep (v_cmp) instead of living across the loop in SGPR pairs
     asm volatile("" : "+v"(l));
-    // ---- A1: torques (_compute_torques, humanoid_env.py:910-925), generalized velocity
+    // ---- A1: torques (_compute_torques, humanoid_env.py:910-925); implicit damping on the
+    // joints whose torque is not clipped: dt*kd joins M's diagonal (with the model armature)
     if (l < 12) {
-      float t = E.pd_kp[l] * (E.pd_tgt[l] - E.q[l]) - E.pd_kd[l] * E.qd[l];
-      E.tau[l] = fminf(fmaxf(t, -E.pd_lim[l]), E.pd_lim[l]);
+      const float t = E.pd_kp[l] * (E.pd_tgt[l] - E.q[l]) - E.pd_kd[l] * E.qd[l];
+      const float lim = E.pd_lim[l];
+      E.tau[l] = fminf(fmaxf(t, -lim), lim);
+      const bool sat = t < -lim || t > lim;
+      E.madd[l] = M->armature[l + 1] + (sat ? 0.f : dt * E.pd_kd[l]);
       E.nu[6 + l] = E.qd[l];
     }
     if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
     __syncthreads();
-    // ---- A2/A3: kinematics + RNEA forward
-    // one register-resident pass over the legs: kinematics (prefix scans), then the per-body
-    // forces and the backward recursions (suffix scans) — no barrier until the base totals
+    // ---- A2..A5: kinematics (prefix scans), per-body forces, backward recursions (suffix scans)
     const KinLane K = kin_scan(E, M, l, gz, true);
     rnea_scan(E, M, l, K, scale0);
     __syncthreads();
@@ -425,15 +470,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
       for (int i = 0; i < 6; i++) E.base_cJ[i] = E.cJ[0][i] + E.cJ[1][i] + E.cJ[7][i];
     }
+    for (int i = l; i < 18 * 20; i += 32) (&E.L[0][0])[i] = 0.f;
     __syncthreads();
-    for (int i = l; i < 18 * 20; i += 32) (&E.u.fac.M[0][0])[i] = 0.f;
-    __syncthreads();
-    // ---- A6/A7: base block (lane 0); joint columns of M (lanes 1..12)
+    // ---- A6/A7: base block (lane 0); joint columns of M (lanes 1..12), + armature + implicit damping
     if (l == 0) {
       const float m0 = E.base_cm;
       f3 s = ld3(E.base_cs);
       const float* J0 = E.base_cJ;
-      float (*A)[20] = E.u.fac.M;
+      float (*A)[20] = E.L;
       A[0][0] = A[1][1] = A[2][2] = m0;
       A[3][1] = -s.z; A[3][2] = s.y;
       A[4][0] = s.z;  A[4][2] = -s.x;
@@ -445,22 +489,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       f3 a = ld3(E.a[b]), o = ld3(E.o[b]);
       f3 cs = ld3(E.cs[b]);
       f3 F = cross(a, cs - E.cm[b] * o);
-      f3 L = symv(E.cJ[b], a) - cross(cs, cross(a, o));
-      float (*A)[20] = E.u.fac.M;
+      f3 Lm = symv(E.cJ[b], a) - cross(cs, cross(a, o));
+      float (*A)[20] = E.L;
       A[col][0] = F.x; A[col][1] = F.y; A[col][2] = F.z;
-      A[col][3] = L.x; A[col][4] = L.y; A[col][5] = L.z;
+      A[col][3] = Lm.x; A[col][4] = Lm.y; A[col][5] = Lm.z;
       const int first = b <= 6 ? 1 : 7;
-      for (int kb = b; kb >= first; kb--) A[col][5 + kb] = dot(ld3(E.a[kb]), L - cross(ld3(E.o[kb]), F));
-      A[col][col] += M->armature[b];
+      for (int kb = b; kb >= first; kb--) A[col][5 + kb] = dot(ld3(E.a[kb]), Lm - cross(ld3(E.o[kb]), F));
+      A[col][col] += E.madd[b - 1];
     }
     __syncthreads();
-    // ---- A8: Cholesky in registers, in the legs-first order [left leg, right leg, base]
-    // (new index i <-> dof o(i) = i < 12 ? 6 + i : i - 12).  M's arrow structure (each leg
-    // couples only to itself and the base) then gives L no left-right-leg block, so those
-    // columns are skipped.  Lane i holds row i; column j's entries L[k][j] reach the other rows
-    // by v_readlane (no LDS round trips, no barriers).  Fixed base: the base block (i >= 12) is
-    // dropped.  Entries right of a lane's diagonal are never read.
-    constexpr int nf = fixed ? 12 : 18;  // factorised size
+    // ---- A8: Cholesky in registers, legs-first order [left leg, right leg, base] (new index
+    // i <-> dof o(i) = i < 12 ? 6 + i : i - 12): M's arrow structure gives L no left-right-leg
+    // block, so those columns are skipped.  Lane i holds row i; each pivot column is broadcast
+    // through LDS (one write, half-wave broadcast reads; same-wave LDS accesses complete in order,
+    // so no barrier) and the rank-1 update is one FMA per trailing entry.  The right-hand side
+    // b = tau - h rides along as an extra column: g = L^-1 b falls out of the same loop.
     {
       float a[18];
       bool nonpd = false;
@@ -469,204 +512,214 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       for (int k = 0; k < 18; k++) {
         const int ok = k < 12 ? 6 + k : k - 12;
         // M holds the lower triangle in dof order (upper entries are zero)
-        a[k] = (l < 18) ? (ol >= ok ? E.u.fac.M[l < 18 ? ol : 0][ok] : E.u.fac.M[ok][l < 18 ? ol : 0]) : 0.f;
+        a[k] = (l < 18) ? (ol >= ok ? E.L[l < 18 ? ol : 0][ok] : E.L[ok][l < 18 ? ol : 0]) : 0.f;
       }
+      float bv = (l < 18) ? (ol >= 6 ? E.tau[(ol >= 6 ? ol : 6) - 6] : 0.f) - E.h[l < 18 ? ol : 0] : 0.f;
       asm volatile("" ::: "memory");
-      // column broadcast through LDS: every lane writes its (unscaled) column-j entry, then reads
-      // the pivot and the trailing entries back as half-wave broadcasts; the rank-1 update is then
-      // ONE FMA per trailing entry for both envs of the wave.  Same-wave LDS accesses complete in
-      // order, so no barrier.  Y (written only in A12) holds the scratch column.
-      float* colbuf = &E.Y[0][0];
 #pragma unroll
       for (int j = 0; j < nf; j++) {
-        if (l < 18) colbuf[l] = a[j];
-        const float d = colbuf[j];
+        if (l < 18) { E.colbuf[l] = a[j]; E.bbuf[l] = bv; }
+        const float d = E.colbuf[j];
+        const float bj = E.bbuf[j];
         nonpd |= !(d > 0.f);
-        const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));  // 1 ulp, see the readlane form
+        const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));  // 1 / L_jj (1 ulp)
         const float t = a[j] * (inv * inv);  // L[l][j] / L[j][j]
+        if (l == 0) { E.invd[j] = inv; E.gv[j] = bj * inv; }
         a[j] = (lane_opaque(l) >= j) ? a[j] * inv : a[j];
+        bv = (lane_opaque(l) > j) ? bv - t * bj : bv;  // b_l -= L[l][j] g_j
 #pragma unroll
         for (int k = j + 1; k < nf; k++) {
           if (j < 6 && k >= 6 && k < 12) continue;  // structural zero: left-leg pivot, right-leg row
-          a[k] -= t * colbuf[k];  // L[l][j] L[k][j] = (a_lj / d) a_kj
+          a[k] -= t * E.colbuf[k];  // L[l][j] L[k][j] = (a_lj / d) a_kj
         }
       }
       if (l < 18) {
 #pragma unroll
-        for (int k = 0; k < 18; k++) E.u.fac.M[l][k] = a[k];
-        // 1 / L_ll from the lane's own row (same-lane LDS write then read: no barrier needed)
-        E.u.fac.invd[l] = __builtin_amdgcn_rcpf(E.u.fac.M[l][l < 18 ? l : 0]);
+        for (int k = 0; k < 18; k++) E.L[l][k] = (k < nf && l < nf) ? a[k] : 0.f;
       }
       if (l == 0 && nonpd) E.bad = 1;
     }
     __syncthreads();
-    // ---- A9: explicit M^-1: lane i solves L L^T x = e_i in the legs-first order (skipping the
-    // structural zeros) and stores column i back in dof order
-    if (l < 18) {
-      float y[18];
-#pragma unroll
-      for (int k = 0; k < 18; k++) y[k] = 0.f;
-      if (l < nf) {
-        const float (*A)[20] = E.u.fac.M;
-#pragma unroll
-        for (int k = 0; k < 18; k++) {
-          if (k >= nf) continue;
-          float s = (k == l) ? 1.f : 0.f;
-#pragma unroll
-          for (int m = 0; m < k; m++) {
-            if (k >= 6 && k < 12 && m < 6) continue;
-            s -= A[k][m] * y[m];
-          }
-          y[k] = s * E.u.fac.invd[k];
-          __builtin_amdgcn_sched_barrier(0);  // keep the row's LDS loads next to their use
-        }
-#pragma unroll
-        for (int k = 17; k >= 0; k--) {
-          if (k >= nf) continue;
-          const float xk = y[k] * E.u.fac.invd[k];
-          y[k] = xk;
-#pragma unroll
-          for (int m = 0; m < k; m++) {
-            if (k >= 6 && k < 12 && m < 6) continue;
-            y[m] -= A[k][m] * xk;
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      const int ol = l < 12 ? 6 + l : l - 12;
-#pragma unroll
-      for (int k = 0; k < 18; k++) {
-        const int ok = k < 12 ? 6 + k : k - 12;
-        E.u.fac.Minv[ok][ol] = (k < nf && l < nf) ? y[k] : 0.f;
-      }
-    }
-    __syncthreads();
-    // ---- A10: unconstrained velocity nu* = nu + dt M^-1 (tau - h)
-    float nu_star = 0.f;
-    if (l < 18) {
-      float acc = 0.f;
-#pragma unroll
-      for (int k = 0; k < 18; k++) acc += E.u.fac.Minv[l][k] * ((k >= 6 ? E.tau[k - 6] : 0.f) - E.h[k]);
-      nu_star = E.nu[l] + dt * acc;
-    }
-    __syncthreads();
-    if (l < 18) E.nu[l] = nu_star;
-    // ---- A11: contact / limit detection and row allocation (whole contact triples first)
+    // ---- A9: contact detection (one candidate per lane, in priority order: ground candidates
+    // [0, num_leg_contacts), the leg-vs-leg capsule pairs, the remaining ground candidates),
+    // joint limits, and row allocation by ballot / popcount
     {
-      bool act_c = false, act_l = false;
-      f3 cx = mk(0, 0, 0), cn = mk(0, 0, 1);
-      float phi = 0.f, gapv = 0.f, sgnv = 1.f;
-      if (l < 16 && l < M->num_contacts && !fixed) {
-        const int b = M->contact_body[l];
-        cx = ld3(E.o[b]) + mv3(E.R[b], ld3(M->contact_pos[l]));
-        float hg;
-        ground(cfg, cx.x + E.root[0], cx.y + E.root[1], &hg, &cn);
-        phi = (cx.z + E.root[2] - hg) * cn.z;
-        act_c = phi < cfg->contact_offset;
-      } else if (l >= 16 && l < 28) {
-        const int j = l - 16;
-        const float glo = E.q[j] - M->lower[j + 1], ghi = M->upper[j + 1] - E.q[j];
+      const int nleg = M->num_leg_contacts, npair = M->num_pairs, nitems = M->num_contacts + npair;
+      bool act_c = false;
+      f3 cn = mk(0, 0, 1), xP = mk(0, 0, 0), xN = mk(0, 0, 0);
+      float phi = 0.f, mu = 0.f;
+      int bP = -1, bN = -1, lam_base = 0;
+      if (l < nitems) {
+        const bool is_pair = l >= nleg && l < nleg + npair;
+        if (!is_pair) {
+          const int c = l < nleg ? l : l - npair;
+          const int b = M->contact_body[c];
+          const f3 x = ld3(E.o[b]) + mv3(E.R[b], ld3(M->contact_pos[c]));
+          float hg;
+          ground(cfg, x.x + E.root[0], x.y + E.root[1], &hg, &cn);
+          const float r = M->contact_radius[c];
+          phi = (x.z + E.root[2] - hg) * cn.z - r;
+          xP = x - r * cn;
+          bP = b;
+          mu = 0.5f * (E.fric + cfg->ground_friction);
+          lam_base = 3 * c;
+          act_c = !fixed && phi < cfg->contact_offset;
+        } else {
+          const int p = l - nleg;
+          const int ca = M->pair[p][0], cb = M->pair[p][1];
+          const int ba = M->capsule_body[ca], bb = M->capsule_body[cb];
+          const f3 oa = ld3(E.o[ba]), ob = ld3(E.o[bb]);
+          f3 pa, pb;
+          seg_seg(oa + mv3(E.R[ba], ld3(M->capsule_p0[ca])), oa + mv3(E.R[ba], ld3(M->capsule_p1[ca])),
+                  ob + mv3(E.R[bb], ld3(M->capsule_p0[cb])), ob + mv3(E.R[bb], ld3(M->capsule_p1[cb])), pa, pb);
+          const f3 dv = pb - pa;
+          const float dist = sqrtf(dot(dv, dv));
+          cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);
+          const float ra = M->capsule_radius[ca], rb = M->capsule_radius[cb];
+          phi = dist - ra - rb;
+          xP = pb - rb * cn;
+          xN = pa + ra * cn;
+          bP = bb;
+          bN = ba;
+          mu = E.fric;
+          lam_base = LAM_PAIR + 3 * p;
+          act_c = phi < cfg->contact_offset;
+        }
+      }
+      bool act_l = false, has_f = false;
+      float gapv = 0.f, sgnv = 1.f, ffric = 0.f;
+      if (l < 12) {
+        const float glo = E.q[l] - M->lower[l + 1], ghi = M->upper[l + 1] - E.q[l];
         if (glo < 0.01f) { act_l = true; gapv = glo; sgnv = 1.f; }
         else if (ghi < 0.01f) { act_l = true; gapv = ghi; sgnv = -1.f; }
+        ffric = M->joint_friction[l + 1];
+        has_f = ffric > 0.f;
       }
-      const uint64_t bal_c = __ballot(act_c), bal_l = __ballot(act_l);
-      const uint32_t mc = (uint32_t)(bal_c >> (32 * half)) & 0xFFFFu;
-      const uint32_t ml = ((uint32_t)(bal_l >> (32 * half)) >> 16) & 0xFFFu;
-      const int nc = min(__popc(mc), RMAX / 3);
-      const int nrows = min(RMAX, 3 * nc + __popc(ml));
+      const uint32_t mc = (uint32_t)(__ballot(act_c) >> (32 * half));
+      const uint32_t ml = (uint32_t)(__ballot(act_l) >> (32 * half)) & 0xFFFu;
+      const uint32_t mf = (uint32_t)(__ballot(has_f) >> (32 * half)) & 0xFFFu;
+      const int npts = min(__popc(mc), MAX_PTS);
+      const int nfr = __popc(mf);
+      const int nrows = min(RMAX, 3 * npts + nfr + __popc(ml));
       const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
       if (l == 0) E.nrows = nrows;
-      if (l >= nrows) { E.rc[l].kind = 2; E.rc[l].tgt = 0.f; E.rc[l].invD = 0.f; E.rc[l].invD2 = 0.f; }
-      if (l < 16) {
-        const int rank = __popc(mc & ((1u << l) - 1u));
-        if (act_c && rank < nc) {
-          const int start = 3 * rank;
-          f3 t1 = mk(1, 0, 0) - cn.x * cn;
-          t1 = rsqrtf(dot(t1, t1)) * t1;
-          f3 t2 = cross(cn, t1);
-          const float tgt = phi >= 0.f ? -phi * inv_dt : fminf(-beta * phi * inv_dt, vmax);
-          for (int d = 0; d < 3; d++) {
-            const int r = start + d;
-            f3 dir = d == 0 ? cn : (d == 1 ? t1 : t2);
-            st3(E.rx[r], cx); st3(E.rd[r], dir);
-            E.rc[r].kind = d; E.rc[r].tgt = d == 0 ? tgt : 0.f;
-            E.rPt[r] = l; E.rBody[r] = M->contact_body[l];
-            E.rLam[r] = E.lamst[l * 3 + d];
-          }
-        } else if (l < HG_NC) {
-          E.lamst[l * 3 + 0] = E.lamst[l * 3 + 1] = E.lamst[l * 3 + 2] = 0.f;
+      // group-level fields and empty slots
+      if (l < NGRP) { E.grp[l].contact = l < npts ? 1 : 0; E.grp[l].mu = 0.f; }
+      for (int r = l; r < 3 * NGRP; r += 32) {
+        if (r >= nrows) {
+          const int g = r / 3, k = r % 3;
+          E.grp[g].tgt[k] = 0.f; E.grp[g].lo[k] = 0.f; E.grp[g].hi[k] = 0.f;
         }
-      } else if (l < 28) {
-        const int j = l - 16;
-        const int r = 3 * nc + __popc(ml & ((1u << j) - 1u));
-        if (act_l && r < RMAX) {
-          E.rc[r].kind = 3; E.rc[r].tgt = gapv >= 0.f ? -gapv * inv_dt : fminf(-beta * gapv * inv_dt, vmax);
-          E.rPt[r] = j; E.rBody[r] = -1;
-          E.rd[r][0] = sgnv;
-          E.rLam[r] = E.lamst[HG_NC * 3 + j];
+      }
+      const int rank = __popc(mc & ((1u << l) - 1u));
+      if (l < nitems) {
+        if (act_c && rank < npts) {
+          const float tgt = phi >= 0.f ? -phi * inv_dt : fminf(-beta * phi * inv_dt, vmax);
+          // tangent basis (reference axis x, or y when the normal is close to x)
+          const f3 ref = fabsf(cn.x) < 0.9f ? mk(1, 0, 0) : mk(0, 1, 0);
+          f3 t1 = ref - dot(ref, cn) * cn;
+          t1 = rsqrtf(dot(t1, t1)) * t1;
+          const f3 t2 = cross(cn, t1);
+          E.grp[rank].mu = mu;
+#pragma unroll
+          for (int d = 0; d < 3; d++) {
+            const int r = 3 * rank + d;
+            const f3 dir = d == 0 ? cn : (d == 1 ? t1 : t2);
+            st3(E.rd[r], dir);
+            st3(E.u.rg.xP[r], xP);
+            st3(E.u.rg.xN[r], xN);
+            E.rbP[r] = bP; E.rbN[r] = bN;
+            E.rlam[r] = lam_base + d;
+            E.rLam[r] = E.lamst[lam_base + d];
+            E.grp[rank].tgt[d] = d == 0 ? tgt : 0.f;
+            E.grp[rank].lo[d] = d == 0 ? 0.f : -BIG;
+            E.grp[rank].hi[d] = BIG;
+          }
         } else {
-          E.lamst[HG_NC * 3 + j] = 0.f;
+          E.lamst[lam_base + 0] = E.lamst[lam_base + 1] = E.lamst[lam_base + 2] = 0.f;
+        }
+      }
+      if (l < 12) {
+        if (has_f) {  // joint friction: |lambda| <= f dt
+          const int r = 3 * npts + __popc(mf & ((1u << l) - 1u));
+          E.rd[r][0] = 1.f; E.rbP[r] = -1 - l; E.rbN[r] = -1;
+          E.rlam[r] = LAM_FRIC + l;
+          E.rLam[r] = E.lamst[LAM_FRIC + l];
+          E.grp[r / 3].tgt[r % 3] = 0.f; E.grp[r / 3].lo[r % 3] = -ffric * dt; E.grp[r / 3].hi[r % 3] = ffric * dt;
+        } else {
+          E.lamst[LAM_FRIC + l] = 0.f;
+        }
+        const int r = 3 * npts + nfr + __popc(ml & ((1u << l) - 1u));
+        if (act_l && r < RMAX) {
+          E.rd[r][0] = sgnv; E.rbP[r] = -1 - l; E.rbN[r] = -1;
+          E.rlam[r] = LAM_LIM + l;
+          E.rLam[r] = E.lamst[LAM_LIM + l];
+          E.grp[r / 3].tgt[r % 3] = gapv >= 0.f ? -gapv * inv_dt : fminf(-beta * gapv * inv_dt, vmax);
+          E.grp[r / 3].lo[r % 3] = 0.f; E.grp[r / 3].hi[r % 3] = BIG;
+        } else {
+          E.lamst[LAM_LIM + l] = 0.f;
         }
       }
     }
     __syncthreads();
     const int nrows = E.nrows;
-    // ---- A12: Jacobian row (registers), Y = M^-1 J^T, 1/D, J nu*
-    float J[18];
-#pragma unroll
-    for (int i = 0; i < 18; i++) J[i] = 0.f;
-    float vrow = 0.f;
     const bool own = l < nrows;
-    if (own) {
-      const int kind = E.rc[l].kind;
-      if (kind == 3) {
-        const int j = E.rPt[l];
+    // ---- A10: Jacobian row (registers, dof order), z = L^-1 J^T (legs-first), row velocity
+    // J nu* = J nu + dt z . g
+    float z[18];
+    float v0 = 0.f;
+    {
+      float J[18];
 #pragma unroll
-        for (int jj = 0; jj < 12; jj++) J[6 + jj] = (jj == j) ? E.rd[l][0] : 0.f;
-      } else {
-        const f3 x = ld3(E.rx[l]), d = ld3(E.rd[l]);
-        const int b = E.rBody[l];
-        J[0] = d.x; J[1] = d.y; J[2] = d.z;
-        const f3 xd = cross(x, d);
-        J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
-        const int lo = b >= 7 ? 7 : 1;
+      for (int i = 0; i < 18; i++) J[i] = 0.f;
+      if (own) {
+        const int bP = E.rbP[l], bN = E.rbN[l];
+        if (bP < 0) {  // joint row (friction / limit): sign * e_dof
+          const int j = -1 - bP;
 #pragma unroll
-        for (int k = 1; k <= 12; k++) {
-          const bool anc = b != 0 && k >= lo && k <= b && (k <= 6) == (b <= 6);
-          J[5 + k] = anc ? dot(d, cross(ld3(E.a[k]), x - ld3(E.o[k]))) : 0.f;
+          for (int jj = 0; jj < 12; jj++) J[6 + jj] = (jj == j) ? E.rd[l][0] : 0.f;
+        } else {       // contact row: J = J_bP(xP) d - J_bN(xN) d
+          const f3 d = ld3(E.rd[l]), xp = ld3(E.u.rg.xP[l]), xn = ld3(E.u.rg.xN[l]);
+          const bool pair2 = bN >= 0;
+          J[0] = pair2 ? 0.f : d.x; J[1] = pair2 ? 0.f : d.y; J[2] = pair2 ? 0.f : d.z;
+          const f3 xd = cross(xp, d) - (pair2 ? cross(xn, d) : mk(0, 0, 0));
+          J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
+#pragma unroll
+          for (int k = 1; k <= 12; k++) J[5 + k] = chain_term(E, bP, k, xp, d) - chain_term(E, bN, k, xn, d);
         }
       }
+#pragma unroll
+      for (int i = 0; i < 18; i++) v0 += J[i] * E.nu[i];
+      // forward substitution with L broadcast from LDS (legs-first order; arrow structure)
+#pragma unroll
+      for (int k = 0; k < 18; k++) {
+        if (k >= nf) { z[k] = 0.f; continue; }
+        float s = J[k < 12 ? 6 + k : k - 12];
+#pragma unroll
+        for (int m = 0; m < k; m++) {
+          if (k >= 6 && k < 12 && m < 6) continue;
+          s -= E.L[k][m] * z[m];
+        }
+        z[k] = s * E.invd[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 18; k++) v0 += dt * (z[k] * E.gv[k]);
     }
-    // ---- Y = M^-1 J^T and W = J Y on the matrix cores (v_mfma_f32_32x32x2_f32), one 32x32
-    // product per env.  MFMA operand i/kk = lane%32 / lane/32, so the wave's two envs are
-    // interleaved with v_permlane32_swap: swap(X, Z) -> (X.lo|Z.lo, X.hi|Z.hi).
-    //   Y_h (dof x row): 9 k-pairs (2p, 2p+1); A = M^-1_h (rows >= 18 zero) read from LDS,
-    //   B = J_h^T.  D layout: lane (kk, n), vgpr v holds Y_h[8(v/4) + 4kk + v%4][n].
-    //   W_h = J_h Y_h: contraction pairs follow that layout, k = 8(q/4) + q%4 (+4 for kk = 1),
-    //   so Y's accumulators are the B operands as they stand.
-    f32x16 dy0 = {0}, dy1 = {0}, dw0 = {0}, dw1 = {0};
+    __syncthreads();  // every lane's row points are read before Z overwrites them
+#pragma unroll
+    for (int k = 0; k < 18; k++) E.u.Z[l][k] = z[k];
+    // ---- A11: W = Z^T Z on the matrix cores (v_mfma_f32_32x32x2f32).  MFMA operand i/kk =
+    // lane%32 / lane/32, so the wave's two envs are interleaved with v_permlane32_swap:
+    // swap(X, Y) -> (X.lo|Y.lo, X.hi|Y.hi) is env 0's / env 1's [32 rows x 2 k] operand, and the
+    // same register is the B operand (B[kk][n] = z_n[k]).  D layout: lane (n, kk), vgpr v holds
+    // W[8(v/4) + 4kk + v%4][n].
+    f32x16 dw0 = {0}, dw1 = {0};
 #pragma unroll
     for (int p = 0; p < 9; p++) {
-      const float am0 = (l < 18) ? shm[0].u.fac.Minv[l < 18 ? l : 0][2 * p + half] : 0.f;
-      const float am1 = (l < 18) ? shm[1].u.fac.Minv[l < 18 ? l : 0][2 * p + half] : 0.f;
-      float b0, b1;
-      swap32(J[2 * p], J[2 * p + 1], b0, b1);
-      dy0 = __builtin_amdgcn_mfma_f32_32x32x2f32(am0, b0, dy0, 0, 0, 0);
-      dy1 = __builtin_amdgcn_mfma_f32_32x32x2f32(am1, b1, dy1, 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 10; q++) {
-      const int klo = 8 * (q / 4) + q % 4, khi = klo + 4;
       float a0, a1;
-      swap32(J[klo], khi < 18 ? J[khi < 18 ? khi : 0] : 0.f, a0, a1);
-      dw0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, dy0[q], dw0, 0, 0, 0);
-      dw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, dy1[q], dw1, 0, 0, 0);
-    }
-    // Y rows to LDS for the velocity update (A15): this lane holds Y_h[i][l] for its 10 dofs
-#pragma unroll
-    for (int v = 0; v < 10; v++) {
-      const int i = 8 * (v / 4) + 4 * half + v % 4;
-      if (i < 18) { shm[0].Y[l][i] = dy0[v]; shm[1].Y[l][i] = dy1[v]; }
+      swap32(z[2 * p], z[2 * p + 1], a0, a1);
+      dw0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a0, dw0, 0, 0, 0);
+      dw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, a1, dw1, 0, 0, 0);
     }
     // gather each env's W column l into its own lanes: wA[v] = W[8(v/4) + v%4][l],
     // wB[v] = W[8(v/4) + 4 + v%4][l]  (W symmetric: column l == row l)
@@ -676,101 +729,124 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     float wrow[RMAX];
 #pragma unroll
     for (int m = 0; m < RMAX; m++) wrow[m] = (m % 8 < 4) ? wA[4 * (m / 8) + m % 8] : wB[4 * (m / 8) + m % 8 - 4];
-    if (own) {
-      float D = 0.f;
+    // ---- A12: group constants (1/W_rr and the in-group couplings), warm-started row velocities
+    {
+      float Dd = 0.f, W1 = 0.f, W2 = 0.f;  // W[l][l], W[l][l-1], W[l][l-2]
 #pragma unroll
-      for (int m = 0; m < RMAX; m++) D = (l == m) ? wrow[m] : D;
-      float v0 = 0.f;
-#pragma unroll
-      for (int i = 0; i < 18; i++) v0 += J[i] * E.nu[i];
+      for (int m = 0; m < RMAX; m++) {
+        Dd = (l == m) ? wrow[m] : Dd;
+        W1 = (l == m + 1) ? wrow[m] : W1;
+        W2 = (l == m + 2) ? wrow[m] : W2;
+      }
+      const int g = l / 3, k = l % 3;
+      E.grp[g].invD[k] = own ? __builtin_amdgcn_rcpf(Dd) : 0.f;
+      if (k == 1) E.grp[g].Wba = W1;
+      if (k == 2) { E.grp[g].Wca = W2; E.grp[g].Wcb = W1; }
+      if (l == 31) { E.grp[10].invD[2] = 0.f; E.grp[10].Wca = 0.f; E.grp[10].Wcb = 0.f; }  // virtual slot 32
+      float v = v0;
 #pragma unroll
       for (int m = 0; m < RMAX; m++)
-        if (m < nrows) v0 += wrow[m] * E.rLam[m];
-      E.rc[l].invD = __builtin_amdgcn_rcpf(D);
-      vrow = v0;
+        if (m < nrows) v += wrow[m] * E.rLam[m];
+      v0 = own ? v : 0.f;
     }
     __syncthreads();
-    if (own && E.rc[l].kind == 1) E.rc[l].invD2 = E.rc[l + 1].invD;
-    // rows that are a no-op in BOTH envs of the wave (tangent partner rows, unused rows) are
-    // skipped by a scalar branch: with contacts allocated first as triples they line up
-    const uint64_t live_b = __ballot(own && E.rc[l].kind != 2);
-    const uint32_t live_rows = __builtin_amdgcn_readfirstlane((uint32_t)live_b | (uint32_t)(live_b >> 32));
-    __syncthreads();
-    // ---- A14: projected Gauss-Seidel, rows in order (normal, then its tangent pair).  The row
-    // velocity v_r lives in lane r and is read with v_readlane; the impulses are replicated: every
-    // lane of an env holds all 32 of its env's impulses in registers (uniform per half-wave), so
-    // reading and updating lambda_r costs no cross-lane traffic.  The update is uniform over the
-    // env's 32 lanes and branch-free (both halves of the wave run it whatever their row kinds):
-    //   normal / limit row:  lambda <- max(lambda + (tgt - v) / D, 0)
-    //   tangent pair (r, r+1): unconstrained 2-D step, projected onto the disc mu * lambda_n,
-    //   lambda_n being the normal impulse updated one row earlier
-    //   kind 2 / unused rows: no-op (rc.kind = 2 for rows >= nrows)
+    // ---- A13: projected Gauss-Seidel over the 3-slot groups.  The impulses are replicated: every
+    // lane of an env holds all 32 of its env's impulses (uniform per half-wave); the row velocity
+    // v_r lives in lane r and is read with scalar v_readlane pairs.  Per group (a, b, c):
+    //   a: lambda_a <- clamp(lambda_a + (tgt_a - v_a) / W_aa, lo_a, hi_a)   (normal / single row)
+    //   contact: the tangent pair's unconstrained steps from v_b + W_ba dl_a, v_c + W_ca dl_a,
+    //            projected onto the disc mu * lambda_a (as the oracle: both from the same nu)
+    //   singles: b from v_b + W_ba dl_a, then c from v_c + W_ca dl_a + W_cb dl_b
+    // then every row velocity takes the group's three updates (one FMA each).  Branch-free over
+    // the group kinds; groups empty in both envs of the wave are skipped (scalar branch).
     {
       float lam[RMAX];
 #pragma unroll
       for (int m = 0; m < RMAX; m++) lam[m] = m < nrows ? E.rLam[m] : 0.f;
-      const float mu = 0.5f * (E.fric + cfg->ground_friction);
+      float vrow = v0;
+      const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;
       const int npgs = cfg->pgs_iterations;
       for (int it = 0; it < npgs; it++) {
-        float prev_ln = 0.f;
 #pragma unroll
-        for (int r = 0; r < RMAX; r++) {
-          if (live_rows & (1u << r)) {
-          const RowC c = E.rc[r];
-          const float vr = RL(vrow, r), lr = lam[r];
-          const bool isF = c.kind == 1, isN = c.kind == 0 || c.kind == 3;
-          const float ln = fmaxf(lr + (c.tgt - vr) * c.invD, 0.f);
-          float dl0 = isN ? ln - lr : 0.f;
-          if (r + 1 < RMAX) {
-            const float vr2 = RL(vrow, r + 1), lr2 = lam[r + 1];
-            float l1 = lr - vr * c.invD, l2 = lr2 - vr2 * c.invD2;
-            const float lim = mu * prev_ln, nn2 = l1 * l1 + l2 * l2;
+        for (int g = 0; g < NGRP; g++) {
+          if (g < ng) {
+            const int ra = 3 * g, rb = 3 * g + 1, rc = 3 * g + 2;
+            const GroupC& G = E.grp[g];
+            const float va = RL(vrow, ra), vb = RL(vrow, rb);
+            const float vc = rc < RMAX ? RL(vrow, rc < RMAX ? rc : 0) : 0.f;
+            const float la = lam[ra], lb = lam[rb], lc = rc < RMAX ? lam[rc < RMAX ? rc : 0] : 0.f;
+            const float na = fminf(fmaxf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0]), G.hi[0]);
+            const float da = na - la;
+            const float vb1 = vb + G.Wba * da, vc1 = vc + G.Wca * da;
+            // contact: tangent pair on the friction disc
+            const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
+            const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
             const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
-            dl0 = isF ? l1 * sc - lr : dl0;
-            const float dl1 = isF ? l2 * sc - lr2 : 0.f;
-            vrow += wrow[r] * dl0 + wrow[r + 1] * dl1;
-            lam[r + 1] += dl1;
-          } else {
-            vrow += wrow[r] * dl0;
-          }
-          lam[r] += dl0;
-          prev_ln = isN ? ln : prev_ln;
+            // single rows in sequence
+            const float nbs = fminf(fmaxf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1]), G.hi[1]);
+            const float dbs = nbs - lb;
+            const float vc2 = vc1 + G.Wcb * dbs;
+            const float ncs = fminf(fmaxf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2]), G.hi[2]);
+            const bool ct = G.contact != 0;
+            const float db = ct ? l1 * sc - lb : dbs;
+            const float dc = ct ? l2 * sc - lc : ncs - lc;
+            if (rc < RMAX) {
+              vrow += wrow[ra] * da + wrow[rb] * db + wrow[rc < RMAX ? rc : 0] * dc;
+              lam[rc < RMAX ? rc : 0] += dc;
+            } else {
+              vrow += wrow[ra] * da + wrow[rb] * db;
+            }
+            lam[ra] += da;
+            lam[rb] += db;
           }
         }
       }
-      // ---- A15: nu = nu* + Y^T lambda; contact forces; warm-start store
+      // ---- A14: nu_new = nu + L^-T (dt g + Z^T lambda): lanes = dofs (legs-first order k)
+      float y = 0.f;
+      if (l < nf) {
+        float u = dt * E.gv[l];
+#pragma unroll
+        for (int m = 0; m < RMAX; m++) u += E.u.Z[m][l] * lam[m];
+        y = u;
+      }
       if (l == 0) {
 #pragma unroll
-        for (int m = 0; m < RMAX; m++)
-          if (m < nrows) E.rLam[m] = lam[m];
+        for (int m = 0; m < RMAX; m++) E.rLam[m] = lam[m];
       }
-    }
-    for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
-    __syncthreads();
-    const float mylam = own ? E.rLam[l] : 0.f;
-    float nu_new = 0.f;
-    if (l < 18) {
-      float s = E.nu[l];
-      for (int r = 0; r < nrows; r++) s += E.Y[r][l] * E.rLam[r];
-      nu_new = s;
-    }
-    if (own) {
-      const int kind = E.rc[l].kind;
-      if (kind == 3) {
-        E.lamst[HG_NC * 3 + E.rPt[l]] = mylam;
-      } else {
-        E.lamst[E.rPt[l] * 3 + kind] = mylam;
-        const int b = E.rBody[l];
-        const float s = mylam * inv_dt;
-        atomicAdd(&E.cf[b][0], E.rd[l][0] * s);
-        atomicAdd(&E.cf[b][1], E.rd[l][1] * s);
-        atomicAdd(&E.cf[b][2], E.rd[l][2] * s);
+#pragma unroll
+      for (int j = nf - 1; j >= 0; j--) {
+        const float xj = RL(y, j) * E.invd[j];
+        const int lo = (j >= 6 && j < 12) ? 6 : 0;  // a right-leg column has no left-leg rows
+        y = (l == j) ? xj : ((l >= lo && l < j) ? y - E.L[j][l < 18 ? l : 0] * xj : y);
       }
+      __syncthreads();
+      float nu_new = 0.f;
+      const int od = l < 12 ? 6 + l : l - 12;
+      if (l < 18) nu_new = E.nu[l < 18 ? od : 0] + (l < nf ? y : 0.f);
+      // contact forces (net per body, world frame, last substep) and warm-start store
+      for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
+      const float mylam = own ? E.rLam[l] : 0.f;
+      const bool fin = (l >= 18) || isfinite(nu_new);
+      if ((uint32_t)(__ballot(!fin) >> (32 * half)) != 0u && l == 0) E.bad = 1;
+      __syncthreads();
+      if (own) {
+        E.lamst[E.rlam[l]] = mylam;
+        const int bP = E.rbP[l];
+        if (bP >= 0) {
+          const int bN = E.rbN[l];
+          const float s = mylam * inv_dt;
+          atomicAdd(&E.cf[bP][0], E.rd[l][0] * s);
+          atomicAdd(&E.cf[bP][1], E.rd[l][1] * s);
+          atomicAdd(&E.cf[bP][2], E.rd[l][2] * s);
+          if (bN >= 0) {
+            atomicAdd(&E.cf[bN][0], -E.rd[l][0] * s);
+            atomicAdd(&E.cf[bN][1], -E.rd[l][1] * s);
+            atomicAdd(&E.cf[bN][2], -E.rd[l][2] * s);
+          }
+        }
+      }
+      if (l < 18) E.nu[od] = nu_new;
     }
-    const bool fin = (l >= 18) || isfinite(nu_new);
-    if ((uint32_t)(__ballot(!fin) >> (32 * half)) != 0u && l == 0) E.bad = 1;
-    __syncthreads();
-    if (l < 18) E.nu[l] = nu_new;
     __syncthreads();
     // ---- A16: integrate (semi-implicit Euler; exact quaternion exponential)
     if (l < 12) {
@@ -791,10 +867,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           const float dq0 = wx * s, dq1 = wy * s, dq2 = wz * s, dq3 = ch;
           const float x = dq3 * Q[0] + dq0 * Q[3] + dq1 * Q[2] - dq2 * Q[1];
           const float y = dq3 * Q[1] - dq0 * Q[2] + dq1 * Q[3] + dq2 * Q[0];
-          const float z = dq3 * Q[2] + dq0 * Q[1] - dq1 * Q[0] + dq2 * Q[3];
+          const float zq = dq3 * Q[2] + dq0 * Q[1] - dq1 * Q[0] + dq2 * Q[3];
           const float w = dq3 * Q[3] - dq0 * Q[0] - dq1 * Q[1] - dq2 * Q[2];
-          const float inv = rsqrtf(x * x + y * y + z * z + w * w);
-          Q[0] = x * inv; Q[1] = y * inv; Q[2] = z * inv; Q[3] = w * inv;
+          const float inv = rsqrtf(x * x + y * y + zq * zq + w * w);
+          Q[0] = x * inv; Q[1] = y * inv; Q[2] = zq * inv; Q[3] = w * inv;
         }
       } else {
         for (int i = 7; i < 13; i++) E.root[i] = 0.f;
@@ -812,8 +888,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   if (cfg->add_noise && l < 12 && valid) {
     float z4[4];
     normals4(rng4(cfg, e, step_counter + 1, l, RNG_OBS_NOISE), z4);
-    // per-env rows [e][48]: lanes 0..11 of the wave's two envs store 384 contiguous bytes (whole
-    // cache lines; the former [48][np] columns were 8-byte pieces the L2 fetched lines for)
+    // per-env rows [e][48]: lanes 0..11 of the wave's two envs store 384 contiguous bytes
     *reinterpret_cast<float4*>(S.obs_noise + (size_t)e * 48 + 4 * l) = make_float4(z4[0], z4[1], z4[2], z4[3]);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *S.noise_counter = step_counter + 1;
@@ -865,7 +940,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 }
 
 extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
-                               hipStream_t stream) {
+                              hipStream_t stream) {
   const int grid = (S->n + 1) / 2;
   if (fixed_base)
     hipLaunchKernelGGL(k_step<true>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);

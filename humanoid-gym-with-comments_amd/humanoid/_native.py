@@ -18,8 +18,11 @@ MODEL_PATH = os.path.join(PKG_ROOT, "model", "xbotl_model.json")
 
 HG_MAX_BODIES = 16
 HG_MAX_DOF = 12
-HG_MAX_CONTACTS = 16
+HG_MAX_CONTACTS = 24
+HG_MAX_CAPSULES = 8
+HG_MAX_PAIRS = 8
 HG_NUM_REWARDS = 22
+HG_LAMW = HG_MAX_CONTACTS * 3 + HG_MAX_PAIRS * 3 + 2 * HG_MAX_DOF
 
 f32 = ctypes.c_float
 i32 = ctypes.c_int32
@@ -28,12 +31,17 @@ i32 = ctypes.c_int32
 class HgModel(ctypes.Structure):
     _fields_ = [
         ("num_bodies", i32), ("num_dof", i32), ("num_contacts", i32), ("num_foot_contacts", i32),
+        ("num_leg_contacts", i32), ("num_capsules", i32), ("num_pairs", i32), ("_pad", i32),
         ("parent", i32 * HG_MAX_BODIES), ("contact_body", i32 * HG_MAX_CONTACTS),
+        ("capsule_body", i32 * HG_MAX_CAPSULES), ("pair", (i32 * 2) * HG_MAX_PAIRS),
         ("joint_pos", (f32 * 3) * HG_MAX_BODIES), ("joint_rot", (f32 * 9) * HG_MAX_BODIES),
         ("axis", (f32 * 3) * HG_MAX_BODIES), ("mass", f32 * HG_MAX_BODIES),
         ("com", (f32 * 3) * HG_MAX_BODIES), ("inertia", (f32 * 6) * HG_MAX_BODIES),
         ("armature", f32 * HG_MAX_BODIES), ("lower", f32 * HG_MAX_BODIES), ("upper", f32 * HG_MAX_BODIES),
-        ("contact_pos", (f32 * 3) * HG_MAX_CONTACTS),
+        ("joint_friction", f32 * HG_MAX_BODIES),
+        ("contact_pos", (f32 * 3) * HG_MAX_CONTACTS), ("contact_radius", f32 * HG_MAX_CONTACTS),
+        ("capsule_p0", (f32 * 3) * HG_MAX_CAPSULES), ("capsule_p1", (f32 * 3) * HG_MAX_CAPSULES),
+        ("capsule_radius", f32 * HG_MAX_CAPSULES),
     ]
 
 
@@ -212,12 +220,14 @@ def ptr(t):
 # ------------------------------------------------------------------------------------------------
 # model table
 # ------------------------------------------------------------------------------------------------
-def load_model(path=MODEL_PATH, armature=0.01):
+def load_model(path=MODEL_PATH, armature=0.0, joint_friction=True, self_collisions=True):
     """Build an HgModel from model/xbotl_model.json (output of tools/urdf_compile.py).
 
-    armature: BUILD-DEFINED 0.01 kg m^2 per leg joint, from the robot's own MJCF
-    (resources/robots/XBot/mjcf/XBot-L.xml:37-39 `leg_joint_param armature=0.01`); the Isaac Gym
-    asset option is 0 (humanoid_config.py:114) — see DESIGN.md §Physics for why.
+    armature: joint-space inertia added to every leg joint; the Isaac Gym asset option is 0
+    (humanoid_config.py:118), which the simulator runs stably by treating the PD damping term
+    implicitly.  0.01 kg m^2 is the robot's MJCF value (XBot-L.xml:37-39).
+    joint_friction: apply the URDF's joint friction (0.1 N m on the ankles, XBot-L.urdf:1675-1677).
+    self_collisions: leg-vs-leg capsule pairs (asset.self_collisions = 0 enables them, :103).
     """
     with open(path) as f:
         js = json.load(f)
@@ -243,16 +253,35 @@ def load_model(path=MODEL_PATH, armature=0.01):
             m.lower[b] = j["lower"]
             m.upper[b] = j["upper"]
             m.armature[b] = armature
+            m.joint_friction[b] = j.get("friction", 0.0) if joint_friction else 0.0
         else:
             for i in range(9):
                 m.joint_rot[b][i] = 1.0 if i in (0, 4, 8) else 0.0
     cs = js["contacts"]
+    if len(cs) > HG_MAX_CONTACTS:
+        raise ValueError("too many contact candidates")
     m.num_contacts = len(cs)
-    m.num_foot_contacts = sum(1 for c in cs if c["body"] != 0)
+    m.num_foot_contacts = sum(1 for c in cs if bodies[c["body"]]["name"].endswith("ankle_roll_link"))
+    m.num_leg_contacts = js.get("num_leg_contacts", m.num_foot_contacts)
     for c, cd in enumerate(cs):
         m.contact_body[c] = cd["body"]
+        m.contact_radius[c] = cd.get("radius", 0.0)
         for i in range(3):
             m.contact_pos[c][i] = cd["pos"][i]
+    caps = js.get("capsules", [])
+    m.num_capsules = len(caps)
+    for k, cd in enumerate(caps):
+        m.capsule_body[k] = cd["body"]
+        m.capsule_radius[k] = cd["radius"]
+        for i in range(3):
+            m.capsule_p0[k][i] = cd["p0"][i]
+            m.capsule_p1[k][i] = cd["p1"][i]
+    pairs = js.get("pairs", []) if self_collisions else []
+    if len(pairs) > HG_MAX_PAIRS:
+        raise ValueError("too many self-collision pairs")
+    m.num_pairs = len(pairs)
+    for p, (a, b) in enumerate(pairs):
+        m.pair[p][0], m.pair[p][1] = a, b
     return m, js
 
 

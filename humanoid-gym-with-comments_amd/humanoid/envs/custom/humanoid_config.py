@@ -143,7 +143,11 @@ class XBotLCfg(BaseConfig):
             # physx.num_position_iterations + physx.num_velocity_iterations (4 + 1)
             pgs_iterations = None
             baumgarte = 0.2            # fraction of penetration corrected per substep
-            armature = 0.01            # kg m^2 per leg joint (XBot-L.xml:37-39)
+            # joint-space armature: the asset's 0 (asset.armature, humanoid_config.py:118 of the
+            # reference); the PD damping term is integrated implicitly, which keeps kd = 10 on
+            # the light foot stable at dt = 1 ms (0.01 = the MJCF's value, XBot-L.xml:37-39)
+            armature = 0.0
+            joint_friction = True      # URDF joint friction: 0.1 N m on the ankles (XBot-L.urdf:1675-1677)
 
     class domain_rand:
         randomize_friction = True

@@ -183,7 +183,9 @@ class XBotLFreeEnv(BaseTask):
         (replaces create_sim/_create_envs, humanoid_env.py:333-524)."""
         self.up_axis_idx = 2
         self.hg = N.lib()
-        model, js = N.load_model(armature=self.cfg.sim.hg.armature)
+        hgc = self.cfg.sim.hg
+        model, js = N.load_model(armature=hgc.armature, joint_friction=getattr(hgc, "joint_friction", True),
+                                 self_collisions=self.cfg.asset.self_collisions == 0)
         self._model, self._model_js = model, js
         mesh = self.cfg.terrain.mesh_type
         hf_ptr, hf_shape = None, (0, 0)

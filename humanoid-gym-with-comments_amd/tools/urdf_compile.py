@@ -12,8 +12,19 @@ What it does
     transforms and merging mass / COM / inertia with the parallel-axis theorem;
   * emits bodies in Isaac Gym's depth-first order (base, left leg 6, right leg 6), so
     ``feet = [6, 12]`` and ``knees = [4, 10]`` as in SURVEY App. A;
-  * derives contact candidate points: the 4 sole corners of each ``*_ankle_roll_link`` STL hull
-    (bottom plane y = -0.056 in the link frame) and the 8 corners of the base-link collision box.
+  * derives the collision model (BUILD-DEFINED fits of the URDF collision meshes, which PhysX
+    would collide as convex hulls):
+      - ground contact candidates, in priority order: the 4 sole corners of each
+        ``*_ankle_roll_link`` hull (points, bottom plane y = -0.056 in the link frame); the two end
+        spheres of the thigh (``*_leg_pitch_link``) and shin (``*_knee_link``) capsules; the 8
+        corners of the base-link collision box;
+      - capsules (principal axis of the hull, radius = mean transverse half-extent, segment = the
+        axial extent shrunk by the radius) for the thigh, shin and foot of each leg;
+      - self-collision pairs (self_collisions = 0 enables them, humanoid_config.py:103): every
+        left-leg capsule against every right-leg capsule except foot-thigh, with the contact
+        normal from the left capsule to the right one;
+  * records each joint's URDF ``dynamics friction`` (0.1 N m on the four ankle joints), which the
+    simulator applies as a Coulomb friction bound on the joint.
 
 Usage:  python tools/urdf_compile.py /root/reference/resources/robots/XBot [out.json]
 """
@@ -129,7 +140,14 @@ def compile_urdf(robot_dir):
                 damping=float(dyn.get("damping", 0)) if dyn is not None else 0.0)
         out_bodies.append(body)
 
-    # contact candidates
+    # collision model: capsules per leg link, ground candidates, self-collision pairs
+    index = {b["name"]: bi for bi, b in enumerate(out_bodies)}
+    capsules = []
+    for side in ("left", "right"):
+        for part in ("leg_pitch", "knee", "ankle_roll"):
+            name = f"{side}_{part}_link"
+            capsules.append(dict(body=index[name], part=part, side=side,
+                                 **fit_capsule(load_stl(os.path.join(robot_dir, "meshes", name + ".STL")))))
     contacts = []
     for bi, b in enumerate(out_bodies):
         if b["name"].endswith("ankle_roll_link"):
@@ -139,7 +157,20 @@ def compile_urdf(robot_dir):
             x0, x1 = sole[:, 0].min(), sole[:, 0].max()
             z0, z1 = sole[:, 2].min(), sole[:, 2].max()
             for (x, z) in [(x0, z0), (x1, z0), (x0, z1), (x1, z1)]:
-                contacts.append(dict(body=bi, pos=[float(x), float(ymin), float(z)]))
+                contacts.append(dict(body=bi, pos=[float(x), float(ymin), float(z)], radius=0.0))
+    for part in ("knee", "leg_pitch"):  # shin, then thigh end spheres
+        for c in capsules:
+            if c["part"] == part:
+                for end in ("p0", "p1"):
+                    contacts.append(dict(body=c["body"], pos=c[end], radius=c["radius"]))
+    num_leg_contacts = len(contacts)
+    pairs = []
+    for a, ca in enumerate(capsules):
+        for b, cb in enumerate(capsules):
+            if ca["side"] == "left" and cb["side"] == "right":
+                if {ca["part"], cb["part"]} == {"leg_pitch", "ankle_roll"}:
+                    continue  # a foot cannot reach the other leg's thigh
+                pairs.append([a, b])
     base_col = links["base_link"].find("collision")
     bp, _ = parse_origin(base_col.find("origin"))
     size = [float(s) for s in base_col.find("geometry").find("box").get("size").split()]
@@ -147,14 +178,36 @@ def compile_urdf(robot_dir):
         for sy in (-1, 1):
             for sz in (-1, 1):
                 contacts.append(dict(body=0, pos=[bp[0] + sx * size[0] / 2, bp[1] + sy * size[1] / 2,
-                                                  bp[2] + sz * size[2] / 2]))
+                                                  bp[2] + sz * size[2] / 2], radius=0.0))
     return dict(
         robot="XBot-L",
         source="resources/robots/XBot/urdf/XBot-L.urdf (collapse_fixed_joints=True)",
         bodies=out_bodies,
         contacts=contacts,
+        num_leg_contacts=num_leg_contacts,
+        capsules=capsules,
+        pairs=pairs,
         total_mass=float(sum(b["mass"] for b in out_bodies)),
     )
+
+
+def fit_capsule(v):
+    """Capsule along the hull's principal axis (link frame): radius = mean of the two transverse
+    half-extents (along the minor principal axes), segment = the axial extent shrunk by the
+    radius at both ends (so the end caps reach the hull's axial extremes)."""
+    c = v.mean(0)
+    _, _, vt = np.linalg.svd(v - c, full_matrices=False)
+    ax = vt[0]
+    t = (v - c) @ ax
+    half = [0.5 * (np.ptp((v - c) @ vt[k])) for k in (1, 2)]
+    r = float(np.mean(half))
+    lo, hi = t.min() + r, t.max() - r
+    if hi < lo:
+        lo = hi = 0.5 * (t.min() + t.max())
+    mid = 0.5 * (((v - c) @ vt[1]).max() + ((v - c) @ vt[1]).min()) * vt[1] + \
+        0.5 * (((v - c) @ vt[2]).max() + ((v - c) @ vt[2]).min()) * vt[2]
+    base = c + mid  # axis through the centre of the transverse bounding box
+    return dict(p0=(base + lo * ax).tolist(), p1=(base + hi * ax).tolist(), radius=r)
 
 
 if __name__ == "__main__":

@@ -36,29 +36,48 @@ extern "C" {
 
 #define HG_MAX_BODIES 16
 #define HG_MAX_DOF 12
-#define HG_MAX_CONTACTS 16
+#define HG_MAX_CONTACTS 24  /* ground contact candidates (points / spheres) */
+#define HG_MAX_CAPSULES 8
+#define HG_MAX_PAIRS 8      /* self-collision capsule pairs */
 #define HG_NUM_REWARDS 22
 #define HG_MAX_TENSORS 32
+/* solver warm-start impulses per env: 3 per ground candidate, 3 per pair, joint limits, joint friction */
+#define HG_LAMW (HG_MAX_CONTACTS * 3 + HG_MAX_PAIRS * 3 + 2 * HG_MAX_DOF)
 
 /* Articulated model table (output of tools/urdf_compile.py; replaces gym.load_asset +
  * get_asset_* queries, humanoid_env.py:455-470).  Body 0 is the floating base; body b>=1 is
- * attached to parent[b] by revolute joint (dof index b-1).  Frames follow URDF conventions. */
+ * attached to parent[b] by revolute joint (dof index b-1).  Frames follow URDF conventions.
+ * Collision model (BUILD-DEFINED fits of the URDF collision meshes): ground contact candidates
+ * are points (radius 0: sole corners, base-box corners) or spheres (capsule end caps); capsules
+ * collide pairwise (self-collision, humanoid_config.py:103) with the normal from capsule
+ * pair[p][0] to pair[p][1].  Contact priority (the solver keeps at most 9 contact points per env):
+ * ground candidates [0, num_leg_contacts), then the pairs, then the remaining candidates. */
 typedef struct hg_model {
   int32_t num_bodies;
   int32_t num_dof;
-  int32_t num_contacts;     /* candidate contact points */
-  int32_t num_foot_contacts;/* the first num_foot_contacts candidates are foot-sole points */
+  int32_t num_contacts;      /* ground contact candidates */
+  int32_t num_foot_contacts; /* the first num_foot_contacts candidates are foot-sole points */
+  int32_t num_leg_contacts;  /* candidates ranked before the self-collision pairs */
+  int32_t num_capsules;
+  int32_t num_pairs;
+  int32_t _pad;
   int32_t parent[HG_MAX_BODIES];
   int32_t contact_body[HG_MAX_CONTACTS];
+  int32_t capsule_body[HG_MAX_CAPSULES];
+  int32_t pair[HG_MAX_PAIRS][2];
   float joint_pos[HG_MAX_BODIES][3];   /* joint origin in parent-body frame */
   float joint_rot[HG_MAX_BODIES][9];   /* parent-body -> joint frame rotation, row-major */
   float axis[HG_MAX_BODIES][3];        /* joint axis in child frame */
   float mass[HG_MAX_BODIES];
   float com[HG_MAX_BODIES][3];         /* body frame */
   float inertia[HG_MAX_BODIES][6];     /* about COM, body frame: xx yy zz xy xz yz */
-  float armature[HG_MAX_BODIES];
+  float armature[HG_MAX_BODIES];       /* joint-space inertia added to M's diagonal (asset armature, 0) */
   float lower[HG_MAX_BODIES], upper[HG_MAX_BODIES];
+  float joint_friction[HG_MAX_BODIES]; /* Coulomb friction torque bound, N m (URDF dynamics friction) */
   float contact_pos[HG_MAX_CONTACTS][3];
+  float contact_radius[HG_MAX_CONTACTS];
+  float capsule_p0[HG_MAX_CAPSULES][3], capsule_p1[HG_MAX_CAPSULES][3];  /* segment, body frame */
+  float capsule_radius[HG_MAX_CAPSULES];
 } hg_model;
 
 /* Simulation + env-logic configuration.  Field meanings follow XBotLCfg
@@ -147,7 +166,7 @@ enum hg_tensor_id {
   HG_T_BASE_LIN_VEL, HG_T_BASE_ANG_VEL, HG_T_PROJ_GRAVITY, HG_T_BASE_EULER,
   HG_T_REF_DOF_POS, HG_T_ENV_ORIGINS,
   HG_T_EP_STATS,         /* [22 + 2] episode reward means of the last resetting step, n_reset, any */
-  HG_T_CONTACT_LAMBDA,   /* solver warm-start impulses [C*3 + D, N] */
+  HG_T_CONTACT_LAMBDA,   /* solver warm-start impulses [HG_LAMW, N] */
   HG_T_NONFINITE,        /* [N] int32 count of non-finite recoveries */
   HG_T_TERRAIN_LEVEL,    /* [N] int32 curriculum level (row of terrain_origins) */
   HG_T_TERRAIN_TYPE,     /* [N] int32 terrain type (column of terrain_origins) */

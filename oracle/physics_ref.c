@@ -19,15 +19,24 @@
  *
  * Algorithm per substep (dt = sim.dt), generalized velocity nu = [v_base(3) w_base(3) qd(12)],
  * all vectors in a world-aligned frame centred on the base origin:
- *   1. forward kinematics, 2. bias forces h (RNEA, gravity as base acceleration),
- *   3. joint-space inertia M (composite-rigid-body, + armature), 4. Cholesky M = L L^T,
- *   5. nu* = nu + dt M^-1 (tau - h),
- *   6. contacts (sole corners + base box corners vs plane/heightfield, speculative within
- *      contact_offset) and joint limits as unilateral velocity constraints, solved by projected
- *      Gauss-Seidel on impulses with Y = M^-1 J^T (warm-started from the previous substep),
- *      friction cone |lambda_t| <= mu lambda_n, mu = mean(env friction, ground friction)
- *      (PhysX average combine mode),
- *   7. semi-implicit Euler: q += dt qd, p += dt v, quaternion by exact exponential map.
+ *   1. PD torques tau = clip(kp (target - q) - kd qd, +-limit) (humanoid_env.py:910-925); a joint
+ *      whose torque is not clipped has its damping term integrated implicitly: dt*kd is added to
+ *      its diagonal of M (exact for the linear damping term; keeps armature 0 — the asset's value,
+ *      humanoid_config.py:118 — stable with kd = 10 on the light foot at dt = 1 ms),
+ *   2. forward kinematics, 3. bias forces h (RNEA, gravity as base acceleration),
+ *   4. joint-space inertia M (composite-rigid-body, + armature + implicit damping), 5. Cholesky,
+ *   6. nu* = nu + dt M^-1 (tau - h),
+ *   7. constraint rows, at most 32 per env, in this order:
+ *        contacts (normal + 2 tangents each, at most 9 points, in priority order: foot-sole points,
+ *        shin and thigh capsule end spheres vs the ground, then the leg-vs-leg capsule pairs
+ *        (self-collision, humanoid_config.py:103), then the base-box corners; speculative within
+ *        contact_offset, Baumgarte-corrected below zero), then the joint friction rows (URDF
+ *        dynamics friction, 0.1 N m on the ankles: |lambda| <= f dt), then joint limits;
+ *      solved by projected Gauss-Seidel on impulses with Y = M^-1 J^T (warm-started from the
+ *      previous substep); friction cone |lambda_t| <= mu lambda_n with mu = mean(env friction,
+ *      ground friction) against the ground (PhysX average combine) and the env friction between
+ *      the robot's own shapes,
+ *   8. semi-implicit Euler: q += dt qd, p += dt v, quaternion by exact exponential map.
  *
  * Precision: `real` is double by default; -DREF_FLOAT builds an fp32 variant (used to size the
  * fp32 parity tolerance: |gpu - ref64| <= k |ref32 - ref64| + eps).
@@ -53,15 +62,23 @@ typedef double real;
 #define ND 12
 #define NV 18
 #define NC_MAX HG_MAX_CONTACTS
-#define LAMW (NC_MAX * 3 + ND)
+#define NCAP HG_MAX_CAPSULES
+#define NP_MAX HG_MAX_PAIRS
+#define LAMW HG_LAMW
+#define LAM_PAIR (NC_MAX * 3)              /* warm-start slots: ground candidate c -> 3c + d */
+#define LAM_LIM (NC_MAX * 3 + NP_MAX * 3)  /* pair p -> LAM_PAIR + 3p + d; limit j -> LAM_LIM + j */
+#define LAM_FRIC (LAM_LIM + ND)            /* joint friction j -> LAM_FRIC + j */
+#define MAX_ROWS 32
+#define MAX_CONTACT_POINTS 9
 
 typedef struct {
-  int nb, nc, nfoot;
+  int nb, nc, nfoot, nleg, ncap, npair;
   int parent[NB];
-  int cbody[NC_MAX];
+  int cbody[NC_MAX], capbody[NCAP], pair[NP_MAX][2];
   real jpos[NB][3], jrot[NB][9], axis[NB][3];
-  real mass[NB], com[NB][3], inertia[NB][6], armature[NB], lower[NB], upper[NB];
-  real cpos[NC_MAX][3];
+  real mass[NB], com[NB][3], inertia[NB][6], armature[NB], lower[NB], upper[NB], jfric[NB];
+  real cpos[NC_MAX][3], crad[NC_MAX];
+  real cap0[NCAP][3], cap1[NCAP][3], caprad[NCAP];
 } Model;
 
 /* ---------------------------------------------------------------- small vector algebra */
@@ -131,18 +148,26 @@ static void axis_angle(const real* k, real th, real* Rm) {
 
 static void load_model(const hg_model* hm, Model* m) {
   m->nb = hm->num_bodies; m->nc = hm->num_contacts; m->nfoot = hm->num_foot_contacts;
+  m->nleg = hm->num_leg_contacts; m->ncap = hm->num_capsules; m->npair = hm->num_pairs;
   for (int b = 0; b < NB; b++) {
     m->parent[b] = hm->parent[b];
     for (int i = 0; i < 3; i++) { m->jpos[b][i] = hm->joint_pos[b][i]; m->axis[b][i] = hm->axis[b][i]; m->com[b][i] = hm->com[b][i]; }
     for (int i = 0; i < 9; i++) m->jrot[b][i] = hm->joint_rot[b][i];
     for (int i = 0; i < 6; i++) m->inertia[b][i] = hm->inertia[b][i];
-    m->mass[b] = hm->mass[b]; m->armature[b] = hm->armature[b];
+    m->mass[b] = hm->mass[b]; m->armature[b] = hm->armature[b]; m->jfric[b] = hm->joint_friction[b];
     m->lower[b] = hm->lower[b]; m->upper[b] = hm->upper[b];
   }
   for (int c = 0; c < NC_MAX; c++) {
     m->cbody[c] = hm->contact_body[c];
+    m->crad[c] = hm->contact_radius[c];
     for (int i = 0; i < 3; i++) m->cpos[c][i] = hm->contact_pos[c][i];
   }
+  for (int k = 0; k < NCAP; k++) {
+    m->capbody[k] = hm->capsule_body[k];
+    m->caprad[k] = hm->capsule_radius[k];
+    for (int i = 0; i < 3; i++) { m->cap0[k][i] = hm->capsule_p0[k][i]; m->cap1[k][i] = hm->capsule_p1[k][i]; }
+  }
+  for (int p = 0; p < NP_MAX; p++) { m->pair[p][0] = hm->pair[p][0]; m->pair[p][1] = hm->pair[p][1]; }
 }
 
 /* ---------------------------------------------------------------- terrain */
@@ -332,12 +357,53 @@ static void chol_solve(const real* L, int n, int ld, real* x) {
 }
 
 typedef struct {
-  int kind;      /* 0 contact normal, 1 tangent1, 2 tangent2, 3 joint limit */
-  int pt;        /* candidate contact / dof index */
-  real J[NV], Y[NV], D, target, lam;
+  int kind;      /* 0 contact normal, 1 tangent-1, 2 tangent-2, 3 joint limit, 4 joint friction */
+  int lam_idx;   /* warm-start slot */
+  int bpos, bneg;/* contact force +lambda d / dt on bpos, -lambda d / dt on bneg (-1: none) */
+  real d[3];     /* contact direction (world) */
+  real mu;       /* friction coefficient of the contact (normal rows) */
+  real J[NV], Y[NV], D, target, lo, hi, lam;
 } Row;
 
-#define MAX_ROWS (NC_MAX * 3 + ND)
+/* J += sign * (Jacobian of the point x (base-centred) on body b) projected on d */
+static void add_point_jac(const Model* m, const Kin* k, int b, const real* x, const real* d, real sign, real* J) {
+  real xd[3];
+  v3_cross(x, d, xd);
+  for (int i = 0; i < 3; i++) { J[i] += sign * d[i]; J[3 + i] += sign * xd[i]; }
+  for (int kb = b; kb >= 1; kb = m->parent[kb]) {
+    real rr[3], axr[3];
+    for (int i = 0; i < 3; i++) rr[i] = x[i] - k->o[kb][i];
+    v3_cross(k->a[kb], rr, axr);
+    J[5 + kb] += sign * v3_dot(d, axr);
+  }
+}
+
+static real clamp01(real x) { return x < 0 ? 0 : (x > 1 ? 1 : x); }
+
+/* closest points of segments [p1,q1], [p2,q2] (Ericson, Real-Time Collision Detection 5.1.9) */
+static void seg_seg(const real* p1, const real* q1, const real* p2, const real* q2, real* c1, real* c2) {
+  real d1[3], d2[3], r[3];
+  for (int i = 0; i < 3; i++) { d1[i] = q1[i] - p1[i]; d2[i] = q2[i] - p2[i]; r[i] = p1[i] - p2[i]; }
+  const real a = v3_dot(d1, d1), e = v3_dot(d2, d2), f = v3_dot(d2, r);
+  const real c = v3_dot(d1, r), b = v3_dot(d1, d2);
+  const real denom = a * e - b * b;
+  real s = denom > R(1e-6) * a * e ? clamp01((b * f - c * e) / denom) : 0;
+  real t = (b * s + f) / e;
+  if (t < 0) { t = 0; s = clamp01(-c / a); }
+  else if (t > 1) { t = 1; s = clamp01((b - c) / a); }
+  for (int i = 0; i < 3; i++) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
+}
+
+/* tangent basis of a contact normal n (reference axis x, or y when n is close to x) */
+static void tangents(const real* n, real* t1, real* t2) {
+  real ref[3] = {0, 0, 0};
+  ref[fabs(n[0]) < R(0.9) ? 0 : 1] = 1;
+  const real dd = v3_dot(ref, n);
+  for (int i = 0; i < 3; i++) t1[i] = ref[i] - dd * n[i];
+  const real tn = sqrt(v3_dot(t1, t1));
+  for (int i = 0; i < 3; i++) t1[i] /= tn;
+  v3_cross(n, t1, t2);
+}
 
 /* full generalized solve: M x = b restricted to free dofs (fixed base -> 12 joint dofs) */
 static void msolve(const real* L, int off, int n, real* x) {
@@ -347,10 +413,26 @@ static void msolve(const real* L, int off, int n, real* x) {
   for (int i = 0; i < NV; i++) x[i] = (i >= off) ? t[i - off] : 0;
 }
 
+/* contact candidate: ground point/sphere c, or capsule pair p */
+typedef struct {
+  int active, lam_base, bpos, bneg;
+  real phi, n[3], xpos[3], xneg[3], mu;
+} Contact;
+
 static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* root, real* q,
-                    real* qd, real* lamst, const real* tau, real mass0, real fric, real* cf_out,
+                    real* qd, real* lamst, const real* act, real* tau, real mass0, real fric, real* cf_out,
                     int* nonfinite) {
   const real dt = cfg->sim_dt;
+  /* 1. PD torques; implicit damping on the joints whose torque is not clipped */
+  real madd[ND];
+  for (int j = 0; j < ND; j++) {
+    const real t = R(cfg->kp[j]) * (act[j] * R(cfg->action_scale) + R(cfg->default_dof_pos[j]) - q[j]) -
+                   R(cfg->kd[j]) * qd[j];
+    const real lim = cfg->torque_limit[j];
+    const int sat = t < -lim || t > lim;
+    tau[j] = t < -lim ? -lim : (t > lim ? lim : t);
+    madd[j] = sat ? 0 : dt * R(cfg->kd[j]);
+  }
   real nu[NV];
   for (int i = 0; i < 3; i++) { nu[i] = root[7 + i]; nu[3 + i] = root[10 + i]; }
   for (int j = 0; j < ND; j++) nu[6 + j] = qd[j];
@@ -361,6 +443,7 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
   real h[NV], M[NV][NV];
   bias_forces(m, &k, nu, cfg->gravity_z, h);
   mass_matrix(m, &k, M);
+  for (int j = 0; j < ND; j++) M[6 + j][6 + j] += madd[j];
   const int off = fixed ? 6 : 0, n = NV - off;
   real Lm[NV * NV];
   for (int i = 0; i < n; i++)
@@ -371,57 +454,84 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
   msolve(Lm, off, n, acc);
   for (int i = 0; i < NV; i++) nu[i] += dt * acc[i];
 
-  /* ---- constraint rows ---- */
-  static __thread Row rows[MAX_ROWS];
-  int nr = 0;
-  const real mu = R(0.5) * (fric + cfg->ground_friction);
+  /* ---- contact detection, in priority order ---- */
   const real beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel, off_c = cfg->contact_offset;
-  int body_of_row[MAX_ROWS];
-  if (!fixed) {
-    int nct = 0;
-    for (int c = 0; c < m->nc; c++) {
-      int b = m->cbody[c];
+  Contact cand[NC_MAX + NP_MAX];
+  int ncand = 0;
+  for (int item = 0; item < m->nc + m->npair; item++) {
+    /* items: ground candidates [0, nleg), pairs, ground candidates [nleg, nc) */
+    Contact* ct = &cand[ncand++];
+    memset(ct, 0, sizeof(*ct));
+    const int is_pair = item >= m->nleg && item < m->nleg + m->npair;
+    if (!is_pair) {
+      const int c = item < m->nleg ? item : item - m->npair;
+      const int b = m->cbody[c];
       real x[3];
       mat3_vec(k.Rb[b], m->cpos[c], x);
       for (int i = 0; i < 3; i++) x[i] += k.o[b][i];
-      real xw[3] = {x[0] + root[0], x[1] + root[1], x[2] + root[2]};
       real hg, nrm[3];
-      ground(cfg, hf, xw[0], xw[1], &hg, nrm);
-      real phi = (xw[2] - hg) * nrm[2];
-      /* at most 10 active contacts (30 rows) in candidate order: feet first, then base */
-      if (!(phi < off_c) || nct >= 10) { for (int d = 0; d < 3; d++) lamst[c * 3 + d] = 0; continue; }
-      nct++;
-      /* tangent basis */
-      real t1[3], t2[3];
-      real ref[3] = {1, 0, 0};
-      real dd = v3_dot(ref, nrm);
-      for (int i = 0; i < 3; i++) t1[i] = ref[i] - dd * nrm[i];
-      real tn = sqrt(v3_dot(t1, t1));
-      for (int i = 0; i < 3; i++) t1[i] /= tn;
-      v3_cross(nrm, t1, t2);
-      const real* dirs[3] = {nrm, t1, t2};
-      for (int d = 0; d < 3; d++) {
-        Row* r = &rows[nr];
-        r->kind = d; r->pt = c;
-        const real* e = dirs[d];
-        for (int i = 0; i < 3; i++) r->J[i] = e[i];
-        real xe[3];
-        v3_cross(x, e, xe);
-        for (int i = 0; i < 3; i++) r->J[3 + i] = xe[i];
-        for (int j = 0; j < ND; j++) r->J[6 + j] = 0;
-        for (int kb = b; kb >= 1; kb = m->parent[kb]) {
-          real rr[3], axr[3];
-          for (int i = 0; i < 3; i++) rr[i] = x[i] - k.o[kb][i];
-          v3_cross(k.a[kb], rr, axr);
-          r->J[5 + kb] = v3_dot(e, axr);
-        }
-        if (d == 0) r->target = phi >= 0 ? -phi / dt : fmin(-beta * phi / dt, vmax);
-        else r->target = 0;
-        r->lam = lamst[c * 3 + d];
-        body_of_row[nr] = b;
-        nr++;
-      }
+      ground(cfg, hf, x[0] + root[0], x[1] + root[1], &hg, nrm);
+      const real r = m->crad[c];
+      ct->phi = (x[2] + root[2] - hg) * nrm[2] - r;
+      for (int i = 0; i < 3; i++) { ct->n[i] = nrm[i]; ct->xpos[i] = x[i] - r * nrm[i]; }
+      ct->bpos = b; ct->bneg = -1;
+      ct->mu = R(0.5) * (fric + cfg->ground_friction);
+      ct->lam_base = 3 * c;
+      ct->active = !fixed && ct->phi < off_c;
+    } else {
+      const int p = item - m->nleg;
+      const int ca = m->pair[p][0], cb = m->pair[p][1];
+      const int ba = m->capbody[ca], bb = m->capbody[cb];
+      real a0[3], a1[3], b0[3], b1[3], pa[3], pb[3], dv[3];
+      mat3_vec(k.Rb[ba], m->cap0[ca], a0); mat3_vec(k.Rb[ba], m->cap1[ca], a1);
+      mat3_vec(k.Rb[bb], m->cap0[cb], b0); mat3_vec(k.Rb[bb], m->cap1[cb], b1);
+      for (int i = 0; i < 3; i++) { a0[i] += k.o[ba][i]; a1[i] += k.o[ba][i]; b0[i] += k.o[bb][i]; b1[i] += k.o[bb][i]; }
+      seg_seg(a0, a1, b0, b1, pa, pb);
+      for (int i = 0; i < 3; i++) dv[i] = pb[i] - pa[i];
+      const real dist = sqrt(v3_dot(dv, dv));
+      if (dist > R(1e-9)) for (int i = 0; i < 3; i++) ct->n[i] = dv[i] / dist;
+      else { ct->n[0] = 0; ct->n[1] = -1; ct->n[2] = 0; }  /* left -> right is -y in the base frame */
+      const real ra = m->caprad[ca], rb = m->caprad[cb];
+      ct->phi = dist - ra - rb;
+      for (int i = 0; i < 3; i++) { ct->xpos[i] = pb[i] - rb * ct->n[i]; ct->xneg[i] = pa[i] + ra * ct->n[i]; }
+      ct->bpos = bb; ct->bneg = ba;
+      ct->mu = fric;
+      ct->lam_base = LAM_PAIR + 3 * p;
+      ct->active = ct->phi < off_c;
     }
+  }
+  /* ---- rows: contacts (<= MAX_CONTACT_POINTS), joint friction, joint limits ---- */
+  static __thread Row rows[MAX_ROWS];
+  int nr = 0, npts = 0;
+  for (int ci = 0; ci < ncand; ci++) {
+    Contact* ct = &cand[ci];
+    if (!ct->active || npts >= MAX_CONTACT_POINTS) { for (int d = 0; d < 3; d++) lamst[ct->lam_base + d] = 0; continue; }
+    npts++;
+    real t1[3], t2[3];
+    tangents(ct->n, t1, t2);
+    const real* dirs[3] = {ct->n, t1, t2};
+    for (int d = 0; d < 3; d++) {
+      Row* r = &rows[nr++];
+      memset(r, 0, sizeof(*r));
+      r->kind = d; r->lam_idx = ct->lam_base + d;
+      r->bpos = ct->bpos; r->bneg = ct->bneg;
+      for (int i = 0; i < 3; i++) r->d[i] = dirs[d][i];
+      add_point_jac(m, &k, ct->bpos, ct->xpos, dirs[d], 1, r->J);
+      if (ct->bneg >= 0) add_point_jac(m, &k, ct->bneg, ct->xneg, dirs[d], -1, r->J);
+      if (d == 0) r->target = ct->phi >= 0 ? -ct->phi / dt : fmin(-beta * ct->phi / dt, vmax);
+      r->mu = ct->mu;
+      r->lam = lamst[r->lam_idx];
+    }
+  }
+  for (int j = 0; j < ND; j++) {
+    const real f = m->jfric[j + 1];
+    if (!(f > 0)) { lamst[LAM_FRIC + j] = 0; continue; }
+    Row* r = &rows[nr++];
+    memset(r, 0, sizeof(*r));
+    r->kind = 4; r->lam_idx = LAM_FRIC + j; r->bpos = r->bneg = -1;
+    r->J[6 + j] = 1;
+    r->lo = -f * dt; r->hi = f * dt;
+    r->lam = lamst[r->lam_idx];
   }
   const real lim_margin = R(0.01);
   for (int j = 0; j < ND; j++) {
@@ -429,16 +539,14 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
     real sgn, gap;
     if (glo < lim_margin) { sgn = 1; gap = glo; }
     else if (ghi < lim_margin) { sgn = -1; gap = ghi; }
-    else { lamst[NC_MAX * 3 + j] = 0; continue; }
-    if (nr >= 32) { lamst[NC_MAX * 3 + j] = 0; continue; }  /* at most 32 rows */
-    Row* r = &rows[nr];
-    r->kind = 3; r->pt = j;
-    memset(r->J, 0, sizeof(r->J));
+    else { lamst[LAM_LIM + j] = 0; continue; }
+    if (nr >= MAX_ROWS) { lamst[LAM_LIM + j] = 0; continue; }
+    Row* r = &rows[nr++];
+    memset(r, 0, sizeof(*r));
+    r->kind = 3; r->lam_idx = LAM_LIM + j; r->bpos = r->bneg = -1;
     r->J[6 + j] = sgn;
     r->target = gap >= 0 ? -gap / dt : fmin(-beta * gap / dt, vmax);
-    r->lam = lamst[NC_MAX * 3 + j];
-    body_of_row[nr] = -1;
-    nr++;
+    r->lam = lamst[r->lam_idx];
   }
   for (int r = 0; r < nr; r++) {
     for (int i = 0; i < NV; i++) rows[r].Y[i] = rows[r].J[i];
@@ -448,30 +556,30 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
     /* warm start */
     for (int i = 0; i < NV; i++) nu[i] += rows[r].Y[i] * rows[r].lam;
   }
+  /* ---- projected Gauss-Seidel: rows in order; a contact's tangent pair right after its normal ---- */
   for (int it = 0; it < cfg->pgs_iterations; it++) {
     for (int r = 0; r < nr; r++) {
       Row* rn = &rows[r];
-      if (rn->kind == 0 || rn->kind == 3) {
-        real v = 0;
-        for (int i = 0; i < NV; i++) v += rn->J[i] * nu[i];
-        real ln = rn->lam + (rn->target - v) / rn->D;
-        if (ln < 0) ln = 0;
-        real dl = ln - rn->lam;
-        rn->lam = ln;
-        for (int i = 0; i < NV; i++) nu[i] += rn->Y[i] * dl;
-        if (rn->kind == 0) {
-          Row* r1 = &rows[r + 1];
-          Row* r2 = &rows[r + 2];
-          real v1 = 0, v2 = 0;
-          for (int i = 0; i < NV; i++) { v1 += r1->J[i] * nu[i]; v2 += r2->J[i] * nu[i]; }
-          real l1 = r1->lam - v1 / r1->D, l2 = r2->lam - v2 / r2->D;
-          real lim = mu * rn->lam, nn = sqrt(l1 * l1 + l2 * l2);
-          if (nn > lim) { real s = lim / nn; l1 *= s; l2 *= s; }
-          real d1 = l1 - r1->lam, d2 = l2 - r2->lam;
-          r1->lam = l1; r2->lam = l2;
-          for (int i = 0; i < NV; i++) nu[i] += r1->Y[i] * d1 + r2->Y[i] * d2;
-          r += 2;
-        }
+      real v = 0;
+      for (int i = 0; i < NV; i++) v += rn->J[i] * nu[i];
+      real ln = rn->lam + (rn->target - v) / rn->D;
+      if (rn->kind == 4) ln = ln < rn->lo ? rn->lo : (ln > rn->hi ? rn->hi : ln);
+      else if (ln < 0) ln = 0;
+      const real dl = ln - rn->lam;
+      rn->lam = ln;
+      for (int i = 0; i < NV; i++) nu[i] += rn->Y[i] * dl;
+      if (rn->kind == 0) {
+        Row* r1 = &rows[r + 1];
+        Row* r2 = &rows[r + 2];
+        real v1 = 0, v2 = 0;
+        for (int i = 0; i < NV; i++) { v1 += r1->J[i] * nu[i]; v2 += r2->J[i] * nu[i]; }
+        real l1 = r1->lam - v1 / r1->D, l2 = r2->lam - v2 / r2->D;
+        const real lim = rn->mu * rn->lam, nn = sqrt(l1 * l1 + l2 * l2);
+        if (nn > lim) { const real sc = lim / nn; l1 *= sc; l2 *= sc; }
+        const real d1 = l1 - r1->lam, d2 = l2 - r2->lam;
+        r1->lam = l1; r2->lam = l2;
+        for (int i = 0; i < NV; i++) nu[i] += r1->Y[i] * d1 + r2->Y[i] * d2;
+        r += 2;
       }
     }
   }
@@ -479,10 +587,13 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
   for (int b = 0; b < NB * 3; b++) cf_out[b] = 0;
   for (int r = 0; r < nr; r++) {
     Row* rr = &rows[r];
-    if (rr->kind == 3) { lamst[NC_MAX * 3 + rr->pt] = rr->lam; continue; }
-    lamst[rr->pt * 3 + rr->kind] = rr->lam;
-    int b = body_of_row[r];
-    for (int i = 0; i < 3; i++) cf_out[b * 3 + i] += rr->J[i] * rr->lam / dt;
+    lamst[rr->lam_idx] = rr->lam;
+    if (rr->kind > 2) continue;
+    for (int i = 0; i < 3; i++) {
+      const real f = rr->d[i] * rr->lam / dt;
+      cf_out[rr->bpos * 3 + i] += f;
+      if (rr->bneg >= 0) cf_out[rr->bneg * 3 + i] -= f;
+    }
   }
   /* integrate */
   int bad = 0;
@@ -548,16 +659,9 @@ int API(ref_step)(const hg_cfg* cfg, const hg_model* hm, const int16_t* hf, int 
     const real* ae = actions + (size_t)e * ND;
     real tau[ND];
     int bad = 0;
-    for (int s = 0; s < cfg->decimation && !bad; s++) {
-      for (int j = 0; j < ND; j++) {
-        real t = R(cfg->kp[j]) * (ae[j] * R(cfg->action_scale) + R(cfg->default_dof_pos[j]) - qe[j]) -
-                 R(cfg->kd[j]) * qde[j];
-        real lim = cfg->torque_limit[j];
-        tau[j] = t < -lim ? -lim : (t > lim ? lim : t);
-      }
-      substep(cfg, &m, hf, re, qe, qde, lam + (size_t)e * LAMW, tau, mass0[e], fric[e],
+    for (int s = 0; s < cfg->decimation && !bad; s++)
+      substep(cfg, &m, hf, re, qe, qde, lam + (size_t)e * LAMW, ae, tau, mass0[e], fric[e],
               contact + (size_t)e * NB * 3, &bad);
-    }
     for (int j = 0; j < ND; j++) torques[(size_t)e * ND + j] = tau[j];
     nonfinite[e] = bad;
     rigid_states(&m, re, qe, qde, mass0[e], rigid + (size_t)e * NB * 13);

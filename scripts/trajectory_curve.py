@@ -18,7 +18,7 @@ import test_gpu_parity as T  # noqa: E402  (helpers only: _make_env, snapshot, _
 
 def run(fixed, steps, n=16):
     import pipeline_ref as PR
-    env = T._make_env(n, "v2", asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
+    env = T._make_env(n, asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
                       domain_rand__push_robots=False, noise__add_noise=False)
     S, _, _ = T.snapshot(env)
     oc = T._oracle_cfg(env)

@@ -61,7 +61,16 @@ def test_struct_layouts_match_header(tmp_path):
 
 def test_model_table():
     m, js = N.load_model()
-    assert m.num_bodies == 13 and m.num_dof == 12 and m.num_contacts == 16 and m.num_foot_contacts == 8
+    assert m.num_bodies == 13 and m.num_dof == 12 and m.num_contacts == 24 and m.num_foot_contacts == 8
+    assert m.num_leg_contacts == 16 and m.num_capsules == 6 and m.num_pairs == 7
+    # ankle pitch / roll joints carry the URDF's 0.1 N m friction; the asset armature is 0
+    assert [round(m.joint_friction[b], 6) for b in range(1, 13)] == [0, 0, 0, 0, 0.1, 0.1] * 2
+    assert all(m.armature[b] == 0.0 for b in range(13))
+    # pairs: left capsule -> right capsule, no foot-thigh pair
+    caps = js["capsules"]
+    for a, b in js["pairs"]:
+        assert caps[a]["side"] == "left" and caps[b]["side"] == "right"
+        assert {caps[a]["part"], caps[b]["part"]} != {"leg_pitch", "ankle_roll"}
     assert abs(js["total_mass"] - 53.036) < 0.01
     bodies = [b["name"] for b in js["bodies"]]
     assert bodies.index("left_ankle_roll_link") == 6 and bodies.index("right_ankle_roll_link") == 12

@@ -272,50 +272,82 @@ def test_step_physics_parity(physics_env):
                                 ("root", g(env.root_states), r64.root, r32.root),
                                 ("torques", g(env.torques), r64.torques, r32.torques),
                                 ("rigid", g(env.rigid_state), r64.rigid, r32.rigid)):
-        tol = 20 * np.maximum(np.abs(a32 - a64), sp[name]) + 1e-3 * (1 + np.abs(a64))
+        # stated fp32 tolerance: 20 x the larger of the CPU f32-vs-f64 gap and the local
+        # conditioning spread of the f64 step, plus fp32 rounding (2^-20 relative, ~8 ulp)
+        tol = 20 * np.maximum(np.abs(a32 - a64), sp[name]) + 2.0 ** -20 * (1 + np.abs(a64))
         bad = np.abs(gpu - a64) > tol
         assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
+
+
+# Stated fp32 tolerances of the SURVEY §8d parity trajectory (1000 policy steps = 10,000
+# substeps, seed 5, open-loop a_t[j] = 0.5 sin(2 pi t 0.01 / 0.64 + j pi / 6), DR and noise off),
+# HIP K_step vs the f64 reference simulator (oracle/physics_ref.c), DESIGN.md §4:
+#   variant A (fixed base): |dq| <= TRAJ_FIXED_DQ rad, |dtau| <= TRAJ_FIXED_DTAU N m over all steps;
+#   variant B (floating base, chaotic contact dynamics): the running max of |dq| stays within
+#   TRAJ_FLOAT_K x the running max of the CPU f32-vs-f64 divergence (+ TRAJ_FLOAT_FLOOR rad) at
+#   every step — the HIP fp32 path diverges from f64 no faster than fp32 arithmetic itself does.
+TRAJ_FIXED_DQ = 2e-5
+TRAJ_FIXED_DTAU = 2e-2
+TRAJ_FLOAT_K = 2.0
+TRAJ_FLOAT_FLOOR = 1e-5
 
 
 def test_trajectory_1000_steps_fixed_base():
     """SURVEY §8d parity trajectory, variant A (fix_base_link): joint angles / torques of the HIP
     path vs the f64 reference simulator over 1000 policy steps (10,000 substeps)."""
     _need_gpu()
-    err_q, err_tau = _run_trajectory(fixed=True, steps=1000)
-    assert err_q.max() < 2e-3, err_q.max()
-    assert err_tau.max() < 0.5, err_tau.max()
+    c = _run_trajectory(fixed=True, steps=1000)
+    print("fixed base: gpu-vs-f64 |dq| %.3g |dtau| %.3g; cpu f32-vs-f64 |dq| %.3g |dtau| %.3g" % (
+        c["gpu_q"].max(), c["gpu_tau"].max(), c["f32_q"].max(), c["f32_tau"].max()))
+    assert c["gpu_q"].max() <= TRAJ_FIXED_DQ, c["gpu_q"].max()
+    assert c["gpu_tau"].max() <= TRAJ_FIXED_DTAU, c["gpu_tau"].max()
 
 
 def test_trajectory_floating_base():
-    """Variant B (floating base on the plane): tight agreement over the first 100 steps; the
-    contact dynamics then diverge chaotically (fp32 vs fp64), so the rest is reported."""
+    """Variant B (floating base on the plane, the robot falls under open-loop actions): the
+    fp32 HIP path tracks f64 within TRAJ_FLOAT_K x the CPU fp32 divergence envelope at every one
+    of the 1000 steps."""
     _need_gpu()
-    err_q, err_tau = _run_trajectory(fixed=False, steps=300)
-    assert err_q[:100].max() < 5e-2, err_q[:100].max()
-    print("floating-base |dq| max at steps 100/200/300:", err_q[99], err_q[199], err_q[299])
+    c = _run_trajectory(fixed=False, steps=1000)
+    env_gpu, env_f32 = np.maximum.accumulate(c["gpu_q"]), np.maximum.accumulate(c["f32_q"])
+    print("floating base |dq| gpu/f32 at steps 100/300/1000:", [(env_gpu[i], env_f32[i]) for i in (99, 299, 999)])
+    bad = env_gpu > TRAJ_FLOAT_K * env_f32 + TRAJ_FLOAT_FLOOR
+    assert not bad.any(), f"first step over the envelope: {int(np.argmax(bad))}"
 
 
-def _run_trajectory(fixed, steps):
+def _run_trajectory(fixed, steps, n=16):
+    """Per-step max |dq|, |dtau| of the HIP path and of the CPU fp32 oracle, both vs the f64 oracle
+    (curves also written to $HG_TRAJ_OUT/trajectory_<variant>.json when set)."""
+    import json
     import pipeline_ref as PR
-    env = _make_env(16, asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
+    env = _make_env(n, asset__fix_base_link=fixed, domain_rand__dynamic_randomization=0.0,
                     domain_rand__push_robots=False, noise__add_noise=False)
     S, _, _ = snapshot(env)
     oc = _oracle_cfg(env)
-    r64 = _ref_sim(env, S, "f64")
-    prev_gpu = np.zeros((16, 12), np.float32)
-    err_q, err_tau = [], []
+    r64, r32 = _ref_sim(env, S, "f64"), _ref_sim(env, S, "f32")
+    prev_gpu = np.zeros((n, 12), np.float32)
+    c = {k: [] for k in ("gpu_q", "gpu_tau", "f32_q", "f32_tau")}
     j = np.arange(12)
     for t in range(steps):
-        a = np.tile(0.5 * np.sin(2 * np.pi * t * 0.01 / 0.64 + j * np.pi / 6), (16, 1)).astype(np.float32)
-        S_act = torch.from_numpy(a).cuda()
+        a = np.tile(0.5 * np.sin(2 * np.pi * t * 0.01 / 0.64 + j * np.pi / 6), (n, 1)).astype(np.float32)
         a_ref = PR.preprocess_actions(oc, a, prev_gpu, t)
-        _step_only(env, S_act, t)
+        _step_only(env, torch.from_numpy(a).cuda(), t)
         prev_gpu = env.actions.cpu().numpy()
         r64.step(a_ref.astype(np.float64))
-        err_q.append(np.abs(env.dof_pos.cpu().numpy() - r64.q).max())
-        err_tau.append(np.abs(env.torques.cpu().numpy() - r64.torques).max())
+        r32.step(a_ref)
+        q, tau = env.dof_pos.cpu().numpy(), env.torques.cpu().numpy()
+        c["gpu_q"].append(np.abs(q - r64.q).max())
+        c["gpu_tau"].append(np.abs(tau - r64.torques).max())
+        c["f32_q"].append(np.abs(r32.q - r64.q).max())
+        c["f32_tau"].append(np.abs(r32.torques - r64.torques).max())
     assert np.isfinite(env.dof_pos.cpu().numpy()).all()
-    return np.array(err_q), np.array(err_tau)
+    c = {k: np.array(v) for k, v in c.items()}
+    out = os.environ.get("HG_TRAJ_OUT")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, f"trajectory_{'fixed' if fixed else 'floating'}.json"), "w") as f:
+            json.dump({k: [float(x) for x in v] for k, v in c.items()}, f)
+    return c
 
 
 def test_determinism(env):

@@ -3,7 +3,11 @@
 PhysX is unavailable, so physics parity against the reference is unpinned; these checks pin the
 oracle's mechanics to first principles instead: mass matrix symmetric positive
 definite and consistent with the bodies' kinetic energy, free fall, momentum conservation in
-flight, energy conservation without actuation, and static support ≈ m·g."""
+flight, energy conservation without actuation, and static support ≈ m·g (mechanics tests run
+without self-collision and joint friction: random poses interpenetrate the legs).  The collision
+and friction features have their own checks: self-collision impulses are equal and opposite and
+separate the legs, the ankle joint friction holds a sub-threshold load and releases a larger one,
+and armature 0 with the implicit PD damping stands stably."""
 import ctypes
 
 import numpy as np
@@ -24,7 +28,7 @@ def quat_R(q):
 
 @pytest.fixture(scope="module")
 def model():
-    m, js = N.load_model(armature=0.0)
+    m, js = N.load_model(armature=0.0, joint_friction=False, self_collisions=False)
     return m, js
 
 
@@ -175,7 +179,7 @@ def test_energy_conservation_fixed_base(model):
 
 
 def test_static_support_equals_weight():
-    m, js = N.load_model(armature=0.01)   # the product's armature (explicit kd=10 on the bare foot is unstable)
+    m, js = N.load_model()   # the product model: armature 0 (implicit PD damping), friction, self-collision
     n = 2
     cfg = make_cfg(n, kp=0.0)
     for j in range(12):
@@ -190,3 +194,83 @@ def test_static_support_equals_weight():
     np.testing.assert_allclose(fz, js["total_mass"] * G, rtol=0.05)
     sole_z = sim.rigid[:, 6, 2]
     assert (sole_z > 0.03).all()          # no deep penetration (sole is 0.056 below the foot frame)
+
+
+def _capsule_world(js, rigid, c):
+    s = rigid[c["body"]]
+    R = quat_R(s[3:7])
+    return s[:3] + R @ np.array(c["p0"]), s[:3] + R @ np.array(c["p1"])
+
+
+def test_self_collision_separates_legs():
+    """Legs rolled into each other (fixed base in the air): the pair rows produce equal and
+    opposite net forces on the touching left/right bodies and push them apart over a few steps."""
+    m, js = N.load_model()
+    n = 1
+    cfg = make_cfg(n, fixed=True)
+    for j in range(12):
+        cfg.kp[j], cfg.kd[j] = [200, 200, 350, 350, 15, 15][j % 6], 10.0
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 3.0
+    sim.q[0, 0], sim.q[0, 6] = -0.12, 0.12      # shins (bodies 4, 10) overlap by ~2 cm
+    act = np.zeros((n, 12))
+    act[0, 0], act[0, 6] = -0.12 / 0.25, 0.12 / 0.25   # PD target holds the pose: only the contact separates
+    cfg.decimation = 1
+    sim.step(act)
+    f = sim.contact[0]
+    left = f[1:7].sum(0)
+    right = f[7:13].sum(0)
+    assert np.abs(left).max() > 10.0                      # a real contact force
+    np.testing.assert_allclose(left, -right, atol=1e-6 * np.abs(left).max())
+    caps = js["capsules"]
+    a0, a1 = _capsule_world(js, sim.rigid[0], caps[1])    # left shin
+    b0, b1 = _capsule_world(js, sim.rigid[0], caps[4])    # right shin
+    gap0 = np.linalg.norm(0.5 * (a0 + a1) - 0.5 * (b0 + b1))
+    for _ in range(50):
+        sim.step(act)
+    a0, a1 = _capsule_world(js, sim.rigid[0], caps[1])
+    b0, b1 = _capsule_world(js, sim.rigid[0], caps[4])
+    assert np.linalg.norm(0.5 * (a0 + a1) - 0.5 * (b0 + b1)) > gap0 + 5e-3
+    assert sim.nonfinite[0] == 0
+
+
+def test_ankle_joint_friction_holds_and_slips():
+    """The 0.1 N m ankle friction (XBot-L.urdf:1675-1677): a 0.05 N m torque on a fixed-base,
+    unactuated ankle is held (joint velocity stays 0), a 0.5 N m torque turns it."""
+    m, js = N.load_model()
+    n = 2
+    cfg = make_cfg(n, fixed=True, gz=0.0)
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 3.0
+    # kp-only PD as a constant torque source: tau = kp * (a * 0.25 - q) with q ~ 0
+    for j in range(12):
+        cfg.kp[j], cfg.kd[j] = 0.0, 0.0
+    cfg.kp[5] = 1.0
+    act = np.zeros((n, 12))
+    act[0, 5] = 0.05 / 0.25
+    act[1, 5] = 0.5 / 0.25
+    cfg.decimation = 1
+    for _ in range(20):
+        sim.step(act)
+    assert abs(sim.qd[0, 5]) < 1e-9 and abs(sim.q[0, 5]) < 1e-9
+    assert sim.qd[1, 5] > 0.1
+
+
+def test_armature_zero_stands_stably():
+    """Armature 0 (the asset's value) with kd = 10 on the foot at dt = 1 ms: the explicit damping
+    term alone would be unstable on the 1e-3 kg m^2 foot; integrated implicitly it settles."""
+    m, js = N.load_model()
+    assert m.armature[6] == 0.0
+    n = 1
+    cfg = make_cfg(n, kp=0.0)
+    cfg.decimation = 10
+    for j in range(12):
+        cfg.kp[j] = [200, 200, 350, 350, 15, 15][j % 6]
+        cfg.kd[j] = 10.0
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 0.90
+    sim.qd[0, 5] = 5.0   # kick the left ankle roll
+    for _ in range(100):
+        sim.step(np.zeros((n, 12)))
+    assert sim.nonfinite[0] == 0
+    assert np.abs(sim.qd).max() < 0.2
