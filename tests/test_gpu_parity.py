@@ -286,8 +286,8 @@ def test_step_physics_parity(physics_env):
 #   variant B (floating base, chaotic contact dynamics): the running max of |dq| stays within
 #   TRAJ_FLOAT_K x the running max of the CPU f32-vs-f64 divergence (+ TRAJ_FLOAT_FLOOR rad) at
 #   every step — the HIP fp32 path diverges from f64 no faster than fp32 arithmetic itself does.
-TRAJ_FIXED_DQ = 2e-5
-TRAJ_FIXED_DTAU = 2e-2
+TRAJ_FIXED_DQ = 1e-5
+TRAJ_FIXED_DTAU = 1e-2
 TRAJ_FLOAT_K = 2.0
 TRAJ_FLOAT_FLOOR = 1e-5
 
