@@ -62,7 +62,7 @@ struct __align__(16) EnvSh {
     struct { float rigid[13 * 13]; float cf[13 * 3]; } out;            // epilogue staging
   } u;
   float L[18][20];         // M (dof order, lower) then its Cholesky factor (legs-first order)
-  float colbuf[20], bbuf[20];
+  float colbuf[20], bbuf[20];  // Cholesky column broadcasts / g's right-hand side
   GroupC grp[NGRP];
   float rd[RMAX][3];       // row direction (contact rows) / sign in rd[r][0] (joint rows)
   int rbP[RMAX], rbN[RMAX];// contact rows: bodies receiving +/- lambda d; joint rows: rbP = -1 - dof
@@ -71,7 +71,7 @@ struct __align__(16) EnvSh {
   float cf[13][3];
   float base_cm, base_cs[3], base_cJ[6];
   float mass0, fric;
-  int nrows, bad;
+  int nrows, npts, bad;
 };
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
@@ -502,8 +502,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // i <-> dof o(i) = i < 12 ? 6 + i : i - 12): M's arrow structure gives L no left-right-leg
     // block, so those columns are skipped.  Lane i holds row i; each pivot column is broadcast
     // through LDS (one write, half-wave broadcast reads; same-wave LDS accesses complete in order,
-    // so no barrier) and the rank-1 update is one FMA per trailing entry.  The right-hand side
-    // b = tau - h rides along as an extra column: g = L^-1 b falls out of the same loop.
+    // so no barrier) and the rank-1 update is one FMA per trailing entry.  Then g = L^-1 (tau - h)
+    // by a column-oriented forward substitution on the rows still in registers.
     {
       float a[18];
       bool nonpd = false;
@@ -516,22 +516,59 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       }
       float bv = (l < 18) ? (ol >= 6 ? E.tau[(ol >= 6 ? ol : 6) - 6] : 0.f) - E.h[l < 18 ? ol : 0] : 0.f;
       asm volatile("" ::: "memory");
+      // steps 0..5: the left-leg pivot j and the right-leg pivot 6 + j together (the two leg blocks
+      // are independent: a left-leg row has L[.][6 + j] = 0, so its right-pivot multiplier is 0,
+      // and vice versa; base rows take both updates, which commute); steps 6..: base pivots
 #pragma unroll
-      for (int j = 0; j < nf; j++) {
-        if (l < 18) { E.colbuf[l] = a[j]; E.bbuf[l] = bv; }
+      for (int j = 0; j < 6; j++) {
+        const int j2 = 6 + j;
+        if (l < 18) { E.colbuf[l] = a[j]; E.bbuf[l] = a[j2]; }
+        const float d1 = E.colbuf[j], d2 = E.bbuf[j2];
+        nonpd |= !(d1 > 0.f) || !(d2 > 0.f);
+        const float inv1 = __builtin_amdgcn_rsqf(fmaxf(d1, 1e-20f));  // 1 / L_jj (1 ulp)
+        const float inv2 = __builtin_amdgcn_rsqf(fmaxf(d2, 1e-20f));
+        const float t1 = a[j] * (inv1 * inv1);    // L[l][j] / L[j][j]   (0 on right-leg rows)
+        const float t2 = a[j2] * (inv2 * inv2);   // L[l][j2] / L[j2][j2] (0 on left-leg rows)
+        if (l == 0) { E.invd[j] = inv1; E.invd[j2] = inv2; }
+        a[j] = (lane_opaque(l) >= j) ? a[j] * inv1 : a[j];
+        a[j2] = (lane_opaque(l) >= j2) ? a[j2] * inv2 : a[j2];
+#pragma unroll
+        for (int k = j + 1; k < 6; k++) a[k] -= t1 * E.colbuf[k];
+#pragma unroll
+        for (int k = j2 + 1; k < 12; k++) a[k] -= t2 * E.bbuf[k];
+#pragma unroll
+        for (int k = 12; k < nf; k++) a[k] -= t1 * E.colbuf[k] + t2 * E.bbuf[k];
+      }
+#pragma unroll
+      for (int j = 12; j < nf; j++) {
+        if (l < 18) E.colbuf[l] = a[j];
         const float d = E.colbuf[j];
-        const float bj = E.bbuf[j];
         nonpd |= !(d > 0.f);
-        const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));  // 1 / L_jj (1 ulp)
-        const float t = a[j] * (inv * inv);  // L[l][j] / L[j][j]
-        if (l == 0) { E.invd[j] = inv; E.gv[j] = bj * inv; }
+        const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));
+        const float t = a[j] * (inv * inv);
+        if (l == 0) E.invd[j] = inv;
         a[j] = (lane_opaque(l) >= j) ? a[j] * inv : a[j];
-        bv = (lane_opaque(l) > j) ? bv - t * bj : bv;  // b_l -= L[l][j] g_j
 #pragma unroll
-        for (int k = j + 1; k < nf; k++) {
-          if (j < 6 && k >= 6 && k < 12) continue;  // structural zero: left-leg pivot, right-leg row
-          a[k] -= t * E.colbuf[k];  // L[l][j] L[k][j] = (a_lj / d) a_kj
-        }
+        for (int k = j + 1; k < nf; k++) a[k] -= t * E.colbuf[k];
+      }
+      // g = L^-1 b, column-oriented on the factor's rows (lane i holds L[i][.] in a[]): the two
+      // leg blocks in parallel, then the base rows
+      if (l < 18) E.bbuf[l] = bv;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        const int j2 = 6 + j;
+        const float g1 = E.bbuf[j] * E.invd[j], g2 = E.bbuf[j2] * E.invd[j2];
+        if (l == 0) { E.gv[j] = g1; E.gv[j2] = g2; }
+        bv = (lane_opaque(l) > j && (lane_opaque(l) < 6 || lane_opaque(l) >= 12)) ? bv - a[j] * g1 : bv;
+        bv = (lane_opaque(l) > j2) ? bv - a[j2] * g2 : bv;
+        if (l < 18) E.bbuf[l] = bv;
+      }
+#pragma unroll
+      for (int j = 12; j < nf; j++) {
+        const float gj = E.bbuf[j] * E.invd[j];
+        if (l == 0) E.gv[j] = gj;
+        bv = (lane_opaque(l) > j) ? bv - a[j] * gj : bv;
+        if (l < 18) E.bbuf[l] = bv;
       }
       if (l < 18) {
 #pragma unroll
@@ -602,7 +639,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       const int nfr = __popc(mf);
       const int nrows = min(RMAX, 3 * npts + nfr + __popc(ml));
       const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
-      if (l == 0) E.nrows = nrows;
+      if (l == 0) { E.nrows = nrows; E.npts = npts; }
       // group-level fields and empty slots
       if (l < NGRP) { E.grp[l].contact = l < npts ? 1 : 0; E.grp[l].mu = 0.f; }
       for (int r = l; r < 3 * NGRP; r += 32) {
@@ -685,7 +722,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           const f3 xd = cross(xp, d) - (pair2 ? cross(xn, d) : mk(0, 0, 0));
           J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
 #pragma unroll
-          for (int k = 1; k <= 12; k++) J[5 + k] = chain_term(E, bP, k, xp, d) - chain_term(E, bN, k, xn, d);
+          for (int k = 1; k <= 12; k++) J[5 + k] = chain_term(E, bP, k, xp, d);
+        }
+      }
+      // the other capsule's chain (self-collision rows), only when the wave has such a row
+      if (__ballot(own && E.rbN[l] >= 0) != 0) {
+        if (own && E.rbN[l] >= 0) {
+          const int bN = E.rbN[l];
+          const f3 d = ld3(E.rd[l]), xn = ld3(E.u.rg.xN[l]);
+#pragma unroll
+          for (int k = 1; k <= 12; k++) J[5 + k] -= chain_term(E, bN, k, xn, d);
         }
       }
 #pragma unroll
@@ -729,14 +775,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     float wrow[RMAX];
 #pragma unroll
     for (int m = 0; m < RMAX; m++) wrow[m] = (m % 8 < 4) ? wA[4 * (m / 8) + m % 8] : wB[4 * (m / 8) + m % 8 - 4];
-    // ---- A12: group constants (1/W_rr and the in-group couplings), warm-started row velocities
+    // ---- A12: group constants (1/W_rr and the in-group couplings z_r . z_{r-1}, z_r . z_{r-2}
+    // from the Z rows in LDS), warm-started row velocities
     {
       float Dd = 0.f, W1 = 0.f, W2 = 0.f;  // W[l][l], W[l][l-1], W[l][l-2]
+      const int l1 = l >= 1 ? l - 1 : 0, l2 = l >= 2 ? l - 2 : 0;
 #pragma unroll
-      for (int m = 0; m < RMAX; m++) {
-        Dd = (l == m) ? wrow[m] : Dd;
-        W1 = (l == m + 1) ? wrow[m] : W1;
-        W2 = (l == m + 2) ? wrow[m] : W2;
+      for (int k = 0; k < 18; k++) {
+        Dd += z[k] * z[k];
+        W1 += z[k] * E.u.Z[l1][k];
+        W2 += z[k] * E.u.Z[l2][k];
       }
       const int g = l / 3, k = l % 3;
       E.grp[g].invD[k] = own ? __builtin_amdgcn_rcpf(Dd) : 0.f;
@@ -765,6 +813,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       for (int m = 0; m < RMAX; m++) lam[m] = m < nrows ? E.rLam[m] : 0.f;
       float vrow = v0;
       const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;
+      const int npts_min = min(shm[0].npts, shm[1].npts), npts_max = max(shm[0].npts, shm[1].npts);
       const int npgs = cfg->pgs_iterations;
       for (int it = 0; it < npgs; it++) {
 #pragma unroll
@@ -778,18 +827,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const float na = fminf(fmaxf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0]), G.hi[0]);
             const float da = na - la;
             const float vb1 = vb + G.Wba * da, vc1 = vc + G.Wca * da;
-            // contact: tangent pair on the friction disc
-            const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
-            const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
-            const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
-            // single rows in sequence
-            const float nbs = fminf(fmaxf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1]), G.hi[1]);
-            const float dbs = nbs - lb;
-            const float vc2 = vc1 + G.Wcb * dbs;
-            const float ncs = fminf(fmaxf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2]), G.hi[2]);
-            const bool ct = G.contact != 0;
-            const float db = ct ? l1 * sc - lb : dbs;
-            const float dc = ct ? l2 * sc - lc : ncs - lc;
+            float db, dc;
+            if (g < npts_min) {          // a contact in both envs: tangent pair on the friction disc
+              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
+              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
+              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+              db = l1 * sc - lb;
+              dc = l2 * sc - lc;
+            } else if (g >= npts_max) {  // single rows in both envs, in sequence
+              const float nbs = fminf(fmaxf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1]), G.hi[1]);
+              db = nbs - lb;
+              const float vc2 = vc1 + G.Wcb * db;
+              dc = fminf(fmaxf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2]), G.hi[2]) - lc;
+            } else {                     // mixed: both, picked per env
+              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
+              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
+              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+              const float nbs = fminf(fmaxf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1]), G.hi[1]);
+              const float dbs = nbs - lb;
+              const float vc2 = vc1 + G.Wcb * dbs;
+              const float ncs = fminf(fmaxf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2]), G.hi[2]);
+              const bool ct = G.contact != 0;
+              db = ct ? l1 * sc - lb : dbs;
+              dc = ct ? l2 * sc - lc : ncs - lc;
+            }
             if (rc < RMAX) {
               vrow += wrow[ra] * da + wrow[rb] * db + wrow[rc < RMAX ? rc : 0] * dc;
               lam[rc < RMAX ? rc : 0] += dc;
