@@ -43,6 +43,14 @@ struct GroupC {  // PGS constants of one 3-slot group (a, b, c), one broadcast r
   int pad;
 };
 
+struct ContactC {  // one active contact: points on the two bodies (base-centred), normal + tangents
+  float xP[3], xN[3];
+  float dir[3][3];
+  int bP, bN;              // +lambda d on bP, -lambda d on bN (-1: the ground)
+  int lam_base;            // warm-start slots lam_base + 0..2
+  int pad;
+};
+
 struct __align__(16) EnvSh {
   float root[16];
   float q[12], qd[12], act[12], tau[12];
@@ -57,15 +65,15 @@ struct __align__(16) EnvSh {
   float cm[13], cs[13][3], cJ[13][6];
   union {
     struct { float al[13][3], ac[13][3], f[13][3], n[13][3]; } kin;  // RNEA scratch
-    struct { float xP[RMAX][3], xN[RMAX][3]; } rg;                     // row contact points
     float Z[RMAX][20];                                                 // z_r rows, legs-first order
     struct { float rigid[13 * 13]; float cf[13 * 3]; } out;            // epilogue staging
   } u;
   float L[18][20];         // M (dof order, lower) then its Cholesky factor (legs-first order)
-  float colbuf[20], bbuf[20];  // Cholesky column broadcasts / g's right-hand side
+  float colbuf[20], colbuf2[20], bbuf[20];  // Cholesky column / right-hand-side broadcasts
   GroupC grp[NGRP];
-  float rd[RMAX][3];       // row direction (contact rows) / sign in rd[r][0] (joint rows)
-  int rbP[RMAX], rbN[RMAX];// contact rows: bodies receiving +/- lambda d; joint rows: rbP = -1 - dof
+  ContactC ct[MAX_PTS];
+  float rd[RMAX][3];       // joint rows: sign in rd[r][0]
+  int rbP[RMAX], rbN[RMAX];// joint rows: rbP = -1 - dof
   int rlam[RMAX];          // warm-start slot
   float rLam[RMAX];
   float cf[13][3];
@@ -437,6 +445,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     E.pd_lim[l] = cfg->torque_limit[l];
     E.pd_tgt[l] = E.act[l] * cfg->action_scale + cfg->default_dof_pos[l];
   }
+  for (int i = l; i < 18 * 20; i += 32) (&E.L[0][0])[i] = 0.f;  // the left-right cross block stays zero
   const int decimation = cfg->decimation;
 
   for (int sub = 0; sub < decimation; sub++) {
@@ -470,109 +479,93 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
       for (int i = 0; i < 6; i++) E.base_cJ[i] = E.cJ[0][i] + E.cJ[1][i] + E.cJ[7][i];
     }
-    for (int i = l; i < 18 * 20; i += 32) (&E.L[0][0])[i] = 0.f;
     __syncthreads();
-    // ---- A6/A7: base block (lane 0); joint columns of M (lanes 1..12), + armature + implicit damping
+    // ---- A6/A7: M written straight into the factor's legs-first lower triangle (index i <-> dof
+    // o(i) = i < 12 ? 6 + i : i - 12): joint b's lane writes its row b-1 (ancestors in its leg,
+    // diagonal + armature + implicit damping) and its column of the six base rows; lane 0 the base
+    // block.  The left-right cross block stays zero from the launch-time fill.
     if (l == 0) {
       const float m0 = E.base_cm;
       f3 s = ld3(E.base_cs);
       const float* J0 = E.base_cJ;
       float (*A)[20] = E.L;
-      A[0][0] = A[1][1] = A[2][2] = m0;
-      A[3][1] = -s.z; A[3][2] = s.y;
-      A[4][0] = s.z;  A[4][2] = -s.x;
-      A[5][0] = -s.y; A[5][1] = s.x;
-      A[3][3] = J0[0]; A[4][4] = J0[1]; A[5][5] = J0[2];
-      A[4][3] = J0[3]; A[5][3] = J0[4]; A[5][4] = J0[5];
+      A[12][12] = A[13][13] = A[14][14] = m0;
+      A[13][12] = 0.f; A[14][12] = 0.f; A[14][13] = 0.f;
+      A[15][12] = 0.f;  A[15][13] = -s.z; A[15][14] = s.y;
+      A[16][12] = s.z;  A[16][13] = 0.f;  A[16][14] = -s.x;
+      A[17][12] = -s.y; A[17][13] = s.x;  A[17][14] = 0.f;
+      A[15][15] = J0[0]; A[16][16] = J0[1]; A[17][17] = J0[2];
+      A[16][15] = J0[3]; A[17][15] = J0[4]; A[17][16] = J0[5];
     } else if (l <= 12) {
-      const int b = l, col = 5 + b;
+      const int b = l, i = b - 1;
       f3 a = ld3(E.a[b]), o = ld3(E.o[b]);
       f3 cs = ld3(E.cs[b]);
       f3 F = cross(a, cs - E.cm[b] * o);
       f3 Lm = symv(E.cJ[b], a) - cross(cs, cross(a, o));
       float (*A)[20] = E.L;
-      A[col][0] = F.x; A[col][1] = F.y; A[col][2] = F.z;
-      A[col][3] = Lm.x; A[col][4] = Lm.y; A[col][5] = Lm.z;
+      A[12][i] = F.x; A[13][i] = F.y; A[14][i] = F.z;
+      A[15][i] = Lm.x; A[16][i] = Lm.y; A[17][i] = Lm.z;
       const int first = b <= 6 ? 1 : 7;
-      for (int kb = b; kb >= first; kb--) A[col][5 + kb] = dot(ld3(E.a[kb]), Lm - cross(ld3(E.o[kb]), F));
-      A[col][col] += E.madd[b - 1];
+      for (int kb = b; kb >= first; kb--) A[i][kb - 1] = dot(ld3(E.a[kb]), Lm - cross(ld3(E.o[kb]), F));
+      A[i][i] += E.madd[b - 1];
     }
     __syncthreads();
-    // ---- A8: Cholesky in registers, legs-first order [left leg, right leg, base] (new index
-    // i <-> dof o(i) = i < 12 ? 6 + i : i - 12): M's arrow structure gives L no left-right-leg
-    // block, so those columns are skipped.  Lane i holds row i; each pivot column is broadcast
-    // through LDS (one write, half-wave broadcast reads; same-wave LDS accesses complete in order,
-    // so no barrier) and the rank-1 update is one FMA per trailing entry.  Then g = L^-1 (tau - h)
-    // by a column-oriented forward substitution on the rows still in registers.
+    // ---- A8: Cholesky in registers, legs-first order: M's arrow structure gives L no
+    // left-right-leg block.  Lane i holds row i; each pivot column is broadcast through LDS (one
+    // write, half-wave broadcast reads; same-wave LDS accesses complete in order, so no barrier)
+    // and the rank-1 update is one FMA per trailing entry.  The right-hand side b = tau - h rides
+    // along in the same broadcasts: g = L^-1 b comes out of the same steps.
     {
       float a[18];
       bool nonpd = false;
       const int ol = l < 12 ? 6 + l : l - 12;  // this lane's dof
 #pragma unroll
-      for (int k = 0; k < 18; k++) {
-        const int ok = k < 12 ? 6 + k : k - 12;
-        // M holds the lower triangle in dof order (upper entries are zero)
-        a[k] = (l < 18) ? (ol >= ok ? E.L[l < 18 ? ol : 0][ok] : E.L[ok][l < 18 ? ol : 0]) : 0.f;
-      }
+      for (int k = 0; k < 18; k++) a[k] = (l < nf && k <= l) ? E.L[l < 18 ? l : 0][k] : 0.f;
       float bv = (l < 18) ? (ol >= 6 ? E.tau[(ol >= 6 ? ol : 6) - 6] : 0.f) - E.h[l < 18 ? ol : 0] : 0.f;
       asm volatile("" ::: "memory");
-      // steps 0..5: the left-leg pivot j and the right-leg pivot 6 + j together (the two leg blocks
-      // are independent: a left-leg row has L[.][6 + j] = 0, so its right-pivot multiplier is 0,
-      // and vice versa; base rows take both updates, which commute); steps 6..: base pivots
+      // steps 0..5: the left-leg pivot j and the right-leg pivot 6 + j together (a left-leg row has
+      // L[.][6 + j] = 0, so its right-pivot multiplier is 0, and vice versa; base rows take both
+      // updates, which commute); steps 6..: the base pivots
 #pragma unroll
       for (int j = 0; j < 6; j++) {
         const int j2 = 6 + j;
-        if (l < 18) { E.colbuf[l] = a[j]; E.bbuf[l] = a[j2]; }
-        const float d1 = E.colbuf[j], d2 = E.bbuf[j2];
+        if (l < 18) { E.colbuf[l] = a[j]; E.colbuf2[l] = a[j2]; E.bbuf[l] = bv; }
+        const float d1 = E.colbuf[j], d2 = E.colbuf2[j2], b1 = E.bbuf[j], b2 = E.bbuf[j2];
         nonpd |= !(d1 > 0.f) || !(d2 > 0.f);
         const float inv1 = __builtin_amdgcn_rsqf(fmaxf(d1, 1e-20f));  // 1 / L_jj (1 ulp)
         const float inv2 = __builtin_amdgcn_rsqf(fmaxf(d2, 1e-20f));
-        const float t1 = a[j] * (inv1 * inv1);    // L[l][j] / L[j][j]   (0 on right-leg rows)
-        const float t2 = a[j2] * (inv2 * inv2);   // L[l][j2] / L[j2][j2] (0 on left-leg rows)
-        if (l == 0) { E.invd[j] = inv1; E.invd[j2] = inv2; }
-        a[j] = (lane_opaque(l) >= j) ? a[j] * inv1 : a[j];
-        a[j2] = (lane_opaque(l) >= j2) ? a[j2] * inv2 : a[j2];
+        const float g1 = b1 * inv1, g2 = b2 * inv2;
+        if (l == 0) { E.invd[j] = inv1; E.invd[j2] = inv2; E.gv[j] = g1; E.gv[j2] = g2; }
+        const int lo = lane_opaque(l);
+        const float t1 = lo > j ? a[j] * (inv1 * inv1) : 0.f;     // L[l][j] / L[j][j] (0 on right-leg rows)
+        const float t2 = lo > j2 ? a[j2] * (inv2 * inv2) : 0.f;   // L[l][j2] / L[j2][j2] (0 on left-leg rows)
+        a[j] = lo >= j ? a[j] * inv1 : a[j];
+        a[j2] = lo >= j2 ? a[j2] * inv2 : a[j2];
+        bv -= t1 * b1 + t2 * b2;                                   // b_l -= L[l][j] g_j + L[l][j2] g_j2
 #pragma unroll
         for (int k = j + 1; k < 6; k++) a[k] -= t1 * E.colbuf[k];
 #pragma unroll
-        for (int k = j2 + 1; k < 12; k++) a[k] -= t2 * E.bbuf[k];
+        for (int k = j2 + 1; k < 12; k++) a[k] -= t2 * E.colbuf2[k];
 #pragma unroll
-        for (int k = 12; k < nf; k++) a[k] -= t1 * E.colbuf[k] + t2 * E.bbuf[k];
+        for (int k = 12; k < nf; k++) a[k] -= t1 * E.colbuf[k] + t2 * E.colbuf2[k];
       }
 #pragma unroll
       for (int j = 12; j < nf; j++) {
-        if (l < 18) E.colbuf[l] = a[j];
-        const float d = E.colbuf[j];
+        if (l < 18) { E.colbuf[l] = a[j]; E.bbuf[l] = bv; }
+        const float d = E.colbuf[j], bj = E.bbuf[j];
         nonpd |= !(d > 0.f);
         const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));
-        const float t = a[j] * (inv * inv);
-        if (l == 0) E.invd[j] = inv;
+        const float gj = bj * inv;
+        if (l == 0) { E.invd[j] = inv; E.gv[j] = gj; }
+        const float t = lane_opaque(l) > j ? a[j] * (inv * inv) : 0.f;
         a[j] = (lane_opaque(l) >= j) ? a[j] * inv : a[j];
+        bv -= t * bj;
 #pragma unroll
         for (int k = j + 1; k < nf; k++) a[k] -= t * E.colbuf[k];
       }
-      // g = L^-1 b, column-oriented on the factor's rows (lane i holds L[i][.] in a[]): the two
-      // leg blocks in parallel, then the base rows
-      if (l < 18) E.bbuf[l] = bv;
+      if (l < nf) {
 #pragma unroll
-      for (int j = 0; j < 6; j++) {
-        const int j2 = 6 + j;
-        const float g1 = E.bbuf[j] * E.invd[j], g2 = E.bbuf[j2] * E.invd[j2];
-        if (l == 0) { E.gv[j] = g1; E.gv[j2] = g2; }
-        bv = (lane_opaque(l) > j && (lane_opaque(l) < 6 || lane_opaque(l) >= 12)) ? bv - a[j] * g1 : bv;
-        bv = (lane_opaque(l) > j2) ? bv - a[j2] * g2 : bv;
-        if (l < 18) E.bbuf[l] = bv;
-      }
-#pragma unroll
-      for (int j = 12; j < nf; j++) {
-        const float gj = E.bbuf[j] * E.invd[j];
-        if (l == 0) E.gv[j] = gj;
-        bv = (lane_opaque(l) > j) ? bv - a[j] * gj : bv;
-        if (l < 18) E.bbuf[l] = bv;
-      }
-      if (l < 18) {
-#pragma unroll
-        for (int k = 0; k < 18; k++) E.L[l][k] = (k < nf && l < nf) ? a[k] : 0.f;
+        for (int k = 0; k < 18; k++) E.L[l][k] = a[k];
       }
       if (l == 0 && nonpd) E.bad = 1;
     }
@@ -657,21 +650,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           f3 t1 = ref - dot(ref, cn) * cn;
           t1 = rsqrtf(dot(t1, t1)) * t1;
           const f3 t2 = cross(cn, t1);
-          E.grp[rank].mu = mu;
-#pragma unroll
-          for (int d = 0; d < 3; d++) {
-            const int r = 3 * rank + d;
-            const f3 dir = d == 0 ? cn : (d == 1 ? t1 : t2);
-            st3(E.rd[r], dir);
-            st3(E.u.rg.xP[r], xP);
-            st3(E.u.rg.xN[r], xN);
-            E.rbP[r] = bP; E.rbN[r] = bN;
-            E.rlam[r] = lam_base + d;
-            E.rLam[r] = E.lamst[lam_base + d];
-            E.grp[rank].tgt[d] = d == 0 ? tgt : 0.f;
-            E.grp[rank].lo[d] = d == 0 ? 0.f : -BIG;
-            E.grp[rank].hi[d] = BIG;
-          }
+          // one record per contact (its three rows read it in A10)
+          ContactC& C = E.ct[rank];
+          st3(C.xP, xP); st3(C.xN, xN);
+          st3(C.dir[0], cn); st3(C.dir[1], t1); st3(C.dir[2], t2);
+          C.bP = bP; C.bN = bN; C.lam_base = lam_base;
+          GroupC& G = E.grp[rank];
+          G.mu = mu;
+          G.tgt[0] = tgt; G.tgt[1] = 0.f; G.tgt[2] = 0.f;
+          G.lo[0] = 0.f; G.lo[1] = -BIG; G.lo[2] = -BIG;
+          G.hi[0] = BIG; G.hi[1] = BIG; G.hi[2] = BIG;
         } else {
           E.lamst[lam_base + 0] = E.lamst[lam_base + 1] = E.lamst[lam_base + 2] = 0.f;
         }
@@ -709,29 +697,49 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       float J[18];
 #pragma unroll
       for (int i = 0; i < 18; i++) J[i] = 0.f;
-      if (own) {
-        const int bP = E.rbP[l], bN = E.rbN[l];
-        if (bP < 0) {  // joint row (friction / limit): sign * e_dof
-          const int j = -1 - bP;
+      const int npts_e = E.npts;
+      const bool crow = own && l < 3 * npts_e;   // contact row (else joint friction / limit row)
+      if (own && !crow) {  // joint row: sign * e_dof
+        const int j = -1 - E.rbP[l];
 #pragma unroll
-          for (int jj = 0; jj < 12; jj++) J[6 + jj] = (jj == j) ? E.rd[l][0] : 0.f;
-        } else {       // contact row: J = J_bP(xP) d - J_bN(xN) d
-          const f3 d = ld3(E.rd[l]), xp = ld3(E.u.rg.xP[l]), xn = ld3(E.u.rg.xN[l]);
-          const bool pair2 = bN >= 0;
-          J[0] = pair2 ? 0.f : d.x; J[1] = pair2 ? 0.f : d.y; J[2] = pair2 ? 0.f : d.z;
-          const f3 xd = cross(xp, d) - (pair2 ? cross(xn, d) : mk(0, 0, 0));
-          J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
+        for (int jj = 0; jj < 12; jj++) J[6 + jj] = (jj == j) ? E.rd[l][0] : 0.f;
+      }
+      const int cidx = crow ? l / 3 : 0, cdir = crow ? l % 3 : 0;
+      const ContactC& C = E.ct[cidx];
+      if (crow) {  // J = J_bP(xP) d - J_bN(xN) d
+        const f3 d = ld3(C.dir[cdir]), xp = ld3(C.xP);
+        const int bP = C.bP;
+        const bool pair2 = C.bN >= 0;
+        E.rlam[l] = C.lam_base + cdir;
+        E.rLam[l] = E.lamst[C.lam_base + cdir];
+        J[0] = pair2 ? 0.f : d.x; J[1] = pair2 ? 0.f : d.y; J[2] = pair2 ? 0.f : d.z;
+        const f3 xd = cross(xp, d) - (pair2 ? cross(ld3(C.xN), d) : mk(0, 0, 0));
+        J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
+        // the contact body's leg: links kb0 .. bP (6 at most)
+        const bool right = bP >= 7;
+        const int kb0 = right ? 7 : 1;
 #pragma unroll
-          for (int k = 1; k <= 12; k++) J[5 + k] = chain_term(E, bP, k, xp, d);
+        for (int m = 0; m < 6; m++) {
+          const int k = kb0 + m;
+          const float val = (bP > 0 && k <= bP) ? dot(d, cross(ld3(E.a[k]), xp - ld3(E.o[k]))) : 0.f;
+          J[6 + m] = right ? 0.f : val;
+          J[12 + m] = right ? val : 0.f;
         }
       }
       // the other capsule's chain (self-collision rows), only when the wave has such a row
-      if (__ballot(own && E.rbN[l] >= 0) != 0) {
-        if (own && E.rbN[l] >= 0) {
-          const int bN = E.rbN[l];
-          const f3 d = ld3(E.rd[l]), xn = ld3(E.u.rg.xN[l]);
+      if (__ballot(crow && C.bN >= 0) != 0) {
+        if (crow && C.bN >= 0) {
+          const int bN = C.bN;
+          const f3 d = ld3(C.dir[cdir]), xn = ld3(C.xN);
+          const bool right = bN >= 7;
+          const int kb0 = right ? 7 : 1;
 #pragma unroll
-          for (int k = 1; k <= 12; k++) J[5 + k] -= chain_term(E, bN, k, xn, d);
+          for (int m = 0; m < 6; m++) {
+            const int k = kb0 + m;
+            const float val = k <= bN ? dot(d, cross(ld3(E.a[k]), xn - ld3(E.o[k]))) : 0.f;
+            J[6 + m] -= right ? 0.f : val;
+            J[12 + m] -= right ? val : 0.f;
+          }
         }
       }
 #pragma unroll
@@ -751,9 +759,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
       for (int k = 0; k < 18; k++) v0 += dt * (z[k] * E.gv[k]);
     }
-    __syncthreads();  // every lane's row points are read before Z overwrites them
 #pragma unroll
     for (int k = 0; k < 18; k++) E.u.Z[l][k] = z[k];
+    // the group constants below read the neighbouring lanes' rows: a barrier, not program order
+    // (per lane, Z[l-1] and Z[l] are different addresses the compiler may reorder around)
+    __syncthreads();
     // ---- A11: W = Z^T Z on the matrix cores (v_mfma_f32_32x32x2f32).  MFMA operand i/kk =
     // lane%32 / lane/32, so the wave's two envs are interleaved with v_permlane32_swap:
     // swap(X, Y) -> (X.lo|Y.lo, X.hi|Y.hi) is env 0's / env 1's [32 rows x 2 k] operand, and the
@@ -892,17 +902,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       __syncthreads();
       if (own) {
         E.lamst[E.rlam[l]] = mylam;
-        const int bP = E.rbP[l];
-        if (bP >= 0) {
-          const int bN = E.rbN[l];
+        if (l < 3 * E.npts) {
+          const ContactC& C = E.ct[l / 3];
+          const int bP = C.bP, bN = C.bN;
+          const f3 d = ld3(C.dir[l % 3]);
           const float s = mylam * inv_dt;
-          atomicAdd(&E.cf[bP][0], E.rd[l][0] * s);
-          atomicAdd(&E.cf[bP][1], E.rd[l][1] * s);
-          atomicAdd(&E.cf[bP][2], E.rd[l][2] * s);
+          atomicAdd(&E.cf[bP][0], d.x * s);
+          atomicAdd(&E.cf[bP][1], d.y * s);
+          atomicAdd(&E.cf[bP][2], d.z * s);
           if (bN >= 0) {
-            atomicAdd(&E.cf[bN][0], -E.rd[l][0] * s);
-            atomicAdd(&E.cf[bN][1], -E.rd[l][1] * s);
-            atomicAdd(&E.cf[bN][2], -E.rd[l][2] * s);
+            atomicAdd(&E.cf[bN][0], -d.x * s);
+            atomicAdd(&E.cf[bN][1], -d.y * s);
+            atomicAdd(&E.cf[bN][2], -d.z * s);
           }
         }
       }

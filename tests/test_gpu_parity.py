@@ -351,17 +351,31 @@ def _run_trajectory(fixed, steps, n=16):
 
 
 def test_determinism(env):
-    """Same state + same actions -> bitwise-identical step (no inter-env atomics on the path)."""
+    """Same state + same actions -> bitwise-identical steps (no inter-env atomics on the path, no
+    unsynchronised cross-lane LDS traffic): 10 consecutive steps from one snapshot, twice, with
+    some envs' legs rolled into each other so the self-collision rows are exercised too."""
+    from humanoid import _native as N
+    for _ in range(3):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    torch.cuda.synchronize()
+    env.dof_pos[0:8, 0] = -0.12
+    env.dof_pos[0:8, 6] = 0.12
     S, _, _ = snapshot(env)
-    a = torch.randn(env.num_envs, 12, device="cuda:0")
+    acts = [torch.randn(env.num_envs, 12, device="cuda:0") for _ in range(10)]
+    lam = env._view(N.T["CONTACT_LAMBDA"])
     outs = []
+    pair_slots = slice(24 * 3, 32 * 3)
+    pair_active = False
     for _ in range(2):
-        from humanoid import _native as N
         for k in ("root_states", "dof_pos", "dof_vel", "actions"):
             getattr(env, k).copy_(torch.from_numpy(S[k]).cuda())
-        env._view(N.T["CONTACT_LAMBDA"]).copy_(torch.from_numpy(S["lambda"]).cuda())
-        _step_only(env, a, 999)
-        outs.append((env.dof_pos.cpu().clone(), env.root_states.cpu().clone(), env.contact_forces.cpu().clone()))
+        lam.copy_(torch.from_numpy(S["lambda"]).cuda())
+        for t, a in enumerate(acts):
+            _step_only(env, a, 999 + t)
+            pair_active |= bool((lam[:, pair_slots] != 0).any())
+        outs.append((env.dof_pos.cpu().clone(), env.root_states.cpu().clone(), env.contact_forces.cpu().clone(),
+                     lam.cpu().clone(), env.rigid_state.cpu().clone()))
+    assert pair_active, "no self-collision row was active"
     for x, y in zip(*outs):
         assert torch.equal(x, y)
 
