@@ -346,6 +346,26 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 // value of lane r of this lane's env (lanes 0..31 or 32..63): both reads are scalar, the pick
 // is one v_cndmask (no divergent branch around the convergent readlane)
 #define RL(x, r) hsel(half, readlane_f((x), (r)), readlane_f((x), 32 + (r)))
+// the same broadcast as ONE ds_swizzle (bit mode: and_mask 0, or_mask r — every lane of each
+// 32-lane half reads lane r of its half): no SGPR round trip, no per-env select
+template <int R>
+__device__ __forceinline__ float bcast32(float x) {
+  static_assert(R >= 0 && R < 32, "lane in the half");
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), R << 5));
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+// bcast32 for a row index that is a compile-time constant after unrolling
+__device__ __forceinline__ float swz(float x, int r) {
+  switch (r) {
+#define HG_SWZ(R) case R: return bcast32<R>(x);
+    HG_SWZ(0) HG_SWZ(1) HG_SWZ(2) HG_SWZ(3) HG_SWZ(4) HG_SWZ(5) HG_SWZ(6) HG_SWZ(7) HG_SWZ(8) HG_SWZ(9)
+    HG_SWZ(10) HG_SWZ(11) HG_SWZ(12) HG_SWZ(13) HG_SWZ(14) HG_SWZ(15) HG_SWZ(16) HG_SWZ(17) HG_SWZ(18)
+    HG_SWZ(19) HG_SWZ(20) HG_SWZ(21) HG_SWZ(22) HG_SWZ(23) HG_SWZ(24) HG_SWZ(25) HG_SWZ(26) HG_SWZ(27)
+    HG_SWZ(28) HG_SWZ(29) HG_SWZ(30) HG_SWZ(31)
+#undef HG_SWZ
+    default: return 0.f;
+  }
+}
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 // v_permlane32_swap: x' = (x.lo | z.lo), z' = (x.hi | z.hi)
 __device__ __forceinline__ void swap32(float x, float z, float& xo, float& zo) {
@@ -831,10 +851,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           if (g < ng) {
             const int ra = 3 * g, rb = 3 * g + 1, rc = 3 * g + 2;
             const GroupC& G = E.grp[g];
-            const float va = RL(vrow, ra), vb = RL(vrow, rb);
-            const float vc = rc < RMAX ? RL(vrow, rc < RMAX ? rc : 0) : 0.f;
+            const float va = swz(vrow, ra), vb = swz(vrow, rb);
+            const float vc = rc < RMAX ? swz(vrow, rc < RMAX ? rc : 0) : 0.f;
             const float la = lam[ra], lb = lam[rb], lc = rc < RMAX ? lam[rc < RMAX ? rc : 0] : 0.f;
-            const float na = fminf(fmaxf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0]), G.hi[0]);
+            const float na = clampf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0], G.hi[0]);
             const float da = na - la;
             const float vb1 = vb + G.Wba * da, vc1 = vc + G.Wca * da;
             float db, dc;
@@ -845,18 +865,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
               db = l1 * sc - lb;
               dc = l2 * sc - lc;
             } else if (g >= npts_max) {  // single rows in both envs, in sequence
-              const float nbs = fminf(fmaxf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1]), G.hi[1]);
+              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
               db = nbs - lb;
               const float vc2 = vc1 + G.Wcb * db;
-              dc = fminf(fmaxf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2]), G.hi[2]) - lc;
+              dc = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]) - lc;
             } else {                     // mixed: both, picked per env
               const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
               const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
               const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
-              const float nbs = fminf(fmaxf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1]), G.hi[1]);
+              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
               const float dbs = nbs - lb;
               const float vc2 = vc1 + G.Wcb * dbs;
-              const float ncs = fminf(fmaxf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2]), G.hi[2]);
+              const float ncs = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
               const bool ct = G.contact != 0;
               db = ct ? l1 * sc - lb : dbs;
               dc = ct ? l2 * sc - lc : ncs - lc;

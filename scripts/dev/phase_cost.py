@@ -17,9 +17,9 @@ OUT = os.path.join(REPO, "build", "phase")
 # (name, start marker, end marker): the code between the markers is emitted twice
 PHASES = {
     "kin": ("    // ---- A2..A5:", "    // base totals (lane 0)"),
-    "mchol": ("    for (int i = l; i < 18 * 20; i += 32) (&E.L[0][0])[i] = 0.f;", "    // ---- A9:"),
+    "mchol": ("    // ---- A6/A7:", "    // ---- A9:"),
     "detect": ("    // ---- A9:", "    const int nrows = E.nrows;"),
-    "jz": ("    // ---- A10:", "    // ---- A11:"),
+    "jz": ("    // ---- A10:", "    // the group constants below read"),
     "grpc": ("    // ---- A12:", "    // ---- A13:"),
 }
 
