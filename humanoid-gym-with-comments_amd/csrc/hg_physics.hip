@@ -340,14 +340,8 @@ __device__ __forceinline__ void mat_to_quat(const float* m, float* q) {
   if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
 }
 
-__device__ __forceinline__ float readlane_f(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-// value of lane r of this lane's env (lanes 0..31 or 32..63): both reads are scalar, the pick
-// is one v_cndmask (no divergent branch around the convergent readlane)
-#define RL(x, r) hsel(half, readlane_f((x), (r)), readlane_f((x), 32 + (r)))
-// the same broadcast as ONE ds_swizzle (bit mode: and_mask 0, or_mask r — every lane of each
-// 32-lane half reads lane r of its half): no SGPR round trip, no per-env select
+// the value of lane R of this lane's 32-lane env half as ONE ds_swizzle (bit mode: and_mask 0,
+// or_mask R): no SGPR round trip, no per-env select
 template <int R>
 __device__ __forceinline__ float bcast32(float x) {
   static_assert(R >= 0 && R < 32, "lane in the half");
@@ -373,7 +367,6 @@ __device__ __forceinline__ void swap32(float x, float z, float& xo, float& zo) {
   xo = __uint_as_float(r[0]);
   zo = __uint_as_float(r[1]);
 }
-__device__ __forceinline__ float hsel(int half, float lo, float hi) { return half ? hi : lo; }
 // the lane index through an empty volatile asm: lane masks built from it are recomputed where
 // they are used (one v_cmp) instead of being hoisted out of the substep loop into SGPR pairs
 // that spill to VGPR lanes (two v_readlane per restore)
@@ -442,7 +435,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const float prev = S.actions[l * np + e];
     a = (1.0f - delay) * a + delay * prev;
     a += cfg->dynamic_randomization * z * a;
-    a = fminf(fmaxf(a, -cfg->clip_actions), cfg->clip_actions);
+    a = clampf(a, -cfg->clip_actions, cfg->clip_actions);
     E.act[l] = a;
     if (valid) S.actions[l * np + e] = a;
     E.q[l] = S.dof_pos[l * np + e];
@@ -476,7 +469,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (l < 12) {
       const float t = E.pd_kp[l] * (E.pd_tgt[l] - E.q[l]) - E.pd_kd[l] * E.qd[l];
       const float lim = E.pd_lim[l];
-      E.tau[l] = fminf(fmaxf(t, -lim), lim);
+      E.tau[l] = clampf(t, -lim, lim);
       const bool sat = t < -lim || t > lim;
       E.madd[l] = M->armature[l + 1] + (sat ? 0.f : dt * E.pd_kd[l]);
       E.nu[6 + l] = E.qd[l];
@@ -777,7 +770,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         z[k] = s * E.invd[k];
       }
 #pragma unroll
-      for (int k = 0; k < 18; k++) v0 += dt * (z[k] * E.gv[k]);
+      for (int k = 0; k < nf; k++) v0 += dt * (z[k] * E.gv[k]);  // gv[k >= nf] is never written (fixed base)
     }
 #pragma unroll
     for (int k = 0; k < 18; k++) E.u.Z[l][k] = z[k];
@@ -805,6 +798,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     float wrow[RMAX];
 #pragma unroll
     for (int m = 0; m < RMAX; m++) wrow[m] = (m % 8 < 4) ? wA[4 * (m / 8) + m % 8] : wB[4 * (m / 8) + m % 8 - 4];
+    // warm-start impulses, replicated in every lane of the env (uniform per half-wave)
+    float lam[RMAX];
+#pragma unroll
+    for (int m = 0; m < RMAX; m++) lam[m] = m < nrows ? E.rLam[m] : 0.f;
     // ---- A12: group constants (1/W_rr and the in-group couplings z_r . z_{r-1}, z_r . z_{r-2}
     // from the Z rows in LDS), warm-started row velocities
     {
@@ -823,8 +820,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       if (l == 31) { E.grp[10].invD[2] = 0.f; E.grp[10].Wca = 0.f; E.grp[10].Wcb = 0.f; }  // virtual slot 32
       float v = v0;
 #pragma unroll
-      for (int m = 0; m < RMAX; m++)
-        if (m < nrows) v += wrow[m] * E.rLam[m];
+      for (int m = 0; m < RMAX; m++) v += wrow[m] * lam[m];
       v0 = own ? v : 0.f;
     }
     __syncthreads();
@@ -838,9 +834,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // then every row velocity takes the group's three updates (one FMA each).  Branch-free over
     // the group kinds; groups empty in both envs of the wave are skipped (scalar branch).
     {
-      float lam[RMAX];
-#pragma unroll
-      for (int m = 0; m < RMAX; m++) lam[m] = m < nrows ? E.rLam[m] : 0.f;
       float vrow = v0;
       const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;
       const int npts_min = min(shm[0].npts, shm[1].npts), npts_max = max(shm[0].npts, shm[1].npts);
@@ -906,7 +899,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       }
 #pragma unroll
       for (int j = nf - 1; j >= 0; j--) {
-        const float xj = RL(y, j) * E.invd[j];
+        const float xj = swz(y, j) * E.invd[j];
         const int lo = (j >= 6 && j < 12) ? 6 : 0;  // a right-leg column has no left-leg rows
         y = (l == j) ? xj : ((l >= lo && l < j) ? y - E.L[j][l < 18 ? l : 0] * xj : y);
       }
