@@ -279,13 +279,13 @@ int hg_tensor(void* sim, int id, hg_desc* d) {
     case HG_T_EP_STATS_RING:
       d->ndim = 2; d->shape[0] = HG_EP_RING; d->shape[1] = 24; d->strides[0] = 24; d->strides[1] = 1;
       return HG_OK;
-    case HG_T_CONTACT_FORCES:  // AoS [N,13,3], contiguous like the reference's net_contact_force view
+    case HG_T_CONTACT_FORCES:  // [N,13,3] (net_contact_force's shape), SoA storage
       d->ndim = 3; d->shape[0] = n; d->shape[1] = HG_NB; d->shape[2] = 3;
-      d->strides[0] = HG_NB * 3; d->strides[1] = 3; d->strides[2] = 1;
+      d->strides[0] = 1; d->strides[1] = 3 * np; d->strides[2] = np;
       return HG_OK;
-    case HG_T_RIGID_STATE:     // AoS [N,13,13], contiguous like rigid_body_state.view(N,-1,13)
+    case HG_T_RIGID_STATE:     // [N,13,13] (rigid_body_state.view(N,-1,13)'s shape), SoA storage
       d->ndim = 3; d->shape[0] = n; d->shape[1] = HG_NB; d->shape[2] = 13;
-      d->strides[0] = HG_NB * 13; d->strides[1] = 13; d->strides[2] = 1;
+      d->strides[0] = 1; d->strides[1] = 13 * np; d->strides[2] = np;
       return HG_OK;
     case HG_T_EPISODE_SUMS:
       d->ndim = 2; d->shape[0] = HG_NUM_REWARDS; d->shape[1] = n; d->strides[0] = np; d->strides[1] = 1;

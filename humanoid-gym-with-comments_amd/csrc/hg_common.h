@@ -19,8 +19,8 @@ struct HgState {
   float* root;        // [13][np]
   float* dof_pos;     // [12][np]
   float* dof_vel;     // [12][np]
-  float* contact;     // [n][13][3]  AoS (reference layout, coalesced per-env stores from K_step)
-  float* rigid;       // [n][13][13] AoS
+  float* contact;     // [13*3][np] SoA
+  float* rigid;       // [13*13][np] SoA
   float* torques;     // [12][np]
   float* actions;     // [12][np]
   float* last_actions;
@@ -61,8 +61,10 @@ struct HgState {
   const hg_model* model;  // device copy
 };
 
-#define HG_CF(S, e, b, i) ((S).contact[(size_t)(e) * (HG_NB * 3) + (b) * 3 + (i)])
-#define HG_RS(S, e, b, f) ((S).rigid[(size_t)(e) * (HG_NB * 13) + (b) * 13 + (f)])
+// contact forces / rigid states are SoA too (field-major, [b*3+i][np] and [b*13+f][np]); the torch
+// views keep the reference's [N,13,3] / [N,13,13] shapes with strides (1, 3 np, np) / (1, 13 np, np)
+#define HG_CF(S, e, b, i) ((S).contact[(size_t)((b) * 3 + (i)) * (S).np + (e)])
+#define HG_RS(S, e, b, f) ((S).rigid[(size_t)((b) * 13 + (f)) * (S).np + (e)])
 
 // ------------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. SC'11).  Keyed by the run seed; counter = (a, b, c, purpose).

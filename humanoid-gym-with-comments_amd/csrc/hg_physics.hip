@@ -983,8 +983,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   __syncthreads();
   kin_scan(E, M, l, gz, false);
   __syncthreads();
-  // stage the [13][13] rigid states and [13][3] contact forces in LDS, then store each env's
-  // rows as one contiguous run (AoS, the reference's tensor layout)
+  // stage the [13][13] rigid states and [13][3] contact forces in LDS, then store them as SoA rows
   if (l < 13) {
     const int b = l;
     float qq[4];
@@ -1011,10 +1010,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (l < 12) S.dof_vel[l * np + e] = 0.f;
     return;
   }
-  float* rs = &HG_RS(S, e, 0, 0);
-  for (int i = l; i < 13 * 13; i += 32) rs[i] = E.u.out.rigid[i];
-  float* cfo = &HG_CF(S, e, 0, 0);
-  for (int i = l; i < 13 * 3; i += 32) cfo[i] = E.u.out.cf[i];
+  // SoA rows: each store instruction writes 32 fields x the wave's two adjacent envs; the
+  // XCD-aware env mapping keeps a line's 32 envs on one L2, where the pieces merge
+  for (int i = l; i < 13 * 13; i += 32) S.rigid[(size_t)i * np + e] = E.u.out.rigid[i];
+  for (int i = l; i < 13 * 3; i += 32) S.contact[(size_t)i * np + e] = E.u.out.cf[i];
   if (l < 13) S.root[l * np + e] = E.root[l];
   if (l < 12) {
     S.dof_pos[l * np + e] = E.q[l];

@@ -148,8 +148,8 @@ enum hg_tensor_id {
   HG_T_ROOT_STATE = 0,   /* [N,13] pos3 quat(xyzw)4 linvel3 angvel3, world   (actor_root_state) */
   HG_T_DOF_POS,          /* [N,D]                                            (dof_state[...,0]) */
   HG_T_DOF_VEL,          /* [N,D]                                            (dof_state[...,1]) */
-  HG_T_CONTACT_FORCES,   /* [N,B,3] net contact force per body, world        (net_contact_force) */
-  HG_T_RIGID_STATE,      /* [N,B,13] per-body pos quat linvel angvel         (rigid_body_state) */
+  HG_T_CONTACT_FORCES,   /* [N,B,3] net contact force per body, world, SoA strides (1,3np,np) (net_contact_force) */
+  HG_T_RIGID_STATE,      /* [N,B,13] per-body pos quat linvel angvel, SoA strides (1,13np,np) (rigid_body_state) */
   HG_T_TORQUES,          /* [N,D] last applied torques                       (self.torques) */
   HG_T_ACTIONS, HG_T_LAST_ACTIONS, HG_T_LAST_LAST_ACTIONS,
   HG_T_LAST_DOF_VEL, HG_T_LAST_ROOT_VEL,
