@@ -49,8 +49,7 @@ struct Gait { float sin_pos, cos_pos, stance[2]; };
 __device__ Gait gait(const hg_cfg* cfg, int64_t ep) {
   float phase = (float)ep * cfg->dt / cfg->cycle_time;
   Gait g;
-  g.sin_pos = sinf(kTwoPiF * phase);
-  g.cos_pos = cosf(kTwoPiF * phase);
+  sincosf(kTwoPiF * phase, &g.sin_pos, &g.cos_pos);  // one argument reduction for both
   g.stance[0] = g.sin_pos >= 0.f ? 1.f : 0.f;
   g.stance[1] = g.sin_pos < 0.f ? 1.f : 0.f;
   if (fabsf(g.sin_pos) < 0.1f) g.stance[0] = g.stance[1] = 1.f;
@@ -446,6 +445,9 @@ __global__ void __launch_bounds__(64) k_post(HgState S, uint64_t counter, int mo
   }
 }
 
+#ifndef HG_POST_PEB
+#define HG_POST_PEB 16
+#endif
 // K_post for a policy step (mode 0 of k_post, same arithmetic in the same order; exponentials by
 // the hardware exp, __expf, within the reward tolerance).
 //
@@ -466,7 +468,8 @@ __global__ void __launch_bounds__(64) k_post(HgState S, uint64_t counter, int mo
 //   O  observation / privileged frames built in LDS by joint and field groups, then written out
 //      row-major with coalesced float4 stores; the last_* copies.
 namespace {
-constexpr int PEB = 64;     // envs per block (one per lane)
+constexpr int PEB = HG_POST_PEB;  // envs per block: lanes 0..PEB-1 of every wave, one env each
+static_assert(PEB == 16 || PEB == 32 || PEB == 64, "envs per block");
 constexpr int PWAVES = 8;   // waves per block
 // LDS slots ([slot][64] floats; ints stored through their bit patterns)
 enum PostSlot {
@@ -495,19 +498,9 @@ __device__ __forceinline__ float dist_term(float dx, float dy, float lo, float h
   const float dmax = fminf(fmaxf(d - hi, 0.f), 0.5f);
   return (__expf(-fabsf(dmin) * 100.f) + __expf(-fabsf(dmax) * 100.f)) / 2.f;
 }
-// sum over the 64 lanes of a wave (every lane active), returned in every lane
-__device__ __forceinline__ float wave_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)); // row_half_mirror
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)); // row_mirror
-  const int b = __float_as_int(v);  // the four 16-lane row sums
-  return (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
-         (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
-}
 }  // namespace
 
-__global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_cfg C, uint64_t counter,
+__global__ void __launch_bounds__(64 * PWAVES) k_post_step(HgState S, const hg_cfg C, uint64_t counter,
                                                               float* __restrict__ frame_obs, float* __restrict__ frame_priv) {
   __shared__ float xs[X_NSLOT * PEB];
   __shared__ float fo[PEB * HG_OBS1];
@@ -517,9 +510,13 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
   const int t = threadIdx.x, l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform job index
   const int np = S.np, n = S.n;
-  const int e0 = blockIdx.x * PEB;
-  const int e = e0 + l;
-  const bool valid = e < n;
+  // XCD-aware: consecutive env groups on one XCD (block b runs on XCD b % 8), so the SoA lines two
+  // groups share (PEB < 32: 4 PEB bytes per row) are fetched through one L2
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
+  const int e0 = (xcd * (nb >> 3) + min(xcd, nb & 7) + kx) * PEB;
+  const bool lane_ok = l < PEB;
+  const int e = e0 + (lane_ok ? l : PEB - 1);
+  const bool valid = lane_ok && e < n;
   const int ec = min(e, n - 1);  // clamped: loads of the padding lanes stay in bounds
   const int nv = min(PEB, n - e0);
 #define X(slot) xs[(slot) * PEB + l]
@@ -537,13 +534,13 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
       const float4* src = reinterpret_cast<const float4*>(S.obs_noise + (size_t)e0 * 48);
 #pragma unroll
       for (int i = 0; i < 2; i++) {
-        const int q = t + i * PEB * PWAVES;
+        const int q = t + i * 64 * PWAVES;
         nz[i] = q < nv * 12 ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       ready = *S.noise_counter == counter;
     }
     float v[24];
-    switch (w) {
+    if (lane_ok) switch (w) {
       case 0:
 #pragma unroll
         for (int i = 0; i < 13; i++) v[i] = ld(S.root, i);
@@ -613,7 +610,7 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
     // noise: float4 q of the block is env q / 12, components 4 (q % 12) ..
 #pragma unroll
     for (int i = 0; i < 2; i++) {
-      const int q = t + i * PEB * PWAVES;
+      const int q = t + i * 64 * PWAVES;
       if (q < PEB * 12) {
         const int qe = q / 12, qq = q % 12;
         float* z = &xs[(X_NOISE + 4 * qq) * PEB + qe];
@@ -903,15 +900,19 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
 
   // ---------------- R: reset_idx (:1109-1163) for the resetting lanes, one field group per wave
   const bool any_reset = __builtin_amdgcn_ballot_w64(valid && do_reset) != 0;  // wave-uniform
-  if (w == 6 && any_reset) {  // episode sums -> this block's statistics (every lane takes part)
-    for (int k = 0; k < HG_NUM_REWARDS; k++) {
-      const float v = (valid && do_reset) ? X(X_ES + k) : 0.f;
-      const float tot = wave_sum(v);
-      if (l == 0) acc_sh[k] = tot;
-      if (valid && do_reset) S.ep_sums[(size_t)k * np + e] = 0.f;
+  if (w == 6 && any_reset) {  // episode sums -> this block's statistics: lane k sums term k over the resetting envs
+    if (l <= HG_NUM_REWARDS) {
+      float tot = 0.f;
+      for (int i = 0; i < nv; i++) {
+        const bool r = xs[X_RESET * PEB + i] != 0.f;
+        tot += r ? (l < HG_NUM_REWARDS ? xs[(X_ES + l) * PEB + i] : 1.f) : 0.f;
+      }
+      acc_sh[l] = tot;
     }
-    const float cnt = wave_sum((valid && do_reset) ? 1.f : 0.f);
-    if (l == 0) acc_sh[HG_NUM_REWARDS] = cnt;
+    if (valid && do_reset) {
+#pragma unroll
+      for (int k = 0; k < HG_NUM_REWARDS; k++) S.ep_sums[(size_t)k * np + e] = 0.f;
+    }
   }
   if (valid) {
     if (w == 7) {  // the reward: the waves' partials in wave order
@@ -984,11 +985,6 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
           else dofs(6);
           break;
         }
-        case 3: case 4: {  // warm-start impulses
-          const int r0 = (w - 3) * (HG_LAMW / 2);
-          for (int r = r0; r < r0 + HG_LAMW / 2; r++) S.lambda[(size_t)r * np + e] = 0.f;
-          break;
-        }
         case 5: {  // _resample_commands (salt 1); the step's heading command stays in slot 2 or 3
           const u4 r = rng4(cfg, e, counter, 1, RNG_CMD);
           float cmd[4] = {0.f, 0.f, X(X_CMD2 + 2), X(X_CMD2 + 3)};
@@ -1016,6 +1012,14 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
         default:
           break;
       }
+    }
+  }
+  if ((w == 3 || w == 4) && any_reset) {  // warm-start impulses: lane -> (env l % PEB, row group l / PEB)
+    constexpr int G = 64 / PEB;                // row groups per wave
+    const int ei = l % PEB, g = l / PEB;
+    const int er = e0 + ei;
+    if (er < n && xs[X_RESET * PEB + ei] != 0.f) {
+      for (int r = (w - 3) * G + g; r < HG_LAMW; r += 2 * G) S.lambda[(size_t)r * np + er] = 0.f;
     }
   }
   lds_barrier();
@@ -1103,14 +1107,14 @@ __global__ void __launch_bounds__(PEB * PWAVES) k_post_step(HgState S, const hg_
   {
     float* go = frame_obs + (size_t)e0 * HG_OBS1;
     float* gp = frame_priv + (size_t)e0 * HG_PRIV1;
-    if (nv == PEB) {  // 16-byte aligned (arena offsets are 256-aligned; 64 * 47 * 4 and 64 * 73 * 4 are multiples of 16)
-      for (int q = t; q < PEB * HG_OBS1 / 4; q += PEB * PWAVES)
+    if (nv == PEB) {  // 16-byte aligned (arena offsets are 256-aligned; 16 * 47 * 4 and 16 * 73 * 4 are multiples of 16)
+      for (int q = t; q < PEB * HG_OBS1 / 4; q += 64 * PWAVES)
         reinterpret_cast<float4*>(go)[q] = reinterpret_cast<const float4*>(fo)[q];
-      for (int q = t; q < PEB * HG_PRIV1 / 4; q += PEB * PWAVES)
+      for (int q = t; q < PEB * HG_PRIV1 / 4; q += 64 * PWAVES)
         reinterpret_cast<float4*>(gp)[q] = reinterpret_cast<const float4*>(fp)[q];
     } else {
-      for (int q = t; q < nv * HG_OBS1; q += PEB * PWAVES) go[q] = fo[q];
-      for (int q = t; q < nv * HG_PRIV1; q += PEB * PWAVES) gp[q] = fp[q];
+      for (int q = t; q < nv * HG_OBS1; q += 64 * PWAVES) go[q] = fo[q];
+      for (int q = t; q < nv * HG_PRIV1; q += 64 * PWAVES) gp[q] = fp[q];
     }
   }
 #undef X
@@ -1167,7 +1171,7 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
                               float inv_len_s, int ep_slot, hipStream_t stream) {
   const int n = S->n;
   if (mode == 0)
-    hipLaunchKernelGGL(k_post_step, dim3((n + PEB - 1) / PEB), dim3(PEB * PWAVES), 0, stream, *S, *hcfg, counter,
+    hipLaunchKernelGGL(k_post_step, dim3((n + PEB - 1) / PEB), dim3(64 * PWAVES), 0, stream, *S, *hcfg, counter,
                        frame_obs, frame_priv);
   else
     hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
