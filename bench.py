@@ -117,7 +117,7 @@ def active_rows(env):
     return float((3 * contacts + limits).mean().item())
 
 
-def make_env(num_envs, device, seed, terrain="plane", push_curriculum=False):
+def make_env(num_envs, device, seed, terrain="plane", push_curriculum=False, env_offset=0, num_envs_total=None):
     from humanoid.envs import XBotLCfg
     from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
     from humanoid.utils.helpers import SimParams
@@ -127,6 +127,8 @@ def make_env(num_envs, device, seed, terrain="plane", push_curriculum=False):
     cfg.terrain.mesh_type = terrain
     cfg.terrain.seed = 5  # identical heightfield on every rank
     cfg.domain_rand.push_curriculum = push_curriculum
+    cfg.env.env_offset = env_offset          # this rank's shard of the global envs
+    cfg.env.num_envs_total = num_envs_total
     return XBotLFreeEnv(cfg, SimParams(), "hg_sim", device, True)
 
 
@@ -232,12 +234,15 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = f"cuda:{local}"
-    torch.manual_seed(5 + rank)
-    np.random.seed(5 + rank)
+    # one seed for every rank: the env draws and the action noise are keyed by the global env id
+    # (rank r holds envs [r * envs, (r + 1) * envs)), so N ranks run the single N * envs job, split
+    torch.manual_seed(5)
+    np.random.seed(5)
     from humanoid.algo.ppo import OnPolicyRunner
     from humanoid.utils.blas_tuning import use_tuned_gemms
     tuned = use_tuned_gemms() if not args.no_gemm_table else False
-    env = make_env(args.envs, device, seed=5 + rank, terrain=args.terrain, push_curriculum=c5)
+    env = make_env(args.envs, device, seed=5, terrain=args.terrain, push_curriculum=c5, env_offset=rank * args.envs,
+                   num_envs_total=world * args.envs)
     runner = OnPolicyRunner(env, train_cfg(args.T, "bf16" if c5 else "fp32", "fp16" if c5 else "fp32"),
                             log_dir=None, device=device)
     timer = KernelTimer(every=int(os.environ.get("HG_TIMER_EVERY", "4")))

@@ -97,7 +97,7 @@ __host__ __device__ inline float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 __host__ __device__ inline float u01_open0(uint32_t x) { return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f); }
 
 __device__ inline u4 rng4(const hg_cfg* cfg, uint32_t env, uint64_t step, uint32_t block, uint32_t purpose) {
-  u4 c = {env, (uint32_t)step, (block & 0xFFFFu) | ((uint32_t)(step >> 32) << 16), purpose};
+  u4 c = {env + (uint32_t)cfg->env_offset, (uint32_t)step, (block & 0xFFFFu) | ((uint32_t)(step >> 32) << 16), purpose};
   return philox4x32_10(c, (uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32));
 }
 

@@ -390,13 +390,6 @@ __device__ __forceinline__ void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3& c1, f3& 
   c2 = p2 + t * d2;
 }
 
-// d . (a_k x (x - o_k)) for every joint k on body b's chain (k in 1..12), 0 elsewhere
-__device__ __forceinline__ float chain_term(const EnvSh& E, int b, int k, f3 x, f3 d) {
-  const int lo = b >= 7 ? 7 : 1;
-  const bool anc = b > 0 && k >= lo && k <= b && (k <= 6) == (b <= 6);
-  return anc ? dot(d, cross(ld3(E.a[k]), x - ld3(E.o[k]))) : 0.f;
-}
-
 }  // namespace
 
 // FIXED = asset.fix_base_link, a compile-time constant so the factorised size and every

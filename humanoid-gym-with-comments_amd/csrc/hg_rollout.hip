@@ -53,8 +53,8 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
                                             int64_t cobs_w, float* __restrict__ act_out, float* __restrict__ logp_out,
                                             float* __restrict__ mu_out, float* __restrict__ sigma_out,
                                             float* __restrict__ value_out, OT* __restrict__ obs_out,
-                                            OT* __restrict__ cobs_out, uint64_t seed, uint64_t counter,
-                                            int env_blocks, int vec) {
+                                            OT* __restrict__ cobs_out, int row_offset, uint64_t seed,
+                                            uint64_t counter, int env_blocks, int vec) {
   if ((int)blockIdx.x < env_blocks) {
     const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
     if (A <= ACT_LANES) {
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
       float term = 0.f;
       if (j < A) {
         float z4[4];
-        normals4(philox_key(seed, (uint32_t)e, counter, (uint32_t)(j >> 2)), z4);
+        normals4(philox_key(seed, (uint32_t)(e + row_offset), counter, (uint32_t)(j >> 2)), z4);
         const float z = (j & 3) == 0 ? z4[0] : (j & 3) == 1 ? z4[1] : (j & 3) == 2 ? z4[2] : z4[3];
         const float m = mean[(size_t)e * A + j], s = std[j];
         const float a = m + s * z;
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
     float lp = 0.f;
     float z4[4];
     for (int j = 0; j < A; j++) {
-      if ((j & 3) == 0) normals4(philox_key(seed, (uint32_t)e, counter, (uint32_t)(j >> 2)), z4);
+      if ((j & 3) == 0) normals4(philox_key(seed, (uint32_t)(e + row_offset), counter, (uint32_t)(j >> 2)), z4);
       const float m = mean[(size_t)e * A + j], s = std[j];
       const float a = m + s * z4[j & 3];
       const float d = a - m;
@@ -142,7 +142,7 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
                               const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
                               int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
                               float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out,
-                              int obs_fp16, uint64_t seed, uint64_t counter, void* stream) {
+                              int obs_fp16, int row_offset, uint64_t seed, uint64_t counter, void* stream) {
   if (!mean || !std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out ||
       !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 ||
       (critic_obs_width > 0 && (!critic_obs || !critic_obs_out)))
@@ -159,12 +159,12 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
     hipLaunchKernelGGL(k_act<__half>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
                        critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
                        actions_out, logp_out, mu_out, sigma_out, value_out, (__half*)obs_out,
-                       (__half*)critic_obs_out, seed, counter, env_blocks, vec);
+                       (__half*)critic_obs_out, row_offset, seed, counter, env_blocks, vec);
   else
     hipLaunchKernelGGL(k_act<float>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
                        critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
                        actions_out, logp_out, mu_out, sigma_out, value_out, (float*)obs_out, (float*)critic_obs_out,
-                       seed, counter, env_blocks, vec);
+                       row_offset, seed, counter, env_blocks, vec);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 

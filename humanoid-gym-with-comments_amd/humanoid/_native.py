@@ -72,7 +72,7 @@ class HgCfg(ctypes.Structure):
         ("feet_body", i32 * 2), ("knee_body", i32 * 2), ("ref_idx", i32 * 6), ("yaw_roll_idx", i32 * 4),
         ("seed", ctypes.c_uint64),
         ("curriculum", i32), ("terrain_rows", i32), ("terrain_cols", i32), ("terrain_env_length", f32),
-        ("max_episode_length_s", f32), ("_pad0", i32), ("terrain_origins", ctypes.c_void_p),
+        ("max_episode_length_s", f32), ("env_offset", i32), ("terrain_origins", ctypes.c_void_p),
     ]
 
 
@@ -157,7 +157,8 @@ def load_library(path=LIB_PATH):
     L.hg_kl_lr_rule.argtypes = [vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.hg_rollout_act.restype = ctypes.c_int
     L.hg_rollout_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
-                                 vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+                                 vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                 vp]
     L.hg_ep_stats_slot.restype = ctypes.c_int
     L.hg_ep_stats_slot.argtypes = [vp]
     L.hg_gather_rows.restype = ctypes.c_int

@@ -67,6 +67,9 @@ class OnPolicyRunner:
         obs_dtype = {"fp32": torch.float32, "fp16": torch.float16}[self.cfg.get("storage_obs_dtype", "fp32")]
         self.alg.init_storage(env.num_envs, self.num_steps_per_env, [env.num_obs], [env.num_privileged_obs],
                               [env.num_actions], obs_dtype=obs_dtype)
+        # the action noise is keyed by the global env id of each storage row
+        env_cfg = getattr(getattr(env, "cfg", None), "env", None)
+        self.alg.row_offset = int(getattr(env_cfg, "env_offset", 0) or 0)
         self.log_dir = log_dir if _rank() == 0 else None
         self.writer = None
         self.tot_timesteps = 0

@@ -95,6 +95,9 @@ class PPO:
         # fused rollout-storage writes on the device (hg_rollout_act / hg_rollout_env); the
         # action noise is Philox keyed by this seed (drawn from torch's generator) and a counter
         self.use_fused_rollout = True
+        # global id of storage row 0 (data parallel: the runner sets the env shard's offset), so the
+        # action noise of a sharded run is the single run's
+        self.row_offset = 0
         # the minibatch loss and its gradient on the fused HIP kernels (hg_loss.py); the symmetry
         # loss configuration keeps the op-by-op expression
         self.use_fused_loss = True
@@ -184,7 +187,7 @@ class PPO:
             p(st.actions[t]), p(st.actions_log_prob[t]), p(st.mu[t]), p(st.sigma[t]),
             p(st.values[t]) if value is not None else None,
             p(st.observations[t]), p(priv[t]) if priv is not None else None,
-            int(st.observations.dtype == torch.float16), ctypes.c_uint64(self._rollout_seed),
+            int(st.observations.dtype == torch.float16), int(self.row_offset), ctypes.c_uint64(self._rollout_seed),
             ctypes.c_uint64(self._rollout_counter), s))
         self._rollout_counter += 1
         tr.actions = st.actions[t]
@@ -450,6 +453,10 @@ class PPO:
         mean_surrogate_loss /= num_updates
         mean_base_lin_vel_loss /= num_updates
         self.storage.clear()
+        # release the last minibatch's autograd graph (ac.distribution holds its mean): a graph kept
+        # alive pins each parameter's AccumulateGrad node to the stream it was created on, and the
+        # captured update (another stream) would then accumulate across streams
+        self.actor_critic.distribution = None
         return mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss
 
     # ------------------------------------------------------------------------------------------

@@ -30,6 +30,12 @@ class XBotLCfg(BaseConfig):
         episode_length_s = 24
         use_ref_actions = False
         num_observation_history_len = 1
+        # data parallel (new): this shard holds global envs [env_offset, env_offset +
+        # num_envs) of num_envs_total (None: num_envs).  Philox draws, plane-grid origins, terrain
+        # levels / types and the creation-time DR are functions of the global env id, so a sharded
+        # run is the single run on num_envs_total envs, split.
+        env_offset = 0
+        num_envs_total = None
 
     class safety:
         pos_limit = 1.0

@@ -121,6 +121,7 @@ def build_hg_cfg(cfg, num_envs, sim_dt, seed, model_js, heightfield=None, hf_sha
     for k, n in enumerate(["left_leg_roll_joint", "left_leg_yaw_joint", "right_leg_roll_joint", "right_leg_yaw_joint"]):
         c.yaw_roll_idx[k] = idx[n]
     c.seed = seed & 0xFFFFFFFFFFFFFFFF
+    c.env_offset = int(getattr(cfg.env, "env_offset", 0))
     c.max_episode_length_s = cfg.env.episode_length_s
     c.terrain_env_length = cfg.terrain.terrain_length
     if terrain_origins is not None and cfg.terrain.curriculum:
@@ -291,8 +292,27 @@ class XBotLFreeEnv(BaseTask):
         self._ep_ring = self._view(T["EP_STATS_RING"])
         self.nonfinite_count = self._view(T["NONFINITE"])
 
+    def _global_ids(self):
+        """(offset, total): this shard's envs are global ids [offset, offset + num_envs) of total."""
+        off = int(getattr(self.cfg.env, "env_offset", 0))
+        total = getattr(self.cfg.env, "num_envs_total", None)
+        total = self.num_envs if total is None else int(total)
+        if off < 0 or off + self.num_envs > total:
+            raise ValueError(f"env shard [{off}, {off + self.num_envs}) outside num_envs_total={total}")
+        return off, total
+
+    def _creation_generator(self, stream):
+        """Creation-time draws over ALL global envs from a private generator keyed by the run seed
+        (the same on every rank), sliced to this shard; the global torch / numpy state is untouched."""
+        g = torch.Generator()
+        g.manual_seed((int(getattr(self.cfg, "seed", 5)) * 1000003 + stream) & 0x7FFFFFFFFFFFFFFF)
+        return g
+
     def _get_env_origins(self):
-        """Env origins (humanoid_env.py:586-611): terrain platforms, or a grid on the plane."""
+        """Env origins (humanoid_env.py:586-611): terrain platforms, or a grid on the plane, as
+        functions of the global env id."""
+        off, total = self._global_ids()
+        gid = torch.arange(off, off + self.num_envs)
         if self.custom_origins:
             max_init_level = self.cfg.terrain.max_init_terrain_level
             if not self.cfg.terrain.curriculum:
@@ -300,33 +320,38 @@ class XBotLFreeEnv(BaseTask):
             # levels/types live in the arena (int32): K_post's reset applies the curriculum
             self.terrain_levels = self._view(N.T["TERRAIN_LEVEL"])
             self.terrain_types = self._view(N.T["TERRAIN_TYPE"])
-            self.terrain_levels[:] = torch.randint(0, max_init_level + 1, (self.num_envs,), device=self.device).to(torch.int32)
-            self.terrain_types[:] = torch.div(torch.arange(self.num_envs, device=self.device),
-                                              (self.num_envs / self.cfg.terrain.num_cols), rounding_mode="floor").to(torch.int32)
+            levels = torch.randint(0, max_init_level + 1, (total,), generator=self._creation_generator(1))
+            self.terrain_levels[:] = levels[off:off + self.num_envs].to(self.device, torch.int32)
+            self.terrain_types[:] = torch.div(gid, (total / self.cfg.terrain.num_cols),
+                                              rounding_mode="floor").to(self.device, torch.int32)
             self.max_terrain_level = self.cfg.terrain.num_rows
             self.env_origins[:] = self.terrain_origins[self.terrain_levels.long(), self.terrain_types.long()]
         else:
-            num_cols = np.floor(np.sqrt(self.num_envs))
-            num_rows = np.ceil(self.num_envs / num_cols)
+            num_cols = np.floor(np.sqrt(total))
+            num_rows = np.ceil(total / num_cols)
             xx, yy = torch.meshgrid(torch.arange(num_rows), torch.arange(num_cols), indexing="ij")
             sp = self.cfg.env.env_spacing
-            self.env_origins[:, 0] = (sp * xx.flatten()[:self.num_envs]).to(self.device)
-            self.env_origins[:, 1] = (sp * yy.flatten()[:self.num_envs]).to(self.device)
+            self.env_origins[:, 0] = (sp * xx.flatten()[gid]).to(self.device)
+            self.env_origins[:, 1] = (sp * yy.flatten()[gid]).to(self.device)
             self.env_origins[:, 2] = 0.0
 
     def _randomize_props(self):
-        """Creation-time DR (humanoid_env.py:528-553, 578-584): friction from 256 buckets, base mass."""
+        """Creation-time DR (humanoid_env.py:528-553, 578-584): friction from 256 buckets, base mass;
+        drawn for every global env and sliced to this shard."""
         dr = self.cfg.domain_rand
+        off, total = self._global_ids()
         if dr.randomize_friction:
             lo, hi = dr.friction_range
-            bucket_ids = torch.randint(0, 256, (self.num_envs, 1))
-            buckets = (hi - lo) * torch.rand(256, 1) + lo
+            g = self._creation_generator(2)
+            bucket_ids = torch.randint(0, 256, (total, 1), generator=g)[off:off + self.num_envs]
+            buckets = (hi - lo) * torch.rand(256, 1, generator=g) + lo
             self.friction_coeffs = buckets[bucket_ids]
             self.env_frictions[:] = self.friction_coeffs.view(-1, 1).to(self.device)
         mass = np.full(self.num_envs, self._model.mass[0], dtype=np.float64)
         if dr.randomize_base_mass:
             lo, hi = dr.added_mass_range
-            mass += np.random.uniform(lo, hi, size=self.num_envs)
+            rs = np.random.RandomState((int(getattr(self.cfg, "seed", 5)) * 1000003 + 3) & 0xFFFFFFFF)
+            mass += rs.uniform(lo, hi, size=total)[off:off + self.num_envs]
         self.body_mass[:] = torch.tensor(mass, dtype=torch.float32, device=self.device).view(-1, 1)
 
     def _init_buffers(self):

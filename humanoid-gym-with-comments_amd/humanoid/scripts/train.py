@@ -6,8 +6,9 @@ Data parallel on one node (one process per GPU, RCCL over xGMI):
 
     python -m torch.distributed.run --standalone --nproc-per-node 8 -m humanoid.scripts.train --task humanoid_ppo
 
-Each rank simulates ``num_envs`` environments on its own GPU with its own seed (seed + rank);
-PPO broadcasts the initial parameters, all-reduces gradients and the KL mean per minibatch and
+Each rank simulates ``num_envs`` environments on its own GPU: rank r holds the global envs
+[r * num_envs, (r + 1) * num_envs) of world * num_envs, with one seed for every rank (the env
+draws and the action noise are keyed by the global env id); PPO broadcasts the initial parameters, all-reduces gradients and the KL mean per minibatch and
 the advantage statistics per iteration (humanoid/algo/ppo/ppo.py).  Only rank 0 writes logs and
 checkpoints.
 """
@@ -36,8 +37,12 @@ def train(args):
     env_cfg, train_cfg = task_registry.get_cfgs(name=args.task)
     if args.seed is None:
         args.seed = train_cfg.seed
-    args.seed = int(args.seed) + rank
-    env, env_cfg = task_registry.make_env(name=args.task, args=args)
+    args.seed = int(args.seed)
+    if args.num_envs is not None:
+        env_cfg.env.num_envs = args.num_envs
+    env_cfg.env.env_offset = rank * env_cfg.env.num_envs
+    env_cfg.env.num_envs_total = world * env_cfg.env.num_envs
+    env, env_cfg = task_registry.make_env(name=args.task, args=args, env_cfg=env_cfg)
     ppo_runner, train_cfg = task_registry.make_alg_runner(env=env, name=args.task, args=args,
                                                           log_root="default" if rank == 0 else None)
     ppo_runner.learn(num_learning_iterations=train_cfg.runner.max_iterations, init_at_random_ep_len=True)

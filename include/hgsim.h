@@ -130,7 +130,8 @@ typedef struct hg_cfg {
   int32_t terrain_rows, terrain_cols;   /* levels x types of terrain_origins */
   float terrain_env_length;             /* move up when the robot walked > length / 2 */
   float max_episode_length_s;           /* move down when it walked < |cmd_xy| * T_ep / 2 */
-  int32_t _pad0;
+  int32_t env_offset;                   /* global id of this shard's env 0 (data parallel): every Philox
+                                         * draw is keyed by the global env id */
   const float* terrain_origins;         /* device [rows, cols, 3], caller-owned */
 } hg_cfg;
 
@@ -245,7 +246,8 @@ int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int6
 
 /* ---- rollout storage writes (replace the tail of PPO.act / process_env_step and
  * RolloutStorage.add_transitions, ppo.py:116-138, rollout_storage.py:83-100) ----
- * hg_rollout_act: actions = mean + std * N(0,1) (Philox keyed by seed, env, counter), their
+ * hg_rollout_act: actions = mean + std * N(0,1) (Philox keyed by seed, row_offset + row, counter:
+ * the global env id under data parallelism), their
  * Normal log-prob summed over actions, mu, sigma, value, and the observation / critic
  * observation rows, all into storage slot t (obs_out/critic_obs_out fp32, or fp16 when
  * obs_fp16).  mean [N,A], std [A], value [N], obs [N,obs_width], critic_obs [N,critic_width]:
@@ -257,7 +259,7 @@ int hg_rollout_act(const float* mean, const float* std, const float* value, cons
                    const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
                    int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
                    float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out, int obs_fp16,
-                   uint64_t seed, uint64_t counter, void* stream);
+                   int row_offset, uint64_t seed, uint64_t counter, void* stream);
 int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
                    int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
                    void* stream);

@@ -25,9 +25,9 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = "cuda:0"
     torch.cuda.set_device(0)
-    torch.manual_seed(5 + rank)
+    torch.manual_seed(5)
     from humanoid.algo.ppo import OnPolicyRunner
-    env = bench.make_env(256, dev, seed=5 + rank)
+    env = bench.make_env(256, dev, seed=5, env_offset=rank * 256, num_envs_total=world * 256)  # global env shards
     tcfg = bench.train_cfg(8)
     runner = OnPolicyRunner(env, tcfg, log_dir=None, device=dev)
     runner.learn(3, init_at_random_ep_len=True)   # eager warm-up, capture, replay

@@ -22,22 +22,32 @@ def run(fixed, steps, n=16):
                       domain_rand__push_robots=False, noise__add_noise=False)
     S, _, _ = T.snapshot(env)
     oc = T._oracle_cfg(env)
-    r64, r32 = T._ref_sim(env, S, "f64"), T._ref_sim(env, S, "f32")
+    r64 = T._ref_sim(env, S, "f64")
+    r32s = [T._ref_sim(env, S, "f32") for _ in range(T.F32_ENSEMBLE)]
+    rng = np.random.default_rng(77)
+    for m in r32s[1:]:  # the test's fp32 ensemble (2^-23 relative perturbations)
+        for a in (m.root, m.q, m.qd):
+            a *= (1 + 2.0 ** -23 * rng.standard_normal(a.shape)).astype(a.dtype)
+    r32 = r32s[0]
     prev = np.zeros((n, 12), np.float32)
     j = np.arange(12)
-    out = {"gpu_vs_f64_q": [], "gpu_vs_f64_tau": [], "f32_vs_f64_q": [], "f32_vs_f64_tau": []}
+    out = {"gpu_vs_f64_q": [], "gpu_vs_f64_tau": [], "f32_vs_f64_q": [], "f32_vs_f64_tau": [],
+           "f32_ensemble_vs_f64_q": [], "f32_ensemble_vs_f64_tau": []}
     for t in range(steps):
         a = np.tile(0.5 * np.sin(2 * np.pi * t * 0.01 / 0.64 + j * np.pi / 6), (n, 1)).astype(np.float32)
         a_ref = PR.preprocess_actions(oc, a, prev, t)
         T._step_only(env, torch.from_numpy(a).cuda(), t)
         prev = env.actions.cpu().numpy()
         r64.step(a_ref.astype(np.float64))
-        r32.step(a_ref)
+        for m in r32s:
+            m.step(a_ref)
         q, tau = env.dof_pos.cpu().numpy(), env.torques.cpu().numpy()
         out["gpu_vs_f64_q"].append(float(np.abs(q - r64.q).max()))
         out["gpu_vs_f64_tau"].append(float(np.abs(tau - r64.torques).max()))
         out["f32_vs_f64_q"].append(float(np.abs(r32.q - r64.q).max()))
         out["f32_vs_f64_tau"].append(float(np.abs(r32.torques - r64.torques).max()))
+        out["f32_ensemble_vs_f64_q"].append(float(max(np.abs(m.q - r64.q).max() for m in r32s)))
+        out["f32_ensemble_vs_f64_tau"].append(float(max(np.abs(m.torques - r64.torques).max() for m in r32s)))
     return out
 
 

@@ -1,0 +1,222 @@
+"""Data parallel on the device, the code the multi-GPU bench runs:
+
+  * sharded envs: two shards [0, n) and [n, 2n) of a 2n-env job step bit-identically to the
+    single 2n-env instance (every env draw and the plane / terrain origins are functions of the
+    global env id);
+  * the PPO update with world_size 2: two ranks share cuda:0 and exchange over gloo (RCCL cannot
+    put two ranks on one device); each holds half of the batch and runs the captured two-graph
+    minibatch path (backward graph -> all-reduce of the flat gradient + KL slot -> step graph),
+    hg_gae with the all-reduced advantage statistics, the fused loss and the fused Adam.  Parameters
+    must be bit-identical across ranks and equal to one process updating the concatenated batch
+    (world_size 1, its one-graph update) under the same minibatch composition, to the stated fp32
+    tolerance (per-minibatch means summed in another order).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _env(n, offset, total, **over):
+    from humanoid.envs import XBotLCfg
+    from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
+    from humanoid.utils.helpers import SimParams
+    cfg = XBotLCfg()
+    cfg.env.num_envs = n
+    cfg.env.env_offset = offset
+    cfg.env.num_envs_total = total
+    cfg.seed = 11
+    cfg.terrain.seed = 5
+    for k, v in over.items():
+        sec, name = k.split("__")
+        setattr(getattr(cfg, sec), name, v)
+    return XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
+
+
+_STATE = ("root_states", "dof_pos", "dof_vel", "commands", "env_origins", "env_frictions", "body_mass",
+          "rand_push_force", "rand_push_torque", "feet_air_time", "last_actions", "ref_dof_pos", "base_euler_xyz")
+
+
+@pytest.mark.parametrize("terrain", ["plane", "heightfield"])
+def test_sharded_envs_equal_single_instance(terrain):
+    """Short episodes (resets), frequent command resamples and pushes, so every Philox purpose is
+    drawn; obs noise on.  Bit-identical, env by env."""
+    _need_gpu()
+    n = 32
+    over = dict(terrain__mesh_type=terrain, env__episode_length_s=0.25, commands__resampling_time=0.1,
+                domain_rand__push_interval_s=0.15)
+    whole = _env(2 * n, 0, 2 * n, **over)
+    shards = [_env(n, r * n, 2 * n, **over) for r in range(2)]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for step in range(60):
+        a = (torch.randn(2 * n, 12, generator=g) * 2.0).to("cuda:0")
+        ow, pw, rw, dw, _ = whole.step(a)
+        outs = [s.step(a[r * n:(r + 1) * n].contiguous()) for r, s in enumerate(shards)]
+        torch.cuda.synchronize()
+        for name, x_w, xs in (("obs", ow, [o[0] for o in outs]), ("priv", pw, [o[1] for o in outs]),
+                              ("rew", rw, [o[2] for o in outs]), ("reset", dw, [o[3] for o in outs])):
+            assert torch.equal(x_w, torch.cat(xs)), f"{name} differs at step {step}"
+        for k in _STATE:
+            assert torch.equal(getattr(whole, k), torch.cat([getattr(s, k) for s in shards])), f"{k} at step {step}"
+    dim = list(whole._sums.shape).index(2 * n)
+    assert torch.equal(whole._sums, torch.cat([s._sums for s in shards], dim=dim))
+
+
+# ------------------------------------------------------------------------------------------------
+# world_size 2 update vs the single process on the concatenated batch
+
+T_STEPS, N_LOCAL, WORLD = 24, 64, 2
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _perm_sequence(k, size):
+    return torch.from_numpy(np.random.RandomState(1000 + k).permutation(size).astype(np.int64))
+
+
+def _global_batch():
+    """Synthetic rollout of WORLD * N_LOCAL envs x T steps (fixed seed)."""
+    rs = np.random.RandomState(7)
+    n = WORLD * N_LOCAL
+    f = lambda *s: rs.standard_normal(s).astype(np.float32)  # noqa: E731
+    return dict(observations=f(T_STEPS, n, 705), privileged_observations=f(T_STEPS, n, 219),
+                actions=f(T_STEPS, n, 12), rewards=0.1 * f(T_STEPS, n, 1), values=f(T_STEPS, n, 1),
+                actions_log_prob=-10.0 + f(T_STEPS, n, 1), mu=0.5 * f(T_STEPS, n, 12),
+                sigma=np.full((T_STEPS, n, 12), 1.0, np.float32),
+                dones=(rs.uniform(size=(T_STEPS, n, 1)) < 0.05).astype(np.uint8), last_critic=f(n, 219))
+
+
+def _worker(rank, world, port, out_path):
+    """world > 1: rank of a gloo group on cuda:0; world == 1: the single process on everything."""
+    import sys
+    for p in (os.path.join(REPO, "humanoid-gym-with-comments_amd"), REPO):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    if world > 1:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from humanoid.algo.ppo import ActorCritic, PPO
+    dev = "cuda:0"
+    tc = bench.train_cfg(T_STEPS)
+    torch.manual_seed(0)
+    ac = ActorCritic(705, 219, 12, **tc["policy"]).to(dev)
+    ppo = PPO(ac, device=dev, **tc["algorithm"])
+    n = N_LOCAL if world > 1 else WORLD * N_LOCAL
+    ppo.init_storage(n, T_STEPS, [705], [219], [12])
+    G = _global_batch()
+    sl = slice(rank * N_LOCAL, (rank + 1) * N_LOCAL) if world > 1 else slice(None)
+    st = ppo.storage
+    # minibatch composition: one local permutation p_k per update call on every rank; the single
+    # process's minibatch i is the union of the ranks' minibatches i
+    calls = [0]
+    real_randperm = torch.randperm
+
+    def randperm(size, *args, out=None, device=None, **kw):
+        k = calls[0]
+        calls[0] += 1
+        if world > 1:
+            idx = _perm_sequence(k, size)
+        else:
+            nmb = ppo.num_mini_batches
+            B = size // WORLD
+            mbl = B // nmb
+            p = _perm_sequence(k, B)
+            parts = []
+            for i in range(nmb):
+                for r in range(WORLD):
+                    b = p[i * mbl:(i + 1) * mbl]
+                    t, el = b // N_LOCAL, b % N_LOCAL
+                    parts.append(t * (WORLD * N_LOCAL) + r * N_LOCAL + el)
+            idx = torch.cat(parts)
+        idx = idx.to(device if device is not None else "cpu")
+        if out is not None:
+            out.copy_(idx)
+            return out
+        return idx
+    torch.randperm = randperm
+    import warnings
+    try:
+        losses = []
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            _updates(ppo, st, G, sl, dev, losses)
+        torch.cuda.synchronize()
+    finally:
+        torch.randperm = real_randperm
+    flat = torch.cat([p.detach().reshape(-1) for p in ac.parameters()]).cpu()
+    torch.save({"flat": flat, "lr": float(ppo.learning_rate), "losses": losses, "graphed": ppo._graphs is not None,
+                "whole": bool(getattr(ppo, "_whole", False)), "calls": calls[0],
+                "accumulate_grad_warnings": sum("AccumulateGrad" in str(w.message) for w in caught)}, out_path)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _updates(ppo, st, G, sl, dev, losses):
+    for _ in range(3):  # eager warm-up, capture + replay, replay
+        for k in ("observations", "privileged_observations", "actions", "rewards", "values", "actions_log_prob",
+                  "mu", "sigma", "dones"):
+            getattr(st, k).copy_(torch.from_numpy(G[k][:, sl]).to(dev))
+        st.step = T_STEPS
+        ppo.compute_returns(torch.from_numpy(G["last_critic"][sl]).to(dev))
+        losses.append(ppo.update())
+
+
+def test_dp_graphed_update_matches_single_process(tmp_path):
+    _need_gpu()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, str(tmp_path / f"rank{r}.pt"))) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0, f"rank process exit code {p.exitcode}"
+    single = ctx.Process(target=_worker, args=(0, 1, 0, str(tmp_path / "single.pt")))
+    single.start()
+    single.join(240)
+    assert single.exitcode == 0
+    R = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    S = torch.load(tmp_path / "single.pt", weights_only=True)
+    assert all(r["graphed"] and not r["whole"] for r in R), "ranks must run the two-graph all-reduce path"
+    assert S["graphed"] and S["whole"]
+    assert R[0]["calls"] == S["calls"] == 3
+    assert all(x["accumulate_grad_warnings"] == 0 for x in R + [S])
+    # ranks: bit-identical parameters and learning rate
+    for r in R[1:]:
+        assert torch.equal(r["flat"], R[0]["flat"])
+        assert r["lr"] == R[0]["lr"]
+    # vs the single process: same learning-rate decisions, parameters within the stated tolerance
+    assert R[0]["lr"] == S["lr"]
+    d = (R[0]["flat"] - S["flat"]).abs()
+    print(f"dp vs single: max |dparam| {d.max().item():.3e}, lr {S['lr']:.3e}, "
+          f"losses dp {R[0]['losses'][-1]} single {S['losses'][-1]}")
+    # 3 updates x 2 epochs x 4 minibatches of Adam steps at lr <= 1e-5 * 1.5^k: a parameter moves by
+    # at most ~lr per step; reassociated fp32 means agree to ~1e-6 relative, so the parameters agree
+    # far inside one step
+    assert d.max().item() <= 1e-6
+    # the loss means a rank reports are over its own rows; their average over the ranks is the
+    # single process's mean over all rows
+    for i, b in enumerate(S["losses"][-1]):
+        a = sum(float(r["losses"][-1][i]) for r in R) / WORLD
+        assert abs(a - float(b)) <= 1e-5 * max(1.0, abs(float(b)))
