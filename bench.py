@@ -100,21 +100,29 @@ class KernelTimer:
         return len(self.events.get(name, []))
 
 
-def physics_flops_per_env_step(rows, decimation=10):
-    """Analytic FLOP count of the K_step algorithm: per substep
-    kinematics 3.3k + bias forces 1.8k + inertia 1.5k + Cholesky 2.0k + solve 0.65k +
-    integration 0.1k, plus per constraint row: Jacobian 0.12k + M^-1 J^T solve 0.65k +
-    diagonal/warm start 0.07k + 6 PGS sweeps x 82.  Plus one end-of-step FK + quaternions (4.0k)."""
-    per_sub = 9350 + rows * (120 + 650 + 72 + 6 * 82)
+def physics_flops_per_env_step(rows, decimation=10, sweeps=5, nf=18):
+    """Analytic FLOP count of the K_step algorithm, per env and policy step.
+    Per substep: kinematics 3.3k + bias forces (RNEA) 1.8k + joint-space inertia (CRBA) 1.5k +
+    Cholesky of the nf x nf legs-first arrow matrix 2.0k + g = L^-1 (tau - h) and the back
+    substitution 0.65k + integration 0.1k; per constraint row: the Jacobian row 0.12k, its forward
+    solve z = L^-1 J^T (nf^2 = 324 FMA -> 0.65k), the Delassus row W = Z^T Z on MFMA (2 nf rows),
+    diagonal / bounds / warm start 0.07k; per PGS sweep and row: the W row times the impulses
+    (2 rows) + the update and clamp (12).  Plus one end-of-step FK + quaternions (4.0k)."""
+    per_sub = 9350 + rows * (120 + 2 * nf * nf + 2 * nf * rows + 72) + sweeps * rows * (2 * rows + 12)
     return decimation * per_sub + 4000
 
 
 def active_rows(env):
+    """Mean constraint rows per env of the last solve, from the warm-start impulse table
+    (HG_LAMW layout, csrc/hg_physics.hip: [0, 72) ground contacts x 3, [72, 96) leg-pair contacts
+    x 3, [96, 108) joint limits, [108, 120) joint-friction rows): a contact with a positive
+    normal impulse holds 3 rows, an active limit 1, every joint with friction 1 (always solved)."""
     from humanoid import _native as N
     lam = env._view(N.T["CONTACT_LAMBDA"])
-    contacts = (lam[:, 0:48:3] > 0).sum(dim=1).float()
-    limits = (lam[:, 48:60] > 0).sum(dim=1).float()
-    return float((3 * contacts + limits).mean().item())
+    contacts = (lam[:, 0:96:3] > 0).sum(dim=1).float()
+    limits = (lam[:, 96:108] != 0).sum(dim=1).float()
+    fric = sum(1 for b in range(len(env._model.joint_friction)) if env._model.joint_friction[b] > 0)
+    return float((3 * contacts + limits).mean().item() + fric)
 
 
 def make_env(num_envs, device, seed, terrain="plane", push_curriculum=False, env_offset=0, num_envs_total=None):
@@ -142,10 +150,22 @@ def train_cfg(T, policy_dtype="fp32", obs_dtype="fp32"):
     return class_to_dict(t)
 
 
-def cpu_baseline(n_envs=256, T=24, threads=None):
+def host_cores():
+    """Host threads the baseline may use: OMP_NUM_THREADS when set (the GPU box's CPU share, 16),
+    else the CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(n_envs=256, T=24, threads=None, iterations=3):
     """The oracle port on the host: C reference physics (f32, OpenMP over envs), numpy env logic
-    (oracle/pipeline_ref.py), torch-CPU policy + GAE + PPO update — one full PPO iteration on
-    n_envs envs.  Returns env-steps/s."""
+    (oracle/pipeline_ref.py), torch-CPU policy + GAE + PPO update — `iterations` full PPO
+    iterations on n_envs envs after the set-up.  Returns (env-steps/s, threads, seconds)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import physics_ref as P
     import pipeline_ref as PR
@@ -154,7 +174,7 @@ def cpu_baseline(n_envs=256, T=24, threads=None):
     from humanoid.envs import XBotLCfg
     from humanoid.envs.custom.humanoid_env import build_hg_cfg
     from humanoid.algo.ppo import ActorCritic, PPO
-    threads = threads or min(16, os.cpu_count() or 1)
+    threads = threads or host_cores()
     torch.set_num_threads(threads)
     os.environ["OMP_NUM_THREADS"] = str(threads)
     P.set_threads(threads)
@@ -183,25 +203,25 @@ def cpu_baseline(n_envs=256, T=24, threads=None):
                                                       lv[:, 0].numpy(), g, l, normalize=False))
     t0 = time.time()
     counter = 0
-    with torch.inference_mode():
-        for _ in range(T):
-            a = ppo.act(torch.from_numpy(obs), torch.from_numpy(priv)).numpy()
-            a_ref = PR.preprocess_actions(oc, a, S["actions"], counter)
-            S["actions"] = a_ref
-            sim.root[:], sim.q[:], sim.qd[:], sim.lam[:] = S["root_states"], S["dof_pos"], S["dof_vel"], S["lambda"]
-            sim.step(a_ref)
-            S.update(root_states=sim.root.copy(), dof_pos=sim.q.copy(), dof_vel=sim.qd.copy(), lambda_=None,
-                     torques=sim.torques.copy(), contact_forces=sim.contact.copy(), rigid_state=sim.rigid.copy())
-            S.pop("lambda_")
-            S["lambda"] = sim.lam.copy()
-            counter += 1
-            obs, priv, rew, reset, timeout, _ = PR.post(oc, S, counter, obs, priv)
-            infos = {"time_outs": torch.from_numpy(timeout)}
-            ppo.process_env_step(torch.from_numpy(rew), torch.from_numpy(reset), infos)
-        ppo.compute_returns(torch.from_numpy(priv))
-    ppo.update()
+    for _ in range(iterations):
+        with torch.inference_mode():
+            for _ in range(T):
+                a = ppo.act(torch.from_numpy(obs), torch.from_numpy(priv)).numpy()
+                a_ref = PR.preprocess_actions(oc, a, S["actions"], counter)
+                S["actions"] = a_ref
+                sim.root[:], sim.q[:], sim.qd[:], sim.lam[:] = S["root_states"], S["dof_pos"], S["dof_vel"], S["lambda"]
+                sim.step(a_ref)
+                S.update(root_states=sim.root.copy(), dof_pos=sim.q.copy(), dof_vel=sim.qd.copy(),
+                         torques=sim.torques.copy(), contact_forces=sim.contact.copy(), rigid_state=sim.rigid.copy())
+                S["lambda"] = sim.lam.copy()
+                counter += 1
+                obs, priv, rew, reset, timeout, _ = PR.post(oc, S, counter, obs, priv)
+                infos = {"time_outs": torch.from_numpy(timeout)}
+                ppo.process_env_step(torch.from_numpy(rew), torch.from_numpy(reset), infos)
+            ppo.compute_returns(torch.from_numpy(priv))
+        ppo.update()
     dt = time.time() - t0
-    return n_envs * T / dt, threads, dt
+    return n_envs * T * iterations / dt, threads, dt
 
 
 def main():
@@ -213,6 +233,7 @@ def main():
     ap.add_argument("--T", type=int, default=24, help="rollout length (num_steps_per_env)")
     ap.add_argument("--cpu-envs", type=int, default=4096, help="CPU baseline sample on all host threads")
     ap.add_argument("--cpu-envs-1core", type=int, default=256, help="CPU baseline sample on one thread")
+    ap.add_argument("--cpu-iterations", type=int, default=3, help="PPO iterations of the CPU baseline samples")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-table", action="store_true", help="hipBLASLt default GEMM heuristics")
     ap.add_argument("--terrain", default="plane", choices=["plane", "heightfield"],
@@ -271,7 +292,7 @@ def main():
     ms_step = timer.mean_ms("k_step")
     flops = physics_flops_per_env_step(rows) * args.envs
     achieved_tflops = flops / (ms_step * 1e-3) / 1e12
-    roofline = {"kernel": "k_step", "bound": "mfma", "pipe": "fp32-valu (f32 MFMA peak = f32 vector peak)",
+    roofline = {"kernel": "k_step", "bound": "fp32-valu", "pipe": "fp32 VALU + f32 MFMA (W = Z^T Z); f32 MFMA peak = f32 vector peak",
                 "achieved": round(achieved_tflops, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": traffic_src,
@@ -303,14 +324,22 @@ def main():
         "learn_time_s": round(runner.last_iteration_stats.get("learn_time", float("nan")), 4),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, threads, dt = cpu_baseline(args.cpu_envs, args.T)
-        v1, _, dt1 = cpu_baseline(args.cpu_envs_1core, args.T, threads=1)
+        # config 2 on all host cores for >= 3 iterations (the headline
+        # baseline), the same on one core over a smaller sample, and config 1 (4 envs, 1 iteration)
+        it = args.cpu_iterations
+        v, threads, dt = cpu_baseline(args.cpu_envs, args.T, iterations=it)
+        v1, _, dt1 = cpu_baseline(args.cpu_envs_1core, args.T, threads=1, iterations=it)
+        vc1, _, dtc1 = cpu_baseline(4, args.T, threads=threads, iterations=1)
         result["cpu_baseline"] = {"value": round(v, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-                                  "sample": f"1 PPO iteration, {args.cpu_envs} envs x {args.T} steps, {dt:.1f} s "
+                                  "sample": f"{it} PPO iterations, {args.cpu_envs} envs x {args.T} steps, {dt:.1f} s "
                                             f"(oracle physics + numpy env logic + torch-CPU PPO)",
                                   "value_1_core": round(v1, 1),
-                                  "sample_1_core": f"1 PPO iteration, {args.cpu_envs_1core} envs x {args.T} steps, "
-                                                   f"{dt1:.1f} s"}
+                                  "sample_1_core": f"{it} PPO iterations, {args.cpu_envs_1core} envs x {args.T} steps, "
+                                                   f"{dt1:.1f} s",
+                                  "config1": {"value": round(vc1, 1), "unit": "env-steps/s", "cores": threads,
+                                              "ppo_iters_per_sec": round(1.0 / dtc1, 3),
+                                              "sample": f"BASELINE configs[0]: 1 PPO iteration, 4 envs x {args.T} "
+                                                        f"steps, {dtc1:.2f} s"}}
         torch.set_num_threads(threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
