@@ -71,7 +71,7 @@ def parse_sim_params(args, cfg):
 
 def get_load_path(root, load_run=-1, checkpoint=-1):
     try:
-        runs = sorted(r for r in os.listdir(root) if r != "exported")
+        runs = sorted(r for r in os.listdir(root) if r not in ("exported", "openloop_action"))  # play.py outputs
         last_run = os.path.join(root, runs[-1])
     except Exception:
         raise ValueError("No runs in this directory: " + root)

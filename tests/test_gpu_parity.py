@@ -1081,3 +1081,37 @@ def test_runner_lazy_stats_are_last_iteration():
     v, s_, lv = (alg._sums / (alg.num_learning_epochs * alg.num_mini_batches)).tolist()
     assert (st["value_loss"], st["surrogate_loss"], st["lin_vel_loss"]) == (v, s_, lv)
     assert all(math.isfinite(x) for x in (v, s_, lv))
+
+
+def test_play_script(tmp_path, monkeypatch):
+    """humanoid/scripts/play.py (reference play.py:49-176) end to end: a checkpoint written by
+    train's caller path under the default log root, then play() resumes it, exports the actor
+    (TorchScript + ONNX), runs the policy on one env with the reference's play settings and writes
+    the action / state traces (the action trace on disk is the one play() returns)."""
+    _need_gpu()
+    import sys
+    import humanoid.scripts.play as play_mod
+    from humanoid.envs import XBotLCfgPPO  # noqa: F401  (registers humanoid_ppo)
+    from humanoid.utils import get_args, task_registry
+    tr_mod = sys.modules["humanoid.utils.task_registry"]  # the module (humanoid.utils re-exports the registry object)
+    monkeypatch.setattr(tr_mod, "LEGGED_GYM_ROOT_DIR", str(tmp_path))
+    monkeypatch.setattr(play_mod, "LEGGED_GYM_ROOT_DIR", str(tmp_path))
+    args = get_args(["--num_envs", "64", "--headless", "--run_name", "p"])
+    env, _ = task_registry.make_env("humanoid_ppo", args=args)
+    _, tcfg = task_registry.get_cfgs("humanoid_ppo")
+    tcfg.runner.num_steps_per_env = 8
+    runner, tcfg = task_registry.make_alg_runner(env, args=args, train_cfg=tcfg)
+    runner.learn(1, init_at_random_ep_len=True)
+    exp = tcfg.runner.experiment_name
+    assert os.path.isdir(tmp_path / "logs" / exp)
+    del runner, env
+    torch.cuda.synchronize()
+    actions = play_mod.play(get_args(["--task", "humanoid_ppo", "--headless"]), steps=40)
+    assert actions.shape == (40, 12) and np.isfinite(actions).all()
+    root = tmp_path / "logs" / exp
+    for f in ("exported/policies/policy_1.pt", "exported/policies/policy.onnx", "openloop_action/openloop_action.npz",
+              "openloop_action/states.npz"):
+        assert (root / f).exists(), f
+    st = np.load(root / "openloop_action" / "states.npz")
+    assert st["dof_pos"].shape == (40, 12) and np.isfinite(st["dof_pos"]).all()
+    np.testing.assert_array_equal(np.load(root / "openloop_action" / "openloop_action.npz")["action"], actions)
