@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0
 # warm-start impulses) + 1316 B written (rigid 13x13, contacts 13x3, root, dofs, torques, actions,
 # warm-start) + 192 B of next-step observation noise (48 floats)
 KSTEP_BYTES_PER_ENV = 492 + 1316 + 192
-PROFILE_DIR = "r1_v8"  # the committed rocprofv3 summaries of the current kernels
+PROFILE_DIR = "r2_v1"  # the committed rocprofv3 summaries of the current kernels
 PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
 
