@@ -16,13 +16,63 @@
 
 namespace {
 
+// Element access for the fp32 and bf16 (config 5 policy) variants: bf16 is stored as __bf16,
+// widened to fp32 for all arithmetic, narrowed with round-to-nearest-even (v_cvt_pk_bf16_f32).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ inline float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ inline float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ inline uint32_t bf_pack(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+template <typename T> __device__ inline float4 ld4(const T* p);
+template <> __device__ inline float4 ld4<float>(const float* p) { return *reinterpret_cast<const float4*>(p); }
+template <> __device__ inline float4 ld4<__bf16>(const __bf16* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(bf_lo(u.x), bf_hi(u.x), bf_lo(u.y), bf_hi(u.y));
+}
+template <typename T> __device__ inline void st4(T* p, float4 v);
+template <> __device__ inline void st4<float>(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+template <> __device__ inline void st4<__bf16>(__bf16* p, float4 v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(bf_pack(v.x, v.y), bf_pack(v.z, v.w));
+}
+template <typename T> __device__ inline float2 ld2(const T* p);
+template <> __device__ inline float2 ld2<float>(const float* p) { return *reinterpret_cast<const float2*>(p); }
+template <> __device__ inline float2 ld2<__bf16>(const __bf16* p) {
+  const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+  return make_float2(bf_lo(u), bf_hi(u));
+}
+template <typename T> __device__ inline void st2(T* p, float2 v);
+template <> __device__ inline void st2<float>(float* p, float2 v) { *reinterpret_cast<float2*>(p) = v; }
+template <> __device__ inline void st2<__bf16>(__bf16* p, float2 v) {
+  *reinterpret_cast<uint32_t*>(p) = bf_pack(v.x, v.y);
+}
+// 8 consecutive elements (16-byte aligned)
+template <typename T> __device__ inline void ld8(const T* p, float v[8]);
+template <> __device__ inline void ld8<float>(const float* p, float v[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 c = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+}
+template <> __device__ inline void ld8<__bf16>(const __bf16* p, float v[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  v[0] = bf_lo(u.x); v[1] = bf_hi(u.x); v[2] = bf_lo(u.y); v[3] = bf_hi(u.y);
+  v[4] = bf_lo(u.z); v[5] = bf_hi(u.z); v[6] = bf_lo(u.w); v[7] = bf_hi(u.w);
+}
+__device__ inline float ld1(const float* p) { return *p; }
+__device__ inline float ld1(const __bf16* p) { return (float)*p; }
+__device__ inline void st1(float* p, float v) { *p = v; }
+__device__ inline void st1(__bf16* p, float v) { *p = (__bf16)v; }
+
 constexpr int TPB = 256;
 constexpr int RT = 32;   // rows per tile: 768 tiles at the 24576-row minibatch (>= 3 blocks per CU)
 
 // width % 4 == 0, width >= 128: float4 columns; W4 = min(width/4, 64) column groups per block,
 // L = TPB / W4 row lanes
-__global__ void __launch_bounds__(TPB) k_act_bwd_vec(const float* __restrict__ gy, const float* __restrict__ y,
-                                                    float* __restrict__ gh, int64_t rows, int width,
+template <typename T>
+__global__ void __launch_bounds__(TPB) k_act_bwd_vec(const T* __restrict__ gy, const T* __restrict__ y,
+                                                    T* __restrict__ gh, int64_t rows, int width,
                                                     float* __restrict__ partial) {
   const int W4 = min(width >> 2, 64);
   const int L = TPB / W4;
@@ -34,14 +84,14 @@ __global__ void __launch_bounds__(TPB) k_act_bwd_vec(const float* __restrict__ g
   if (colok) {
     for (int64_t r = r0 + rho; r < r0 + RT && r < rows; r += L) {
       const int64_t i = r * width + col;
-      float4 v = *reinterpret_cast<const float4*>(gy + i);
+      float4 v = ld4(gy + i);
       if (y) {
-        const float4 o = *reinterpret_cast<const float4*>(y + i);
+        const float4 o = ld4(y + i);
         v.x = o.x > 0.f ? v.x : v.x * (o.x + 1.0f);
         v.y = o.y > 0.f ? v.y : v.y * (o.y + 1.0f);
         v.z = o.z > 0.f ? v.z : v.z * (o.z + 1.0f);
         v.w = o.w > 0.f ? v.w : v.w * (o.w + 1.0f);
-        *reinterpret_cast<float4*>(gh + i) = v;
+        st4(gh + i, v);
       }
       acc.x += v.x;
       acc.y += v.y;
@@ -67,8 +117,9 @@ __global__ void __launch_bounds__(TPB) k_act_bwd_vec(const float* __restrict__ g
 
 // any width <= TPB: thread t -> column t % width, row lane t / width (lanes beyond the last full
 // group idle)
-__global__ void __launch_bounds__(TPB) k_act_bwd_small(const float* __restrict__ gy, const float* __restrict__ y,
-                                                      float* __restrict__ gh, int64_t rows, int width,
+template <typename T>
+__global__ void __launch_bounds__(TPB) k_act_bwd_small(const T* __restrict__ gy, const T* __restrict__ y,
+                                                      T* __restrict__ gh, int64_t rows, int width,
                                                       float* __restrict__ partial) {
   const int L = TPB / width;
   const int c = threadIdx.x % width, rho = threadIdx.x / width;
@@ -77,11 +128,11 @@ __global__ void __launch_bounds__(TPB) k_act_bwd_small(const float* __restrict__
   if (rho < L) {
     for (int64_t r = r0 + rho; r < r0 + RT && r < rows; r += L) {
       const int64_t i = r * width + c;
-      float v = gy[i];
+      float v = ld1(gy + i);
       if (y) {
-        const float o = y[i];
+        const float o = ld1(y + i);
         v = o > 0.f ? v : v * (o + 1.0f);
-        gh[i] = v;
+        st1(gh + i, v);
       }
       acc += v;
     }
@@ -130,21 +181,24 @@ extern "C" int64_t hg_mlp_act_backward_scratch(int64_t rows, int width) {
   return ((rows + RT - 1) / RT) * (int64_t)width;
 }
 
-extern "C" int hg_mlp_act_backward(const float* gy, const float* y, float* gh, int64_t rows, int width,
-                                   float* grad_bias, float* scratch, void* stream) {
+namespace {
+template <typename T>
+int act_backward(const T* gy, const T* y, T* gh, int64_t rows, int width, float* grad_bias, float* scratch,
+                 void* stream) {
   if (!gy || !scratch || rows <= 0 || width <= 0 || (y && !gh)) return HG_ERR_ARG;
   const int64_t tiles64 = (rows + RT - 1) / RT;
   if (tiles64 > 65535 * 16) return HG_ERR_ARG;
   const int tiles = (int)tiles64;
   hipStream_t s = (hipStream_t)stream;
-  const bool vec = (width % 4 == 0) && width >= 128 && ((uintptr_t)gy % 16 == 0) && (!y || (uintptr_t)y % 16 == 0) &&
-                   (!gh || (uintptr_t)gh % 16 == 0);
+  const uintptr_t al = 4 * sizeof(T);  // one 4-element vector per lane
+  const bool vec = (width % 4 == 0) && width >= 128 && ((uintptr_t)gy % al == 0) && (!y || (uintptr_t)y % al == 0) &&
+                   (!gh || (uintptr_t)gh % al == 0);
   if (vec) {
     const int W4 = width / 4 < 64 ? width / 4 : 64;
     const int ct = (width / 4 + W4 - 1) / W4;
-    hipLaunchKernelGGL(k_act_bwd_vec, dim3(tiles, ct), dim3(TPB), 0, s, gy, y, gh, rows, width, scratch);
+    hipLaunchKernelGGL(k_act_bwd_vec<T>, dim3(tiles, ct), dim3(TPB), 0, s, gy, y, gh, rows, width, scratch);
   } else if (width <= TPB) {
-    hipLaunchKernelGGL(k_act_bwd_small, dim3(tiles), dim3(TPB), 0, s, gy, y, gh, rows, width, scratch);
+    hipLaunchKernelGGL(k_act_bwd_small<T>, dim3(tiles), dim3(TPB), 0, s, gy, y, gh, rows, width, scratch);
   } else {
     return HG_ERR_ARG;
   }
@@ -153,6 +207,18 @@ extern "C" int hg_mlp_act_backward(const float* gy, const float* y, float* gh, i
     hipLaunchKernelGGL(k_colsum_final, dim3((width + FC - 1) / FC), dim3(TPB), 0, s, scratch, tiles, width,
                        grad_bias);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+}  // namespace
+
+extern "C" int hg_mlp_act_backward(const float* gy, const float* y, float* gh, int64_t rows, int width,
+                                   float* grad_bias, float* scratch, void* stream) {
+  return act_backward<float>(gy, y, gh, rows, width, grad_bias, scratch, stream);
+}
+
+extern "C" int hg_mlp_act_backward_bf16(const uint16_t* gy, const uint16_t* y, uint16_t* gh, int64_t rows, int width,
+                                        float* grad_bias, float* scratch, void* stream) {
+  return act_backward<__bf16>(reinterpret_cast<const __bf16*>(gy), reinterpret_cast<const __bf16*>(y),
+                              reinterpret_cast<__bf16*>(gh), rows, width, grad_bias, scratch, stream);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -170,8 +236,8 @@ namespace {
 constexpr int SK_K = 128;
 constexpr int SK_ROWS = 64;
 
-template <int N>
-__global__ void __launch_bounds__(256) k_skinny_fwd(const float* __restrict__ x, int64_t ldx,
+template <int N, typename TX>
+__global__ void __launch_bounds__(256) k_skinny_fwd(const TX* __restrict__ x, int64_t ldx,
                                                    const float* __restrict__ W, const float* __restrict__ b,
                                                    float* __restrict__ y, int64_t rows) {
   const int q = threadIdx.x & 15;  // lane within the row's 16-lane group
@@ -187,10 +253,8 @@ __global__ void __launch_bounds__(256) k_skinny_fwd(const float* __restrict__ x,
   const float bq = q < N ? b[q] : 0.f;
   const int64_t groups = (rows + 15) / 16;
   for (int64_t gi = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); gi < rows; gi += (int64_t)gridDim.x * 16) {
-    const float* xr = x + gi * ldx + k0;
-    const float4 a = *reinterpret_cast<const float4*>(xr);
-    const float4 c = *reinterpret_cast<const float4*>(xr + 4);
-    const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    float v[8];
+    ld8(x + gi * ldx + k0, v);
     float out = 0.f;
 #pragma unroll
     for (int n = 0; n < N; n++) {
@@ -208,9 +272,9 @@ __global__ void __launch_bounds__(256) k_skinny_fwd(const float* __restrict__ x,
   (void)groups;
 }
 
-template <int N>
+template <int N, typename TD>
 __global__ void __launch_bounds__(64) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
-                                                 float* __restrict__ dx, int64_t rows) {
+                                                 TD* __restrict__ dx, int64_t rows) {
   __shared__ float g_s[SK_ROWS * N];
   const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
   const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
@@ -232,12 +296,12 @@ __global__ void __launch_bounds__(64) k_skinny_dx(const float* __restrict__ gh, 
       a0 = fmaf(g, w0[n], a0);
       a1 = fmaf(g, w1[n], a1);
     }
-    *reinterpret_cast<float2*>(dx + (r0 + r) * SK_K + c) = make_float2(a0, a1);
+    st2(dx + (r0 + r) * SK_K + c, make_float2(a0, a1));
   }
 }
 
-template <int N>
-__global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, const float* __restrict__ h,
+template <int N, typename TH>
+__global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, const TH* __restrict__ h,
                                                  int64_t ldh, float* __restrict__ partial, int64_t rows) {
   __shared__ float g_s[SK_ROWS * N];
   const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
@@ -248,12 +312,12 @@ __global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, 
   float a0[N], a1[N];
 #pragma unroll
   for (int n = 0; n < N; n++) a0[n] = a1[n] = 0.f;
-  const float* hr = h + r0 * ldh + c;
+  const TH* hr = h + r0 * ldh + c;
   int r = 0;
   for (; r + 8 <= nr; r += 8) {
     float2 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const float2*>(hr + (int64_t)(r + u) * ldh);
+    for (int u = 0; u < 8; u++) v[u] = ld2(hr + (int64_t)(r + u) * ldh);
 #pragma unroll
     for (int u = 0; u < 8; u++) {
 #pragma unroll
@@ -265,7 +329,7 @@ __global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, 
     }
   }
   for (; r < nr; r++) {
-    const float2 v = *reinterpret_cast<const float2*>(hr + (int64_t)r * ldh);
+    const float2 v = ld2(hr + (int64_t)r * ldh);
 #pragma unroll
     for (int n = 0; n < N; n++) {
       const float g = g_s[r * N + n];
@@ -301,18 +365,59 @@ extern "C" int hg_linear_skinny_supported(int n, int k) {
   return (n == 1 || n == 2 || n == 3 || n == 4 || n == 6 || n == 8 || n == 12 || n == 16) && k == SK_K;
 }
 
-extern "C" int hg_linear_skinny_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y,
-                                        int64_t rows, int n, int k, void* stream) {
-  if (!x || !W || !b || !y || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldx < k || ldx % 4 != 0 ||
+namespace {
+template <typename TX>
+int skinny_forward(const TX* x, int64_t ldx, const float* W, const float* b, float* y, int64_t rows, int n, int k,
+                   void* stream) {
+  // 8 elements of x per lane: 16-byte aligned rows
+  const int64_t vec = 16 / sizeof(TX);
+  if (!x || !W || !b || !y || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldx < k || ldx % vec != 0 ||
       (uintptr_t)x % 16 != 0 || (uintptr_t)W % 16 != 0)
     return HG_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t want = (rows + 15) / 16;  // one 16-row group per block pass
   const dim3 grid((unsigned)(want < 1024 ? want : 1024));
-#define HG_SK_FWD(NN) hipLaunchKernelGGL(k_skinny_fwd<NN>, grid, dim3(256), 0, s, x, ldx, W, b, y, rows)
+#define HG_SK_FWD(NN) hipLaunchKernelGGL((k_skinny_fwd<NN, TX>), grid, dim3(256), 0, s, x, ldx, W, b, y, rows)
   HG_SKINNY_SWITCH(n, HG_SK_FWD)
 #undef HG_SK_FWD
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+template <typename TH>
+int skinny_backward(const float* gh, const TH* h, int64_t ldh, const float* W, TH* dx, float* grad_wb, int64_t rows,
+                    int n, int k, float* scratch, void* stream) {
+  // two elements of h / dx per lane
+  if (!gh || !h || !W || !scratch || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldh < k ||
+      ldh % 2 != 0 || (uintptr_t)h % (2 * sizeof(TH)) != 0 || (uintptr_t)W % 8 != 0 ||
+      (dx && (uintptr_t)dx % (2 * sizeof(TH)) != 0))
+    return HG_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = (int)((rows + SK_ROWS - 1) / SK_ROWS);
+  const dim3 grid((unsigned)tiles);
+#define HG_SK_DW(NN) hipLaunchKernelGGL((k_skinny_dw<NN, TH>), grid, dim3(64), 0, s, gh, h, ldh, scratch, rows)
+  HG_SKINNY_SWITCH(n, HG_SK_DW)
+#undef HG_SK_DW
+  const int width = n * k + n;
+  // grad_wb NULL: partials stay in scratch ([tiles, n*k + n]) for a later hg_colsum_jobs launch
+  if (grad_wb)
+    hipLaunchKernelGGL(k_colsum_final, dim3((width + FC - 1) / FC), dim3(TPB), 0, s, scratch, tiles, width, grad_wb);
+  if (dx) {
+#define HG_SK_DX(NN) hipLaunchKernelGGL((k_skinny_dx<NN, TH>), grid, dim3(64), 0, s, gh, W, dx, rows)
+    HG_SKINNY_SWITCH(n, HG_SK_DX)
+#undef HG_SK_DX
+  }
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+}  // namespace
+
+extern "C" int hg_linear_skinny_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y,
+                                        int64_t rows, int n, int k, void* stream) {
+  return skinny_forward<float>(x, ldx, W, b, y, rows, n, k, stream);
+}
+
+extern "C" int hg_linear_skinny_forward_bf16(const uint16_t* x, int64_t ldx, const float* W, const float* b, float* y,
+                                             int64_t rows, int n, int k, void* stream) {
+  return skinny_forward<__bf16>(reinterpret_cast<const __bf16*>(x), ldx, W, b, y, rows, n, k, stream);
 }
 
 extern "C" int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k) {
@@ -323,25 +428,14 @@ extern "C" int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k)
 // grad_wb [n*k + n]: dW (row-major [n, k]) followed by db.  dx [rows, k] (contiguous) may be NULL.
 extern "C" int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, const float* W, float* dx,
                                          float* grad_wb, int64_t rows, int n, int k, float* scratch, void* stream) {
-  if (!gh || !h || !W || !scratch || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldh < k ||
-      ldh % 2 != 0 || (uintptr_t)h % 8 != 0 || (uintptr_t)W % 8 != 0 || (dx && (uintptr_t)dx % 8 != 0))
-    return HG_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  const int tiles = (int)((rows + SK_ROWS - 1) / SK_ROWS);
-  const dim3 grid((unsigned)tiles);
-#define HG_SK_DW(NN) hipLaunchKernelGGL(k_skinny_dw<NN>, grid, dim3(64), 0, s, gh, h, ldh, scratch, rows)
-  HG_SKINNY_SWITCH(n, HG_SK_DW)
-#undef HG_SK_DW
-  const int width = n * k + n;
-  // grad_wb NULL: partials stay in scratch ([tiles, n*k + n]) for a later hg_colsum_jobs launch
-  if (grad_wb)
-    hipLaunchKernelGGL(k_colsum_final, dim3((width + FC - 1) / FC), dim3(TPB), 0, s, scratch, tiles, width, grad_wb);
-  if (dx) {
-#define HG_SK_DX(NN) hipLaunchKernelGGL(k_skinny_dx<NN>, grid, dim3(64), 0, s, gh, W, dx, rows)
-    HG_SKINNY_SWITCH(n, HG_SK_DX)
-#undef HG_SK_DX
-  }
-  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+  return skinny_backward<float>(gh, h, ldh, W, dx, grad_wb, rows, n, k, scratch, stream);
+}
+
+extern "C" int hg_linear_skinny_backward_bf16(const float* gh, const uint16_t* h, int64_t ldh, const float* W,
+                                              uint16_t* dx, float* grad_wb, int64_t rows, int n, int k,
+                                              float* scratch, void* stream) {
+  return skinny_backward<__bf16>(gh, reinterpret_cast<const __bf16*>(h), ldh, W, reinterpret_cast<__bf16*>(dx),
+                                 grad_wb, rows, n, k, scratch, stream);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -426,5 +520,60 @@ extern "C" int hg_colsum_jobs(const float* const* src, float* const* dst, const 
   }
   J.block0[njobs] = (int)blocks;
   hipLaunchKernelGGL(k_colsum_jobs, dim3((unsigned)blocks), dim3(TPB), 0, (hipStream_t)stream, J);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 policy (config 5): fp32 -> bf16 copies of a list of tensors in ONE launch — the hidden
+// layers' weights and biases before a bf16 forward (master weights, gradients and Adam stay fp32).
+// Block b belongs to the job whose [block0[j], block0[j+1]) range holds it; 4 elements per thread
+// (float4 in, two packed bf16 pairs out) when the job is 16-byte aligned with count % 4 == 0,
+// element-wise otherwise.
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int CAST_MAX = 32;
+struct CastJobs {
+  const float* src[CAST_MAX];
+  __bf16* dst[CAST_MAX];
+  int64_t count[CAST_MAX];
+  int block0[CAST_MAX + 1];
+  int njobs;
+};
+
+__global__ void __launch_bounds__(TPB) k_cast_bf16_jobs(CastJobs J) {
+  const int bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < J.njobs && bid >= J.block0[j + 1]) j++;
+  const float* __restrict__ src = J.src[j];
+  __bf16* __restrict__ dst = J.dst[j];
+  const int64_t n = J.count[j];
+  const int64_t e = ((int64_t)(bid - J.block0[j]) * TPB + threadIdx.x) * 4;
+  if (e >= n) return;
+  if (n % 4 == 0 && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 8 == 0) {
+    st4(dst + e, ld4(src + e));
+  } else {
+    for (int64_t i = e; i < e + 4 && i < n; i++) dst[i] = (__bf16)src[i];
+  }
+}
+}  // namespace
+
+extern "C" int hg_cast_bf16_jobs(const float* const* src, uint16_t* const* dst, const int64_t* count, int njobs,
+                                 void* stream) {
+  if (njobs <= 0) return HG_OK;
+  if (njobs > CAST_MAX || !src || !dst || !count) return HG_ERR_ARG;
+  CastJobs J;
+  J.njobs = njobs;
+  int64_t blocks = 0;
+  for (int j = 0; j < njobs; j++) {
+    if (!src[j] || !dst[j] || count[j] <= 0) return HG_ERR_ARG;
+    J.src[j] = src[j];
+    J.dst[j] = reinterpret_cast<__bf16*>(dst[j]);
+    J.count[j] = count[j];
+    J.block0[j] = (int)blocks;
+    blocks += (count[j] + 4 * TPB - 1) / (4 * TPB);
+    if (blocks > (int64_t)1 << 30) return HG_ERR_ARG;
+  }
+  J.block0[njobs] = (int)blocks;
+  hipLaunchKernelGGL(k_cast_bf16_jobs, dim3((unsigned)blocks), dim3(TPB), 0, (hipStream_t)stream, J);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

@@ -191,7 +191,8 @@ struct GatherTab {
   const void* src;
   void* dst;
   int64_t width;  // elements per row
-  int es;         // element bytes: 4 or 2
+  int es;         // element bytes: 4 or 2 (cvt == 0)
+  int cvt;        // 0: copy; 1: fp16 -> bf16; 2: fp32 -> bf16 (the bf16 policy's minibatch inputs)
 };
 struct GatherArgs {
   GatherTab t[3];
@@ -210,6 +211,20 @@ __device__ inline void gather_row(const E* __restrict__ src, E* __restrict__ dst
     dst[j + 192] = d;
   }
   for (; j < w; j += 64) dst[j] = src[j];
+}
+
+// gathered row converted to bf16 on the way (round-to-nearest-even)
+template <typename S>
+__device__ inline void gather_row_bf16(const S* __restrict__ src, __bf16* __restrict__ dst, int64_t w, int lane) {
+  int64_t j = lane;
+  for (; j + 192 < w; j += 256) {
+    const float a = (float)src[j], b = (float)src[j + 64], c = (float)src[j + 128], d = (float)src[j + 192];
+    dst[j] = (__bf16)a;
+    dst[j + 64] = (__bf16)b;
+    dst[j + 128] = (__bf16)c;
+    dst[j + 192] = (__bf16)d;
+  }
+  for (; j < w; j += 64) dst[j] = (__bf16)(float)src[j];
 }
 
 // rows up to 16 x 64 elements: every load of the row's three tables is issued before the first
@@ -251,7 +266,11 @@ __global__ void __launch_bounds__(TPB) k_gather_rows(const int64_t* __restrict__
   }
   for (int t = 0; t < A.ntab; t++) {
     const GatherTab& T = A.t[t];
-    if (T.es == 4)
+    if (T.cvt == 1)
+      gather_row_bf16<_Float16>((const _Float16*)T.src + s * T.width, (__bf16*)T.dst + i * T.width, T.width, lane);
+    else if (T.cvt == 2)
+      gather_row_bf16<float>((const float*)T.src + s * T.width, (__bf16*)T.dst + i * T.width, T.width, lane);
+    else if (T.es == 4)
       gather_row<uint32_t>((const uint32_t*)T.src + s * T.width, (uint32_t*)T.dst + i * T.width, T.width, lane);
     else
       gather_row<uint16_t>((const uint16_t*)T.src + s * T.width, (uint16_t*)T.dst + i * T.width, T.width, lane);
@@ -263,20 +282,42 @@ __global__ void __launch_bounds__(TPB) k_gather_rows(const int64_t* __restrict__
 extern "C" int hg_gather_rows(const int64_t* idx, int64_t rows, int64_t src_rows, const void* src0, void* dst0,
                               int64_t width0, int es0, const void* src1, void* dst1, int64_t width1, int es1,
                               const void* src2, void* dst2, int64_t width2, int es2, void* stream) {
-  if (!idx || rows <= 0 || src_rows <= 0 || !src0 || !dst0) return HG_ERR_ARG;
-  GatherArgs A;
-  A.ntab = 0;
+  hg_gather_table T[3];
   const void* src[3] = {src0, src1, src2};
   void* dst[3] = {dst0, dst1, dst2};
   const int64_t w[3] = {width0, width1, width2};
   const int es[3] = {es0, es1, es2};
+  if (!src0) return HG_ERR_ARG;
+  int n = 0;
   for (int t = 0; t < 3; t++) {
     if (!src[t]) continue;
-    if (!dst[t] || w[t] <= 0 || (es[t] != 4 && es[t] != 2)) return HG_ERR_ARG;
-    A.t[A.ntab++] = GatherTab{src[t], dst[t], w[t], es[t]};
+    if (es[t] != 4 && es[t] != 2) return HG_ERR_ARG;
+    const int ty = es[t] == 4 ? HG_DTYPE_F32 : HG_DTYPE_F16;  // a 2-byte copy is type-agnostic
+    T[n++] = hg_gather_table{src[t], dst[t], w[t], ty, ty};
+  }
+  return hg_gather_rows_ex(idx, rows, src_rows, T, n, stream);
+}
+
+extern "C" int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_rows, const hg_gather_table* tabs,
+                                 int ntab, void* stream) {
+  if (!idx || rows <= 0 || src_rows <= 0 || !tabs || ntab < 1 || ntab > 3) return HG_ERR_ARG;
+  GatherArgs A;
+  A.ntab = 0;
+  for (int t = 0; t < ntab; t++) {
+    const hg_gather_table& g = tabs[t];
+    if (!g.src || !g.dst || g.width <= 0) return HG_ERR_ARG;
+    const auto bytes = [](int ty) { return ty == HG_DTYPE_F32 ? 4 : (ty == HG_DTYPE_F16 || ty == HG_DTYPE_BF16) ? 2 : 0; };
+    const int sb = bytes(g.src_dtype), db = bytes(g.dst_dtype);
+    if (!sb || !db) return HG_ERR_ARG;
+    int cvt = 0;
+    if (g.src_dtype != g.dst_dtype) {
+      if (g.dst_dtype != HG_DTYPE_BF16) return HG_ERR_ARG;
+      cvt = g.src_dtype == HG_DTYPE_F16 ? 1 : 2;
+    }
+    A.t[A.ntab++] = GatherTab{g.src, g.dst, g.width, sb, cvt};
   }
   A.short_rows = 1;
-  for (int t = 0; t < A.ntab; t++) A.short_rows &= (A.t[t].es == 4 && A.t[t].width <= 64 * GK);
+  for (int t = 0; t < A.ntab; t++) A.short_rows &= (A.t[t].cvt == 0 && A.t[t].es == 4 && A.t[t].width <= 64 * GK);
   const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
   hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(TPB), 0, (hipStream_t)stream, idx, rows, src_rows, A);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;

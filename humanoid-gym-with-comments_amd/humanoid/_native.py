@@ -99,11 +99,21 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_post", "hg_ep_stats_slot", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_stats_len", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
-           "hg_rollout_act", "hg_rollout_env", "hg_gather_rows", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
+           "hg_rollout_act", "hg_rollout_env", "hg_gather_rows", "hg_gather_rows_ex", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
            "hg_mlp_act_backward", "hg_mlp_act_backward_scratch", "hg_colsum_jobs", "hg_linear_skinny_supported",
-           "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch", "hg_version"]
+           "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch",
+           "hg_mlp_act_backward_bf16", "hg_linear_skinny_forward_bf16", "hg_linear_skinny_backward_bf16",
+           "hg_cast_bf16_jobs", "hg_version"]
 
 _LIB = None
+
+DTYPE_CODES = {"float32": 0, "float16": 1, "bfloat16": 2}  # HG_DTYPE_* of include/hgsim.h
+
+
+class GatherTable(ctypes.Structure):
+    """hg_gather_table (include/hgsim.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("width", ctypes.c_int64),
+                ("src_dtype", ctypes.c_int32), ("dst_dtype", ctypes.c_int32)]
 
 
 def load_library(path=LIB_PATH):
@@ -161,6 +171,8 @@ def load_library(path=LIB_PATH):
                                  vp]
     L.hg_ep_stats_slot.restype = ctypes.c_int
     L.hg_ep_stats_slot.argtypes = [vp]
+    L.hg_gather_rows_ex.restype = ctypes.c_int
+    L.hg_gather_rows_ex.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(GatherTable), ctypes.c_int, vp]
     L.hg_gather_rows.restype = ctypes.c_int
     L.hg_gather_rows.argtypes = [vp, ctypes.c_int64, ctypes.c_int64] + [vp, vp, ctypes.c_int64, ctypes.c_int] * 3 + [vp]
     L.hg_rollout_env.restype = ctypes.c_int
@@ -191,6 +203,17 @@ def load_library(path=LIB_PATH):
                                             ctypes.c_int, vp, vp]
     L.hg_linear_skinny_backward_scratch.restype = ctypes.c_int64
     L.hg_linear_skinny_backward_scratch.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    L.hg_mlp_act_backward_bf16.restype = ctypes.c_int
+    L.hg_mlp_act_backward_bf16.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp, vp]
+    L.hg_linear_skinny_forward_bf16.restype = ctypes.c_int
+    L.hg_linear_skinny_forward_bf16.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_int,
+                                                ctypes.c_int, vp]
+    L.hg_linear_skinny_backward_bf16.restype = ctypes.c_int
+    L.hg_linear_skinny_backward_bf16.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_int,
+                                                 ctypes.c_int, vp, vp]
+    L.hg_cast_bf16_jobs.restype = ctypes.c_int
+    L.hg_cast_bf16_jobs.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                    ctypes.c_int, vp]
     L.hg_version.restype = ctypes.c_char_p
     L.hg_version.argtypes = []
     return L

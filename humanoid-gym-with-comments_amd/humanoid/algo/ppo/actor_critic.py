@@ -60,8 +60,9 @@ class ActorCritic(nn.Module):
     def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=[256, 256, 256],
                  critic_hidden_dims=[256, 256, 256], base_lin_vel_hidden_dims=[128, 128], init_noise_std=1.0,
                  activation=nn.ELU(), policy_dtype="fp32", **kwargs):
-        """policy_dtype "bf16" (config 5): the three MLPs run under bf16 autocast on the GPU
-        (fp32 master weights and gradients, outputs returned as fp32); "fp32" is the reference."""
+        """policy_dtype "bf16" (config 5): the three MLPs run with bf16 activations and bf16
+        matrix-core GEMMs on the GPU (fp32 accumulation, fp32 master weights, gradients and
+        outputs; hg_mlp.mlp_forward_bf16); "fp32" is the reference."""
         if policy_dtype not in ("fp32", "bf16"):
             raise ValueError(f"policy_dtype must be 'fp32' or 'bf16', got {policy_dtype!r}")
         if kwargs:
@@ -81,6 +82,15 @@ class ActorCritic(nn.Module):
 
     def _mlp(self, net, x):
         if self.policy_dtype == "bf16" and x.is_cuda:
+            if self.fused_mlp:
+                ok = self._fusable.get(("bf16", id(net)))
+                if ok is None:
+                    ok = self._fusable[("bf16", id(net))] = hg_mlp.fusable_bf16(net)
+                if ok:
+                    # bf16 activations / GEMMs with fp32 accumulation, fp32 master weights and
+                    # outputs, fused bf16 backward (hg_mlp.py, csrc/hg_mlp.hip)
+                    return (hg_mlp.mlp_forward_bf16(net, x) if torch.is_grad_enabled()
+                            else hg_mlp.mlp_infer_bf16(net, x))
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 return net(x).float()
         x = x if x.dtype == torch.float32 else x.float()

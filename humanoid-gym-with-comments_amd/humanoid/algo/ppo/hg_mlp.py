@@ -226,3 +226,178 @@ def mlp_infer(net, x, out=None):
         out.view_as(y).copy_(y)
         return out
     return y
+
+
+# ---------------------------------------------------------------------------------------------
+# bf16 policy (config 5, ``policy_dtype="bf16"``).  Master weights, gradients and Adam stay fp32
+# (HgAdam unchanged); a forward casts the hidden layers' weights and biases to bf16 in one launch
+# (hg_cast_bf16_jobs) and runs the hidden GEMMs as bf16 x bf16 -> bf16 with fp32 accumulation
+# (hipBLASLt on the bf16 matrix cores), ELU in bf16.  The skinny output layer reads its bf16 input
+# with the fp32 W and writes fp32 (the loss, the sample and the value see fp32 outputs).  Backward:
+# the activation gradients flow in bf16 through the fused ELU-backward/bias pass
+# (hg_mlp_act_backward_bf16, fp32 bias partials), the weight gradients are bf16 GEMMs with fp32
+# output (``out_dtype=torch.float32``: no bf16 rounding of the accumulated gradient), and the
+# skinny layer's dW/db are fp32 partials of the same deterministic column sums.
+# ---------------------------------------------------------------------------------------------
+_BF16 = torch.bfloat16
+
+
+def fusable_bf16(net):
+    """fusable(net) with an output layer the skinny bf16-input kernels handle."""
+    if not fusable(net):
+        return False
+    last = list(net)[-1]
+    return bool(N.lib().hg_linear_skinny_supported(last.out_features, last.in_features))
+
+
+def cast_hidden_bf16(params):
+    """bf16 copies of the hidden layers' (W, b) — all but the last pair of ``params`` — in ONE
+    hg_cast_bf16_jobs launch.  Returns [W0, b0, W1, b1, ...] as bf16 tensors."""
+    src = [p.detach() for p in params[:-2]]
+    if not src:
+        return []
+    src = [p if p.is_contiguous() else p.contiguous() for p in src]
+    dst = [torch.empty(p.shape, dtype=_BF16, device=p.device) for p in src]
+    n = len(src)
+    vp = ctypes.c_void_p
+    rc = N.lib().hg_cast_bf16_jobs((vp * n)(*[p.data_ptr() for p in src]), (vp * n)(*[d.data_ptr() for d in dst]),
+                                   (ctypes.c_int64 * n)(*[p.numel() for p in src]), n, _stream(src[0].device))
+    if rc != 0:
+        raise RuntimeError(f"hg_cast_bf16_jobs failed ({rc})")
+    return dst
+
+
+def _skinny_ok_bf16(h, W):
+    n, k = W.shape
+    return (bool(N.lib().hg_linear_skinny_supported(n, k)) and h.dim() == 2 and h.dtype == _BF16
+            and h.stride(1) == 1 and h.stride(0) % 8 == 0 and h.data_ptr() % 16 == 0 and W.is_contiguous())
+
+
+def _skinny_forward_bf16(h, W, b, out=None):
+    rows, n = h.shape[0], W.shape[0]
+    y = torch.empty(rows, n, dtype=torch.float32, device=h.device) if out is None else out
+    if y.numel() != rows * n or not y.is_contiguous() or y.dtype != torch.float32:
+        raise RuntimeError("skinny forward: out must be a contiguous float32 tensor of rows x n elements")
+    rc = N.lib().hg_linear_skinny_forward_bf16(h.data_ptr(), h.stride(0), W.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                               rows, n, W.shape[1], _stream(h.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_linear_skinny_forward_bf16 failed ({rc})")
+    return y
+
+
+def _skinny_backward_bf16(g, h, W, need_dx, red):
+    rows, (n, k) = g.shape[0], W.shape
+    L = N.lib()
+    wb = torch.empty(n * k + n, dtype=torch.float32, device=g.device)
+    dx = torch.empty(rows, k, dtype=_BF16, device=g.device) if need_dx else None
+    scratch = torch.empty(int(L.hg_linear_skinny_backward_scratch(rows, n, k)), dtype=torch.float32, device=g.device)
+    rc = L.hg_linear_skinny_backward_bf16(g.data_ptr(), h.data_ptr(), h.stride(0), W.data_ptr(),
+                                          dx.data_ptr() if need_dx else None, None, rows, n, k, scratch.data_ptr(),
+                                          _stream(g.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_linear_skinny_backward_bf16 failed ({rc})")
+    red.add(scratch, wb, n * k + n, scratch.numel() // (n * k + n))
+    return wb[: n * k].view(n, k), wb[n * k:], dx
+
+
+def _act_backward_bf16(gy, y, gb, red):
+    rows, width = gy.shape
+    L = N.lib()
+    scratch = torch.empty(int(L.hg_mlp_act_backward_scratch(rows, width)), dtype=torch.float32, device=gy.device)
+    gh = torch.empty_like(gy)
+    rc = L.hg_mlp_act_backward_bf16(gy.data_ptr(), y.data_ptr(), gh.data_ptr(), rows, width, None,
+                                    scratch.data_ptr(), _stream(gy.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_mlp_act_backward_bf16 failed ({rc})")
+    red.add(scratch, gb, width, scratch.numel() // width)
+    return gh
+
+
+# Split-K of the bf16 weight gradients as rows per chunk (S = rows / chunk, a power of two that
+# divides rows): hipBLASLt's bf16 -> fp32 GEMM over the whole minibatch runs the [n, k] output on a
+# handful of tiles (160-260 us at 49152 rows).  Measured on MI355X (scripts/bf16_gemm_probe.py,
+# 49152 / 24576 rows, bmm with fp32 chunk outputs + the chunk-sum read): 512x705 260 -> 64 us
+# (S=32), 256x512 219 -> 30, 128x256 171 -> 21, 128x705 202 -> 42, 768x219 216 -> 44, 256x768
+# 226 -> 44; best at 1536-3072 rows per chunk (128x128: 6144).
+_DW_CHUNK_BF16 = {(128, 128): 6144, (128, 256): 3072}
+_DW_CHUNK_BF16_DEFAULT = 1536
+
+
+def _bf16_split(rows, n, k):
+    S = 1
+    chunk = _DW_CHUNK_BF16.get((n, k), _DW_CHUNK_BF16_DEFAULT)
+    while S < 64 and rows % (2 * S) == 0 and rows // (2 * S) >= chunk:
+        S *= 2
+    return S
+
+
+def _weight_grad_bf16(gh, x, red):
+    """dW[n, k] = gh^T x from bf16 operands, accumulated and returned in fp32."""
+    rows, n = gh.shape
+    k = x.shape[1]
+    S = _bf16_split(rows, n, k)
+    if S == 1:
+        return torch.mm(gh.t(), x, out_dtype=torch.float32)
+    chunks = torch.bmm(gh.view(S, rows // S, n).transpose(1, 2), x.view(S, rows // S, k), out_dtype=torch.float32)
+    dw = torch.empty(n, k, dtype=torch.float32, device=gh.device)
+    red.add(chunks, dw, n * k, S)
+    return dw
+
+
+def _hidden_forward_bf16(x, wb):
+    """bf16 input of every layer: [x, y_0, ..., y_{n-2}] (y_i = elu(h W_i^T + b_i) in bf16)."""
+    h = x if x.dtype == _BF16 else x.to(_BF16)
+    if not h.is_contiguous():
+        h = h.contiguous()
+    ins = [h]
+    for i in range(len(wb) // 2):
+        h = F.elu(torch.addmm(wb[2 * i + 1], h, wb[2 * i].t()))
+        ins.append(h)
+    return ins
+
+
+class _MLPbf16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, *params):
+        n = len(params) // 2
+        wb = cast_hidden_bf16(params)
+        ins = _hidden_forward_bf16(x, wb)
+        Wl, bl = params[-2], params[-1]
+        y = _skinny_forward_bf16(ins[-1], Wl, bl)
+        ctx.save_for_backward(*ins, *wb[0::2], Wl)
+        ctx.n = n
+        ctx.x_dtype = x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        ins, Wbs, Wl = saved[:n], saved[n:2 * n - 1], saved[2 * n - 1]
+        grads = [None] * (2 * n)
+        g = g.contiguous().float()
+        red = _Reductions()
+        need_x = ctx.needs_input_grad[0]
+        grads[-2], grads[-1], g = _skinny_backward_bf16(g, ins[n - 1], Wl, n > 1 or need_x, red)
+        for i in range(n - 2, -1, -1):
+            rows, width = g.shape
+            gb = torch.empty(width, dtype=torch.float32, device=g.device)
+            gh = _act_backward_bf16(g, ins[i + 1], gb, red)
+            grads[2 * i + 1] = gb
+            grads[2 * i] = _weight_grad_bf16(gh, ins[i], red)
+            g = torch.mm(gh, Wbs[i]) if (i > 0 or need_x) else None
+        red.launch(ins[0].device)
+        gx = g.to(ctx.x_dtype) if (need_x and g is not None) else None
+        return (gx, *grads)
+
+
+def mlp_forward_bf16(net, x):
+    """net(x) for a ``fusable_bf16`` nn.Sequential on the bf16 path, fp32 output, fused backward."""
+    return _MLPbf16.apply(x, *_params(net))
+
+
+def mlp_infer_bf16(net, x, out=None):
+    """net(x) on the bf16 path without autograd (rollout inference); fp32 output (into ``out``)."""
+    params = [p.detach() for p in _params(net)]
+    ins = _hidden_forward_bf16(x, cast_hidden_bf16(params))
+    return _skinny_forward_bf16(ins[-1], params[-2], params[-1], out)

@@ -483,6 +483,15 @@ class PPO:
         # minibatch needs three gathers (obs, critic obs, table) instead of ten
         A = st.actions.shape[-1]
         self._pack_src = [st.actions, st.values, st.returns, st.actions_log_prob, st.advantages, st.mu, st.sigma]
+        # bf16 policy on the fused path: the obs / critic minibatch rows are converted to bf16 by the
+        # gather (the networks' input dtype), and the lin-vel target — privileged obs [53:56],
+        # rollout_storage.py / ppo.py:160 — travels in the fp32 table so it keeps the storage's bits
+        ac = self.actor_critic
+        mb_dtype = (torch.bfloat16 if getattr(ac, "policy_dtype", "fp32") == "bf16" and ac.fused_mlp
+                    and self._fused_loss else None)
+        self._lin_vel_packed = mb_dtype is not None
+        if self._lin_vel_packed:
+            self._pack_src.append(critic.view(st.num_transitions_per_env, st.num_envs, -1)[..., 53:56])
         widths = [t.shape[-1] for t in self._pack_src]
         self._packed = torch.empty(obs.shape[0], sum(widths), dtype=torch.float32, device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
@@ -496,8 +505,8 @@ class PPO:
         if self._flat_grad is None:
             self.optimizer.zero_grad(set_to_none=True)  # backward allocates the grads in the graph pool
         # minibatch rows land in static buffers: the three row gathers are one HIP launch
-        self._mb_obs = torch.empty(mb, obs.shape[1], dtype=obs.dtype, device=dev)
-        self._mb_critic = (torch.empty(mb, critic.shape[1], dtype=critic.dtype, device=dev)
+        self._mb_obs = torch.empty(mb, obs.shape[1], dtype=mb_dtype or obs.dtype, device=dev)
+        self._mb_critic = (torch.empty(mb, critic.shape[1], dtype=mb_dtype or critic.dtype, device=dev)
                            if critic is not obs else self._mb_obs)
         self._mb_packed = torch.empty(mb, self._packed.shape[1], dtype=torch.float32, device=dev)
         tables = [(obs, self._mb_obs), (self._packed, self._mb_packed)]
@@ -534,7 +543,7 @@ class PPO:
         crit_b = self._mb_critic
         b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
         pk = self._mb_packed
-        for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma"),
+        for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma", "lin_vel"),
                               pk.split(self._mb_widths, dim=1)):
             b[name] = part
         if self._fused_loss:

@@ -165,23 +165,26 @@ class RolloutStorage:
 def gather_rows(idx, tables):
     """dst[i] = src[idx[i]] for up to three (src, dst) pairs of row-major [rows, width] device
     tensors (float32 / float16 / bfloat16), in one launch of the HIP gather kernel
-    (``hg_gather_rows``, csrc/hg_rollout.hip) on the current stream — graph-capturable.  Replaces
-    the `table[batch_idx]` gathers of the minibatch generator (rollout_storage.py:153-191)."""
+    (``hg_gather_rows_ex``, csrc/hg_rollout.hip) on the current stream — graph-capturable.  Replaces
+    the `table[batch_idx]` gathers of the minibatch generator (rollout_storage.py:153-191).  A
+    bfloat16 dst of a float16 / float32 src is converted on the way (the bf16 policy's inputs)."""
     from humanoid import _native as N
     if not 1 <= len(tables) <= 3:
         raise ValueError("gather_rows takes one to three (src, dst) pairs")
     if idx.dtype != torch.int64 or not idx.is_cuda or not idx.is_contiguous():
         raise RuntimeError("gather_rows: idx must be a contiguous int64 device tensor")
     rows, src_rows = idx.numel(), tables[0][0].shape[0]
-    args = []
-    for src, dst in tables:
-        if (src.dim() != 2 or not src.is_contiguous() or not dst.is_contiguous() or src.dtype != dst.dtype
-                or dst.shape != (rows, src.shape[1]) or src.shape[0] != src_rows or src.element_size() not in (2, 4)):
-            raise RuntimeError("gather_rows: src [R, W] and dst [rows, W] must be contiguous, same dtype, "
-                               "2- or 4-byte elements")
-        args += [ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), src.shape[1], src.element_size()]
-    args += [None, None, 0, 4] * (3 - len(tables))
+    tabs = (N.GatherTable * 3)()
+    for t, (src, dst) in enumerate(tables):
+        conv = src.dtype == dst.dtype or (dst.dtype == torch.bfloat16 and src.dtype in (torch.float16, torch.float32))
+        if (src.dim() != 2 or not src.is_contiguous() or not dst.is_contiguous() or not conv
+                or dst.shape != (rows, src.shape[1]) or src.shape[0] != src_rows
+                or str(src.dtype)[6:] not in N.DTYPE_CODES or str(dst.dtype)[6:] not in N.DTYPE_CODES):
+            raise RuntimeError("gather_rows: src [R, W] and dst [rows, W] must be contiguous float32 / float16 / "
+                               "bfloat16, same dtype or a bfloat16 dst")
+        tabs[t] = N.GatherTable(src.data_ptr(), dst.data_ptr(), src.shape[1], N.DTYPE_CODES[str(src.dtype)[6:]],
+                                N.DTYPE_CODES[str(dst.dtype)[6:]])
     s = ctypes.c_void_p(torch.cuda.current_stream(idx.device).cuda_stream)
-    rc = N.lib().hg_gather_rows(ctypes.c_void_p(idx.data_ptr()), rows, src_rows, *args, s)
+    rc = N.lib().hg_gather_rows_ex(ctypes.c_void_p(idx.data_ptr()), rows, src_rows, tabs, len(tables), s)
     if rc != 0:
-        raise RuntimeError(f"hg_gather_rows failed ({rc})")
+        raise RuntimeError(f"hg_gather_rows_ex failed ({rc})")

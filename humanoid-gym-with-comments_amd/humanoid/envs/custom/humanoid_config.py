@@ -245,7 +245,7 @@ class XBotLCfgPPO(BaseConfig):
         init_noise_std = 1.0
         actor_hidden_dims = [512, 256, 128]
         critic_hidden_dims = [768, 256, 128]
-        policy_dtype = "fp32"      # "bf16": MLPs under bf16 autocast (config 5)
+        policy_dtype = "fp32"      # "bf16": bf16 activations + matrix-core GEMMs, fp32 master weights (config 5)
 
     class algorithm:
         value_loss_coef = 1.0

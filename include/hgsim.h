@@ -273,6 +273,20 @@ int hg_gather_rows(const int64_t* idx, int64_t rows, int64_t src_rows, const voi
                    int64_t width0, int es0, const void* src1, void* dst1, int64_t width1, int es1,
                    const void* src2, void* dst2, int64_t width2, int es2, void* stream);
 
+/* Typed form: per table the source and destination element types (HG_DTYPE_*); equal types copy,
+ * fp16 -> bf16 and fp32 -> bf16 convert on the way (round-to-nearest-even) — the bf16 policy's
+ * minibatch inputs gathered straight from fp16 / fp32 rollout storage.  1 <= ntab <= 3. */
+enum { HG_DTYPE_F32 = 0, HG_DTYPE_F16 = 1, HG_DTYPE_BF16 = 2 };
+typedef struct hg_gather_table {
+  const void* src;
+  void* dst;
+  int64_t width;
+  int32_t src_dtype;
+  int32_t dst_dtype;
+} hg_gather_table;
+int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_rows, const hg_gather_table* tabs, int ntab,
+                      void* stream);
+
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----
  * A list of float32 device tensors (param, grad, Adam exp_avg / exp_avg_sq, per-tensor step
@@ -367,6 +381,22 @@ int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, cons
                               float* grad_wb, int64_t rows, int n, int k,
                               float* scratch /* >= hg_linear_skinny_backward_scratch() floats */, void* stream);
 int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k);
+/* bf16 policy (config 5, policy_dtype "bf16"): the same three passes with the activations,
+ * activation gradients and hidden-layer inputs in bf16 (uint16_t bit patterns, round-to-nearest-
+ * even), all accumulation, bias/weight-gradient partials, W of the skinny layer and its output y /
+ * incoming gradient gh in float32.  Alignment: the bf16 arrays of the activation backward 8-byte,
+ * skinny x rows 16-byte (ldx % 8 == 0), skinny h / dx 4-byte. */
+int hg_mlp_act_backward_bf16(const uint16_t* gy, const uint16_t* y, uint16_t* gh, int64_t rows, int width,
+                             float* grad_bias, float* scratch /* >= hg_mlp_act_backward_scratch() floats */,
+                             void* stream);
+int hg_linear_skinny_forward_bf16(const uint16_t* x, int64_t ldx, const float* W, const float* b, float* y,
+                                  int64_t rows, int n, int k, void* stream);
+int hg_linear_skinny_backward_bf16(const float* gh, const uint16_t* h, int64_t ldh, const float* W, uint16_t* dx,
+                                   float* grad_wb, int64_t rows, int n, int k,
+                                   float* scratch /* >= hg_linear_skinny_backward_scratch() floats */, void* stream);
+/* dst[j][0..count[j]) = bf16(src[j][...]) for j < njobs <= 32, one launch (the bf16 copies of
+ * the fp32 master weights a bf16 forward reads). */
+int hg_cast_bf16_jobs(const float* const* src, uint16_t* const* dst, const int64_t* count, int njobs, void* stream);
 /* Batched column sums (the deferred reductions of one MLP backward in one launch: bias-gradient
  * tile partials and split-K weight-gradient chunks, replacing per-layer grad.sum(0) launches):
  * dst[j][c] = sum over p < parts[j] of src[j][p * width[j] + c], fixed order, for j < njobs <= 16.

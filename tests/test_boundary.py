@@ -50,12 +50,15 @@ def test_library_loads_without_gpu():
 def test_struct_layouts_match_header(tmp_path):
     c = tmp_path / "sz.c"
     c.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "hgsim.h"\nint main(){printf("%zu %zu %zu %zu %zu",'
-                 'sizeof(hg_model),sizeof(hg_cfg),offsetof(hg_cfg,heightfield),offsetof(hg_cfg,seed),sizeof(hg_desc));}')
+                 'sizeof(hg_model),sizeof(hg_cfg),offsetof(hg_cfg,heightfield),offsetof(hg_cfg,seed),sizeof(hg_desc));'
+                 'printf(" %zu %zu %zu",sizeof(hg_gather_table),offsetof(hg_gather_table,width),'
+                 'offsetof(hg_gather_table,dst_dtype));}')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(c), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(N.HgModel), ctypes.sizeof(N.HgCfg), N.HgCfg.heightfield.offset, N.HgCfg.seed.offset,
-            ctypes.sizeof(N.HgDesc)]
+            ctypes.sizeof(N.HgDesc), ctypes.sizeof(N.GatherTable), N.GatherTable.width.offset,
+            N.GatherTable.dst_dtype.offset]
     assert got == want
 
 

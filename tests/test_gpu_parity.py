@@ -973,6 +973,72 @@ def test_fused_mlp_backward_matches_torch():
     torch.testing.assert_close(gx_f, gx_t, rtol=2e-4, atol=2e-5)
 
 
+# bf16 policy tolerance (config 5), relative L2 error ||a - b|| / ||b|| against the fp32 torch
+# reference on the same fp32 master weights: outputs and every parameter / input gradient.  bf16
+# keeps 8 significant bits (unit roundoff 2^-9 = 2e-3); over the 3-4 layers the measured errors are
+# (1-7)e-3 (autocast: (1-8)e-3), so the bound is BF16_REL_TOL = 1.5e-2.  And the fused path must be as accurate as torch
+# autocast on the same network: error <= 1.25 x autocast's + 1e-3.
+BF16_REL_TOL = 1.5e-2
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("B", [3001, 8192])
+def test_bf16_mlp_matches_fp32_reference(B):
+    """policy_dtype "bf16": hg_mlp.mlp_forward_bf16 (bf16 activations and matrix-core GEMMs, fused
+    bf16 ELU-backward / bias pass, fp32-output weight gradients, skinny bf16-input output layer)
+    against torch fp32 autograd of the same nn.Sequential (actor_critic.py:36-149), at the stated
+    bf16 tolerance; 8192 rows take the split-K weight-gradient path.  Also the rollout inference
+    path (no autograd)."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic
+    torch.manual_seed(11)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     base_lin_vel_hidden_dims=[128, 128], policy_dtype="bf16").cuda()
+    obs = torch.randn(B, 705, device="cuda:0")
+    critic = torch.randn(B, 219, device="cuda:0")
+    w_mu, w_v, w_lv = (torch.randn(B, 12, device="cuda:0"), torch.randn(B, 1, device="cuda:0"),
+                       torch.randn(B, 3, device="cuda:0"))
+
+    def run(mode):
+        for p in ac.parameters():
+            p.grad = None
+        x = obs.clone().requires_grad_()
+        if mode == "fp32":
+            mu, v, lv = ac.actor(x), ac.critic(critic), ac.base_lin_vel(x)
+        else:
+            ac.fused_mlp = mode == "fused"
+            mu, v, lv = ac._mlp(ac.actor, x), ac._mlp(ac.critic, critic), ac._mlp(ac.base_lin_vel, x)
+            assert mu.dtype == torch.float32 and v.dtype == torch.float32
+        ((mu * w_mu).sum() + (v * w_v).sum() + (lv * w_lv).sum()).backward()
+        names = [n for n, p in ac.named_parameters() if p.grad is not None]
+        return ([t.detach().clone() for t in (mu, v, lv)], dict(zip(names, [p.grad.clone() for n, p in
+                ac.named_parameters() if p.grad is not None])), x.grad.clone())
+
+    out_r, g_r, gx_r = run("fp32")
+    out_a, g_a, gx_a = run("autocast")
+    out_f, g_f, gx_f = run("fused")
+    assert set(g_f) == set(g_r)
+    errs = {}
+    for name, a, ac_, r in [(f"out{i}", out_f[i], out_a[i], out_r[i]) for i in range(3)] + \
+            [(n, g_f[n], g_a[n], g_r[n]) for n in g_r if n != "std"] + [("dx", gx_f, gx_a, gx_r)]:
+        e, ea = _rel(a, r), _rel(ac_, r)
+        errs[name] = (e, ea)
+        assert e <= BF16_REL_TOL, f"{name}: bf16 rel err {e:.3e} > {BF16_REL_TOL}"
+        assert e <= 1.25 * ea + 1e-3, f"{name}: fused bf16 rel err {e:.3e} vs autocast {ea:.3e}"
+    print("bf16 rel errors (fused, autocast):", {k: (round(v[0], 5), round(v[1], 5)) for k, v in errs.items()})
+    with torch.no_grad():
+        ac.fused_mlp = True
+        for net, inp in ((ac.actor, obs), (ac.critic, critic), (ac.base_lin_vel, obs)):
+            y = ac._mlp(net, inp)
+            assert _rel(y, net(inp)) <= BF16_REL_TOL
+            # inference and training forward compute the same bf16 arithmetic
+            with torch.enable_grad():
+                torch.testing.assert_close(y, ac._mlp(net, inp).detach(), rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_gather_rows_matches_torch_indexing(dtype):
     """hg_gather_rows vs table[idx] (the reference generator's gathers, rollout_storage.py:153-191):
@@ -993,6 +1059,31 @@ def test_gather_rows_matches_torch_indexing(dtype):
         assert torch.equal(d0, obs[idx]) and torch.equal(d1, crit[idx]) and torch.equal(d2, pk[idx])
     with pytest.raises(RuntimeError):
         gather_rows(idx, [(obs, torch.empty(rows, 705, dtype=torch.float64, device="cuda:0"))])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_gather_rows_to_bf16(dtype):
+    """hg_gather_rows_ex with a bfloat16 destination (the bf16 policy's minibatch inputs): the
+    gathered rows equal torch's table[idx].to(bfloat16) bitwise (round-to-nearest-even), an fp32
+    table in the same launch is copied unchanged."""
+    _need_gpu()
+    from humanoid.algo.ppo.rollout_storage import gather_rows
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    R = 24 * 96
+    obs = (torch.randn(R, 705, device="cuda:0", generator=g) * 7).to(dtype)
+    crit = (torch.randn(R, 219, device="cuda:0", generator=g) * 1e-3).to(dtype)
+    pk = torch.randn(R, 43, device="cuda:0", generator=g)
+    for rows in (R // 4, 1, 333):
+        idx = torch.randperm(R, device="cuda:0", generator=g)[:rows]
+        d0 = torch.empty(rows, 705, dtype=torch.bfloat16, device="cuda:0")
+        d1 = torch.empty(rows, 219, dtype=torch.bfloat16, device="cuda:0")
+        d2 = torch.empty(rows, 43, device="cuda:0")
+        gather_rows(idx, [(obs, d0), (crit, d1), (pk, d2)])
+        torch.cuda.synchronize()
+        assert torch.equal(d0, obs[idx].to(torch.bfloat16)) and torch.equal(d1, crit[idx].to(torch.bfloat16))
+        assert torch.equal(d2, pk[idx])
+    with pytest.raises(RuntimeError):  # bf16 -> fp16 is not a supported conversion
+        gather_rows(idx, [(d0, torch.empty(rows, 705, dtype=torch.float16, device="cuda:0"))])
 
 
 def test_deferred_mlp_reductions_match():
