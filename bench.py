@@ -34,10 +34,11 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) dense peak
 HBM_PEAK_GBS = 8000.0
-# K_step algorithmic HBM bytes per env and launch: 492 B read (state, actions,
-# warm-start impulses) + 1316 B written (rigid 13x13, contacts 13x3, root, dofs, torques, actions,
-# warm-start) + 192 B of next-step observation noise (48 floats)
-KSTEP_BYTES_PER_ENV = 492 + 1316 + 192
+# K_step algorithmic HBM bytes per env and launch: 732 B read (policy actions,
+# previous actions, dof pos / vel, root, 120 warm-start impulses, mass, friction) + 1748 B written
+# (actions, rigid 13x13, contacts 13x3, root, dof pos / vel, torques, 120 warm-start impulses, and
+# the next post launch's 48 observation-noise normals)
+KSTEP_BYTES_PER_ENV = 732 + 1748
 PROFILE_DIR = "r2_v1"  # the committed rocprofv3 summaries of the current kernels
 PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
