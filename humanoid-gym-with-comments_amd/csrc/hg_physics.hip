@@ -55,20 +55,20 @@ struct __align__(16) EnvSh {
   float root[16];
   float q[12], qd[12], act[12], tau[12];
   float pd_kp[12], pd_kd[12], pd_lim[12], pd_tgt[12], madd[12];
-  float nu[20];
-  float h[20];
-  float gv[20];            // g = L^-1 (tau - h), legs-first order
-  float invd[20];          // 1 / L_kk
+  alignas(16) float nu[20];
+  alignas(16) float h[20];
+  alignas(16) float gv[20];  // g = L^-1 (tau - h), legs-first order
+  alignas(16) float invd[20];  // 1 / L_kk
   float lamst[HG_LAMW];
   float R[13][9];
   float o[13][3], a[13][3], w[13][3], v[13][3];
   float cm[13], cs[13][3], cJ[13][6];
-  union {
+  union alignas(16) {
     struct { float al[13][3], ac[13][3], f[13][3], n[13][3]; } kin;  // RNEA scratch
     float Z[RMAX][20];                                                 // z_r rows, legs-first order
     struct { float rigid[13 * 13]; float cf[13 * 3]; } out;            // epilogue staging
   } u;
-  float L[18][20];         // M (dof order, lower) then its Cholesky factor (legs-first order)
+  alignas(16) float L[18][20];  // M (dof order, lower) then its Cholesky factor (legs-first order)
   float colbuf[20], colbuf2[20], bbuf[20];  // Cholesky column / right-hand-side broadcasts
   GroupC grp[NGRP];
   ContactC ct[MAX_PTS];
@@ -81,9 +81,30 @@ struct __align__(16) EnvSh {
   float mass0, fric;
   int nrows, npts, bad;
 };
+static_assert(offsetof(EnvSh, L) % 16 == 0 && offsetof(EnvSh, invd) % 16 == 0 && offsetof(EnvSh, gv) % 16 == 0 &&
+              offsetof(EnvSh, u) % 16 == 0, "16-byte LDS row accesses (ld_vec / st_vec)");
 
 __device__ __forceinline__ f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ void st3(float* p, f3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+// N consecutive floats from / to 16-byte-aligned LDS as 16-byte accesses with immediate offsets
+// (N rounded up to a multiple of 4 on loads: the rows read this way are padded to 20 floats)
+// out must hold N rounded up to a multiple of 4
+__device__ __forceinline__ void ld_vec(const float* p, float* out, int N) {  // N: constant after unrolling
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    if (4 * q >= N) break;
+    const float4 t = reinterpret_cast<const float4*>(p)[q];
+    out[4 * q] = t.x; out[4 * q + 1] = t.y; out[4 * q + 2] = t.z; out[4 * q + 3] = t.w;
+  }
+}
+template <int N>
+__device__ __forceinline__ void st_vec(float* p, const float* in) {
+#pragma unroll
+  for (int q = 0; q < N / 4; q++)
+    reinterpret_cast<float4*>(p)[q] = make_float4(in[4 * q], in[4 * q + 1], in[4 * q + 2], in[4 * q + 3]);
+  if (N % 4 >= 2) reinterpret_cast<float2*>(p)[2 * (N / 4)] = make_float2(in[N & ~3], in[(N & ~3) + 1]);
+  if (N % 2) p[N - 1] = in[N - 1];
+}
 __device__ __forceinline__ f3 mv3(const float* R, f3 v) {
   return mk(R[0] * v.x + R[1] * v.y + R[2] * v.z, R[3] * v.x + R[4] * v.y + R[5] * v.z,
             R[6] * v.x + R[7] * v.y + R[8] * v.z);
@@ -453,6 +474,38 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   for (int i = l; i < 18 * 20; i += 32) (&E.L[0][0])[i] = 0.f;  // the left-right cross block stays zero
   const int decimation = cfg->decimation;
+  // per-lane model constants of the detection phase, in registers for the whole launch (they
+  // were global loads at the head of every substep's detection): this lane's ground candidate
+  // (body, sole point / sphere centre, radius) or capsule pair (bodies, segment ends, radii),
+  // and its joint's limits and friction
+  const int nleg = M->num_leg_contacts, npair = M->num_pairs, nitems = M->num_contacts + npair;
+  const bool det_pair = l >= nleg && l < nleg + npair;
+  const int det_c = min(l < nleg ? l : l - npair, HG_MAX_CONTACTS - 1);
+  const int det_p = min(max(l - nleg, 0), HG_MAX_PAIRS - 1);
+  int det_b0, det_b1;
+  float det_k[14];
+  if (!det_pair) {
+    det_b0 = M->contact_body[det_c];
+    det_b1 = -1;
+    const f3 cp = ld3(M->contact_pos[det_c]);
+    det_k[0] = cp.x; det_k[1] = cp.y; det_k[2] = cp.z;
+    det_k[3] = M->contact_radius[det_c];
+#pragma unroll
+    for (int i = 4; i < 14; i++) det_k[i] = 0.f;
+  } else {
+    const int ca = M->pair[det_p][0], cb = M->pair[det_p][1];
+    det_b0 = M->capsule_body[ca];
+    det_b1 = M->capsule_body[cb];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      det_k[i] = M->capsule_p0[ca][i]; det_k[3 + i] = M->capsule_p1[ca][i];
+      det_k[6 + i] = M->capsule_p0[cb][i]; det_k[9 + i] = M->capsule_p1[cb][i];
+    }
+    det_k[12] = M->capsule_radius[ca];
+    det_k[13] = M->capsule_radius[cb];
+  }
+  const int lj = l < 12 ? l + 1 : 1;
+  const float lim_lo = M->lower[lj], lim_hi = M->upper[lj], jfric = M->joint_friction[lj];
 
   for (int sub = 0; sub < decimation; sub++) {
     // lane masks are rebuilt per substep (v_cmp) instead of living across the loop in SGPR pairs
@@ -522,11 +575,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // and the rank-1 update is one FMA per trailing entry.  The right-hand side b = tau - h rides
     // along in the same broadcasts: g = L^-1 b comes out of the same steps.
     {
-      float a[18];
+      float a[20];  // 18 used; ld_vec fills whole 16-byte groups
       bool nonpd = false;
       const int ol = l < 12 ? 6 + l : l - 12;  // this lane's dof
+      ld_vec(E.L[l < 18 ? l : 0], a, 18);
 #pragma unroll
-      for (int k = 0; k < 18; k++) a[k] = (l < nf && k <= l) ? E.L[l < 18 ? l : 0][k] : 0.f;
+      for (int k = 0; k < 18; k++) a[k] = (l < nf && k <= l) ? a[k] : 0.f;
       float bv = (l < 18) ? (ol >= 6 ? E.tau[(ol >= 6 ? ol : 6) - 6] : 0.f) - E.h[l < 18 ? ol : 0] : 0.f;
       asm volatile("" ::: "memory");
       // steps 0..5: the left-leg pivot j and the right-leg pivot 6 + j together (a left-leg row has
@@ -569,10 +623,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int k = j + 1; k < nf; k++) a[k] -= t * E.colbuf[k];
       }
-      if (l < nf) {
-#pragma unroll
-        for (int k = 0; k < 18; k++) E.L[l][k] = a[k];
-      }
+      if (l < nf) st_vec<18>(E.L[l], a);
       if (l == 0 && nonpd) E.bad = 1;
     }
     __syncthreads();
@@ -580,20 +631,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // [0, num_leg_contacts), the leg-vs-leg capsule pairs, the remaining ground candidates),
     // joint limits, and row allocation by ballot / popcount
     {
-      const int nleg = M->num_leg_contacts, npair = M->num_pairs, nitems = M->num_contacts + npair;
       bool act_c = false;
       f3 cn = mk(0, 0, 1), xP = mk(0, 0, 0), xN = mk(0, 0, 0);
       float phi = 0.f, mu = 0.f;
       int bP = -1, bN = -1, lam_base = 0;
       if (l < nitems) {
-        const bool is_pair = l >= nleg && l < nleg + npair;
-        if (!is_pair) {
-          const int c = l < nleg ? l : l - npair;
-          const int b = M->contact_body[c];
-          const f3 x = ld3(E.o[b]) + mv3(E.R[b], ld3(M->contact_pos[c]));
+        if (!det_pair) {
+          const int c = det_c;
+          const int b = det_b0;
+          const f3 x = ld3(E.o[b]) + mv3(E.R[b], mk(det_k[0], det_k[1], det_k[2]));
           float hg;
           ground(cfg, x.x + E.root[0], x.y + E.root[1], &hg, &cn);
-          const float r = M->contact_radius[c];
+          const float r = det_k[3];
           phi = (x.z + E.root[2] - hg) * cn.z - r;
           xP = x - r * cn;
           bP = b;
@@ -601,17 +650,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           lam_base = 3 * c;
           act_c = !fixed && phi < cfg->contact_offset;
         } else {
-          const int p = l - nleg;
-          const int ca = M->pair[p][0], cb = M->pair[p][1];
-          const int ba = M->capsule_body[ca], bb = M->capsule_body[cb];
+          const int p = det_p;
+          const int ba = det_b0, bb = det_b1;
           const f3 oa = ld3(E.o[ba]), ob = ld3(E.o[bb]);
           f3 pa, pb;
-          seg_seg(oa + mv3(E.R[ba], ld3(M->capsule_p0[ca])), oa + mv3(E.R[ba], ld3(M->capsule_p1[ca])),
-                  ob + mv3(E.R[bb], ld3(M->capsule_p0[cb])), ob + mv3(E.R[bb], ld3(M->capsule_p1[cb])), pa, pb);
+          seg_seg(oa + mv3(E.R[ba], mk(det_k[0], det_k[1], det_k[2])), oa + mv3(E.R[ba], mk(det_k[3], det_k[4], det_k[5])),
+                  ob + mv3(E.R[bb], mk(det_k[6], det_k[7], det_k[8])), ob + mv3(E.R[bb], mk(det_k[9], det_k[10], det_k[11])),
+                  pa, pb);
           const f3 dv = pb - pa;
           const float dist = sqrtf(dot(dv, dv));
           cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);
-          const float ra = M->capsule_radius[ca], rb = M->capsule_radius[cb];
+          const float ra = det_k[12], rb = det_k[13];
           phi = dist - ra - rb;
           xP = pb - rb * cn;
           xN = pa + ra * cn;
@@ -625,10 +674,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       bool act_l = false, has_f = false;
       float gapv = 0.f, sgnv = 1.f, ffric = 0.f;
       if (l < 12) {
-        const float glo = E.q[l] - M->lower[l + 1], ghi = M->upper[l + 1] - E.q[l];
+        const float glo = E.q[l] - lim_lo, ghi = lim_hi - E.q[l];
         if (glo < 0.01f) { act_l = true; gapv = glo; sgnv = 1.f; }
         else if (ghi < 0.01f) { act_l = true; gapv = ghi; sgnv = -1.f; }
-        ffric = M->joint_friction[l + 1];
+        ffric = jfric;
         has_f = ffric > 0.f;
       }
       const uint32_t mc = (uint32_t)(__ballot(act_c) >> (32 * half));
@@ -751,22 +800,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
       for (int i = 0; i < 18; i++) v0 += J[i] * E.nu[i];
       // forward substitution with L broadcast from LDS (legs-first order; arrow structure)
+      float invd[20], gvr[20];
+      ld_vec(E.invd, invd, 20);
+      ld_vec(E.gv, gvr, 20);
 #pragma unroll
       for (int k = 0; k < 18; k++) {
         if (k >= nf) { z[k] = 0.f; continue; }
         float s = J[k < 12 ? 6 + k : k - 12];
+        float Lk[20];
+        ld_vec(E.L[k], Lk, k);  // row k below the diagonal
 #pragma unroll
         for (int m = 0; m < k; m++) {
           if (k >= 6 && k < 12 && m < 6) continue;
-          s -= E.L[k][m] * z[m];
+          s -= Lk[m] * z[m];
         }
-        z[k] = s * E.invd[k];
+        z[k] = s * invd[k];
       }
 #pragma unroll
-      for (int k = 0; k < nf; k++) v0 += dt * (z[k] * E.gv[k]);  // gv[k >= nf] is never written (fixed base)
+      for (int k = 0; k < nf; k++) v0 += dt * (z[k] * gvr[k]);  // gv[k >= nf] is never written (fixed base)
     }
-#pragma unroll
-    for (int k = 0; k < 18; k++) E.u.Z[l][k] = z[k];
+    st_vec<18>(E.u.Z[l], z);
     // the group constants below read the neighbouring lanes' rows: a barrier, not program order
     // (per lane, Z[l-1] and Z[l] are different addresses the compiler may reorder around)
     __syncthreads();
@@ -800,11 +853,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     {
       float Dd = 0.f, W1 = 0.f, W2 = 0.f;  // W[l][l], W[l][l-1], W[l][l-2]
       const int l1 = l >= 1 ? l - 1 : 0, l2 = l >= 2 ? l - 2 : 0;
+      float z1[20], z2[20];
+      ld_vec(E.u.Z[l1], z1, 18);
+      ld_vec(E.u.Z[l2], z2, 18);
 #pragma unroll
       for (int k = 0; k < 18; k++) {
         Dd += z[k] * z[k];
-        W1 += z[k] * E.u.Z[l1][k];
-        W2 += z[k] * E.u.Z[l2][k];
+        W1 += z[k] * z1[k];
+        W2 += z[k] * z2[k];
       }
       const int g = l / 3, k = l % 3;
       E.grp[g].invD[k] = own ? __builtin_amdgcn_rcpf(Dd) : 0.f;
@@ -890,25 +946,42 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int m = 0; m < RMAX; m++) E.rLam[m] = lam[m];
       }
+      // back substitution L^T x = y, column-oriented: the base pivots 17..12, then the two legs'
+      // pivots 6 + k and k together (a leg's column has no rows in the other leg, so the two
+      // chains are independent): 12 broadcast round trips instead of 18, the same operations per
+      // element in the same order
 #pragma unroll
-      for (int j = nf - 1; j >= 0; j--) {
+      for (int j = nf - 1; j >= 12; j--) {
         const float xj = swz(y, j) * E.invd[j];
-        const int lo = (j >= 6 && j < 12) ? 6 : 0;  // a right-leg column has no left-leg rows
+        y = (l == j) ? xj : ((l < j) ? y - E.L[j][l < 18 ? l : 0] * xj : y);
+      }
+#pragma unroll
+      for (int k = 5; k >= 0; k--) {
+        const int jr = 6 + k, jl = k;
+        const float xr = swz(y, jr) * E.invd[jr];
+        const float xl = swz(y, jl) * E.invd[jl];
+        const bool right = l >= 6 && l < 12;
+        const int j = right ? jr : jl;
+        const float xj = right ? xr : xl;
+        const int lo = right ? 6 : 0;
         y = (l == j) ? xj : ((l >= lo && l < j) ? y - E.L[j][l < 18 ? l : 0] * xj : y);
       }
       __syncthreads();
       float nu_new = 0.f;
       const int od = l < 12 ? 6 + l : l - 12;
       if (l < 18) nu_new = E.nu[l < 18 ? od : 0] + (l < nf ? y : 0.f);
-      // contact forces (net per body, world frame, last substep) and warm-start store
-      for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
+      // contact forces (net per body, world frame; only the last substep's are reported) and
+      // warm-start store
+      const bool last_sub = sub == decimation - 1;
+      if (last_sub)
+        for (int i = l; i < 13 * 3; i += 32) (&E.cf[0][0])[i] = 0.f;
       const float mylam = own ? E.rLam[l] : 0.f;
       const bool fin = (l >= 18) || isfinite(nu_new);
       if ((uint32_t)(__ballot(!fin) >> (32 * half)) != 0u && l == 0) E.bad = 1;
       __syncthreads();
       if (own) {
         E.lamst[E.rlam[l]] = mylam;
-        if (l < 3 * E.npts) {
+        if (last_sub && l < 3 * E.npts) {
           const ContactC& C = E.ct[l / 3];
           const int bP = C.bP, bN = C.bN;
           const f3 d = ld3(C.dir[l % 3]);
