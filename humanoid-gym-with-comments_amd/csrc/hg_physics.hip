@@ -34,14 +34,15 @@ constexpr int LAM_LIM = LAM_PAIR + HG_MAX_PAIRS * 3;
 constexpr int LAM_FRIC = LAM_LIM + HG_ND;
 constexpr float BIG = 3.0e38f;
 
-struct GroupC {  // PGS constants of one 3-slot group (a, b, c), one broadcast read per field
+struct __align__(16) GroupC {  // PGS constants of one 3-slot group (a, b, c): five 16-byte reads
   float invD[3];
   float Wba, Wca, Wcb;     // W[b][a], W[c][a], W[c][b]
   float tgt[3], lo[3], hi[3];
   float mu;
   int contact;             // 1: (a, b, c) = a contact's normal and tangent pair; 0: single rows
-  int pad;
+  int pad[3];
 };
+static_assert(sizeof(GroupC) == 80, "GroupC is five 16-byte LDS reads");
 
 struct ContactC {  // one active contact: points on the two bodies (base-centred), normal + tangents
   float xP[3], xN[3];
@@ -70,7 +71,7 @@ struct __align__(16) EnvSh {
   } u;
   alignas(16) float L[18][20];  // M (dof order, lower) then its Cholesky factor (legs-first order)
   float colbuf[20], colbuf2[20], bbuf[20];  // Cholesky column / right-hand-side broadcasts
-  GroupC grp[NGRP];
+  alignas(16) GroupC grp[NGRP];
   ContactC ct[MAX_PTS];
   float rd[RMAX][3];       // joint rows: sign in rd[r][0]
   int rbP[RMAX], rbN[RMAX];// joint rows: rbP = -1 - dof
@@ -885,7 +886,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     {
       float vrow = v0;
       const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;
-      const int npts_min = min(shm[0].npts, shm[1].npts), npts_max = max(shm[0].npts, shm[1].npts);
       const int npgs = cfg->pgs_iterations;
       for (int it = 0; it < npgs; it++) {
 #pragma unroll
@@ -899,19 +899,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const float na = clampf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0], G.hi[0]);
             const float da = na - la;
             const float vb1 = vb + G.Wba * da, vc1 = vc + G.Wca * da;
+            // both row kinds computed, picked per env (branch-free: one instruction stream for
+            // every group, no scalar branches on the chain)
             float db, dc;
-            if (g < npts_min) {          // a contact in both envs: tangent pair on the friction disc
-              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
-              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
-              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
-              db = l1 * sc - lb;
-              dc = l2 * sc - lc;
-            } else if (g >= npts_max) {  // single rows in both envs, in sequence
-              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
-              db = nbs - lb;
-              const float vc2 = vc1 + G.Wcb * db;
-              dc = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]) - lc;
-            } else {                     // mixed: both, picked per env
+            {
               const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
               const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
               const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
