@@ -70,7 +70,11 @@ struct __align__(16) EnvSh {
     struct { float rigid[13 * 13]; float cf[13 * 3]; } out;            // epilogue staging
   } u;
   alignas(16) float L[18][20];  // M (dof order, lower) then its Cholesky factor (legs-first order)
-  float colbuf[20], colbuf2[20], bbuf[20];  // Cholesky column / right-hand-side broadcasts
+  // Cholesky column / right-hand-side broadcasts: one slot per lane (every lane writes, no
+  // exec-mask branch), rows 0..17 read back as 16-byte groups
+  alignas(16) float colbuf[32];
+  alignas(16) float colbuf2[32];
+  alignas(16) float bbuf[32];
   alignas(16) GroupC grp[NGRP];
   ContactC ct[MAX_PTS];
   float rd[RMAX][3];       // joint rows: sign in rd[r][0]
@@ -587,43 +591,53 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       // steps 0..5: the left-leg pivot j and the right-leg pivot 6 + j together (a left-leg row has
       // L[.][6 + j] = 0, so its right-pivot multiplier is 0, and vice versa; base rows take both
       // updates, which commute); steps 6..: the base pivots
+      float my_inv = 0.f, my_g = 0.f;  // this lane's pivot (l == j): 1 / L_ll and g_l, stored after the loop
 #pragma unroll
       for (int j = 0; j < 6; j++) {
         const int j2 = 6 + j;
-        if (l < 18) { E.colbuf[l] = a[j]; E.colbuf2[l] = a[j2]; E.bbuf[l] = bv; }
-        const float d1 = E.colbuf[j], d2 = E.colbuf2[j2], b1 = E.bbuf[j], b2 = E.bbuf[j2];
+        E.colbuf[l] = a[j]; E.colbuf2[l] = a[j2]; E.bbuf[l] = bv;
+        float c1[20], c2[20];  // column j (rows 0..7, 12..19) and column j2 (rows 4..19)
+        ld_vec(E.colbuf, c1, 8);
+        ld_vec(E.colbuf + 12, c1 + 12, 8);
+        ld_vec(E.colbuf2 + 4, c2 + 4, 16);
+        const float d1 = c1[j], d2 = c2[j2], b1 = E.bbuf[j], b2 = E.bbuf[j2];
         nonpd |= !(d1 > 0.f) || !(d2 > 0.f);
         const float inv1 = __builtin_amdgcn_rsqf(fmaxf(d1, 1e-20f));  // 1 / L_jj (1 ulp)
         const float inv2 = __builtin_amdgcn_rsqf(fmaxf(d2, 1e-20f));
         const float g1 = b1 * inv1, g2 = b2 * inv2;
-        if (l == 0) { E.invd[j] = inv1; E.invd[j2] = inv2; E.gv[j] = g1; E.gv[j2] = g2; }
         const int lo = lane_opaque(l);
+        my_inv = lo == j ? inv1 : (lo == j2 ? inv2 : my_inv);
+        my_g = lo == j ? g1 : (lo == j2 ? g2 : my_g);
         const float t1 = lo > j ? a[j] * (inv1 * inv1) : 0.f;     // L[l][j] / L[j][j] (0 on right-leg rows)
         const float t2 = lo > j2 ? a[j2] * (inv2 * inv2) : 0.f;   // L[l][j2] / L[j2][j2] (0 on left-leg rows)
         a[j] = lo >= j ? a[j] * inv1 : a[j];
         a[j2] = lo >= j2 ? a[j2] * inv2 : a[j2];
         bv -= t1 * b1 + t2 * b2;                                   // b_l -= L[l][j] g_j + L[l][j2] g_j2
 #pragma unroll
-        for (int k = j + 1; k < 6; k++) a[k] -= t1 * E.colbuf[k];
+        for (int k = j + 1; k < 6; k++) a[k] -= t1 * c1[k];
 #pragma unroll
-        for (int k = j2 + 1; k < 12; k++) a[k] -= t2 * E.colbuf2[k];
+        for (int k = j2 + 1; k < 12; k++) a[k] -= t2 * c2[k];
 #pragma unroll
-        for (int k = 12; k < nf; k++) a[k] -= t1 * E.colbuf[k] + t2 * E.colbuf2[k];
+        for (int k = 12; k < nf; k++) a[k] -= t1 * c1[k] + t2 * c2[k];
       }
 #pragma unroll
       for (int j = 12; j < nf; j++) {
-        if (l < 18) { E.colbuf[l] = a[j]; E.bbuf[l] = bv; }
-        const float d = E.colbuf[j], bj = E.bbuf[j];
+        E.colbuf[l] = a[j]; E.bbuf[l] = bv;
+        float c1[20];  // column j, rows 12..19
+        ld_vec(E.colbuf + 12, c1 + 12, 8);
+        const float d = c1[j], bj = E.bbuf[j];
         nonpd |= !(d > 0.f);
         const float inv = __builtin_amdgcn_rsqf(fmaxf(d, 1e-20f));
         const float gj = bj * inv;
-        if (l == 0) { E.invd[j] = inv; E.gv[j] = gj; }
+        my_inv = lane_opaque(l) == j ? inv : my_inv;
+        my_g = lane_opaque(l) == j ? gj : my_g;
         const float t = lane_opaque(l) > j ? a[j] * (inv * inv) : 0.f;
         a[j] = (lane_opaque(l) >= j) ? a[j] * inv : a[j];
         bv -= t * bj;
 #pragma unroll
-        for (int k = j + 1; k < nf; k++) a[k] -= t * E.colbuf[k];
+        for (int k = j + 1; k < nf; k++) a[k] -= t * c1[k];
       }
+      if (l < nf) { E.invd[l] = my_inv; E.gv[l] = my_g; }
       if (l < nf) st_vec<18>(E.L[l], a);
       if (l == 0 && nonpd) E.bad = 1;
     }
