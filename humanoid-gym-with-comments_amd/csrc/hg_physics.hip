@@ -80,7 +80,7 @@ struct __align__(16) EnvSh {
   float rd[RMAX][3];       // joint rows: sign in rd[r][0]
   int rbP[RMAX], rbN[RMAX];// joint rows: rbP = -1 - dof
   int rlam[RMAX];          // warm-start slot
-  float rLam[RMAX];
+  alignas(16) float rLam[RMAX];
   float cf[13][3];
   float base_cm, base_cs[3], base_cJ[6];
   float mass0, fric;
@@ -166,6 +166,11 @@ __device__ __forceinline__ float keep_dpp(float x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// materialise a value here (an LDS read completes before the selects that use it instead of being
+// sunk behind an exec-mask branch)
+__device__ __forceinline__ void pin(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(int& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(f3& v) { pin(v.x); pin(v.y); pin(v.z); }
 template <int N>
 __device__ __forceinline__ void scan_step(f3& v, int k) {
   const f3 u = mk(keep_dpp(shr<N>(v.x)), keep_dpp(shr<N>(v.y)), keep_dpp(shr<N>(v.z)));
@@ -769,49 +774,58 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       for (int i = 0; i < 18; i++) J[i] = 0.f;
       const int npts_e = E.npts;
       const bool crow = own && l < 3 * npts_e;   // contact row (else joint friction / limit row)
-      if (own && !crow) {  // joint row: sign * e_dof
-        const int j = -1 - E.rbP[l];
-#pragma unroll
-        for (int jj = 0; jj < 12; jj++) J[6 + jj] = (jj == j) ? E.rd[l][0] : 0.f;
-      }
+      const bool jrow = own && !crow;
+      // Branch-free over the row kinds: every lane reads its joint-row slot and a (clamped) contact
+      // record and builds both rows; the reads are pinned ahead of the selects so they never sit
+      // behind an exec-mask branch.
+      int jdof = -1 - E.rbP[l];
+      float jsgn = E.rd[l][0];
+      pin(jdof);
+      pin(jsgn);
       const int cidx = crow ? l / 3 : 0, cdir = crow ? l % 3 : 0;
       const ContactC& C = E.ct[cidx];
-      if (crow) {  // J = J_bP(xP) d - J_bN(xN) d
-        const f3 d = ld3(C.dir[cdir]), xp = ld3(C.xP);
-        const int bP = C.bP;
-        const bool pair2 = C.bN >= 0;
-        E.rlam[l] = C.lam_base + cdir;
-        E.rLam[l] = E.lamst[C.lam_base + cdir];
-        J[0] = pair2 ? 0.f : d.x; J[1] = pair2 ? 0.f : d.y; J[2] = pair2 ? 0.f : d.z;
-        const f3 xd = cross(xp, d) - (pair2 ? cross(ld3(C.xN), d) : mk(0, 0, 0));
-        J[3] = xd.x; J[4] = xd.y; J[5] = xd.z;
+      f3 d = ld3(C.dir[cdir]), xp = ld3(C.xP), xn = ld3(C.xN);
+      int bP = C.bP, bN = C.bN;
+      const int lamb = min(max(C.lam_base, 0), HG_LAMW - 3) + cdir;
+      float lamv = E.lamst[lamb];
+      pin(d); pin(xp); pin(xn); pin(bP); pin(bN); pin(lamv);
+      if (crow) { E.rlam[l] = lamb; E.rLam[l] = lamv; }
+      // contact row J = J_bP(xP) d - J_bN(xN) d
+      const bool pair2 = bN >= 0;
+      float Jc[18];
+      Jc[0] = pair2 ? 0.f : d.x; Jc[1] = pair2 ? 0.f : d.y; Jc[2] = pair2 ? 0.f : d.z;
+      const f3 xd = cross(xp, d) - (pair2 ? cross(xn, d) : mk(0, 0, 0));
+      Jc[3] = xd.x; Jc[4] = xd.y; Jc[5] = xd.z;
+      {
         // the contact body's leg: links kb0 .. bP (6 at most)
         const bool right = bP >= 7;
         const int kb0 = right ? 7 : 1;
 #pragma unroll
         for (int m = 0; m < 6; m++) {
           const int k = kb0 + m;
-          const float val = (bP > 0 && k <= bP) ? dot(d, cross(ld3(E.a[k]), xp - ld3(E.o[k]))) : 0.f;
-          J[6 + m] = right ? 0.f : val;
-          J[12 + m] = right ? val : 0.f;
+          f3 ak = ld3(E.a[k]), ok = ld3(E.o[k]);
+          pin(ak); pin(ok);
+          const float val = (bP > 0 && k <= bP) ? dot(d, cross(ak, xp - ok)) : 0.f;
+          Jc[6 + m] = right ? 0.f : val;
+          Jc[12 + m] = right ? val : 0.f;
         }
       }
       // the other capsule's chain (self-collision rows), only when the wave has such a row
-      if (__ballot(crow && C.bN >= 0) != 0) {
-        if (crow && C.bN >= 0) {
-          const int bN = C.bN;
-          const f3 d = ld3(C.dir[cdir]), xn = ld3(C.xN);
-          const bool right = bN >= 7;
-          const int kb0 = right ? 7 : 1;
+      if (__ballot(crow && pair2) != 0) {
+        const bool right = bN >= 7;
+        const int kb0 = right ? 7 : 1;
 #pragma unroll
-          for (int m = 0; m < 6; m++) {
-            const int k = kb0 + m;
-            const float val = k <= bN ? dot(d, cross(ld3(E.a[k]), xn - ld3(E.o[k]))) : 0.f;
-            J[6 + m] -= right ? 0.f : val;
-            J[12 + m] -= right ? val : 0.f;
-          }
+        for (int m = 0; m < 6; m++) {
+          const int k = kb0 + m;
+          f3 ak = ld3(E.a[k]), ok = ld3(E.o[k]);
+          pin(ak); pin(ok);
+          const float val = (pair2 && k <= bN) ? dot(d, cross(ak, xn - ok)) : 0.f;
+          Jc[6 + m] -= right ? 0.f : val;
+          Jc[12 + m] -= right ? val : 0.f;
         }
       }
+#pragma unroll
+      for (int i = 0; i < 18; i++) J[i] = crow ? Jc[i] : ((jrow && i >= 6 && i - 6 == jdof) ? jsgn : 0.f);
 #pragma unroll
       for (int i = 0; i < 18; i++) v0 += J[i] * E.nu[i];
       // forward substitution with L broadcast from LDS (legs-first order; arrow structure)
@@ -940,36 +954,41 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
       }
       // ---- A14: nu_new = nu + L^-T (dt g + Z^T lambda): lanes = dofs (legs-first order k)
-      float y = 0.f;
-      if (l < nf) {
-        float u = dt * E.gv[l];
+      // every lane computes (lanes >= nf on a clamped column, discarded): no exec-mask branch
+      const int lc = l < 18 ? l : 17;
+      float y;
+      {
+        float u = dt * E.gv[lc];
 #pragma unroll
-        for (int m = 0; m < RMAX; m++) u += E.u.Z[m][l] * lam[m];
-        y = u;
+        for (int m = 0; m < RMAX; m++) u += E.u.Z[m][lc] * lam[m];
+        y = l < nf ? u : 0.f;
       }
-      if (l == 0) {
-#pragma unroll
-        for (int m = 0; m < RMAX; m++) E.rLam[m] = lam[m];
-      }
+      if (l == 0) st_vec<RMAX>(E.rLam, lam);
       // back substitution L^T x = y, column-oriented: the base pivots 17..12, then the two legs'
       // pivots 6 + k and k together (a leg's column has no rows in the other leg, so the two
       // chains are independent): 12 broadcast round trips instead of 18, the same operations per
       // element in the same order
+      // (the L entry is read on every lane, pinned before the select, so the compiler does not
+      // put the read behind an exec-mask branch)
 #pragma unroll
       for (int j = nf - 1; j >= 12; j--) {
+        float Ljl = E.L[j][lc];
+        asm volatile("" : "+v"(Ljl));
         const float xj = swz(y, j) * E.invd[j];
-        y = (l == j) ? xj : ((l < j) ? y - E.L[j][l < 18 ? l : 0] * xj : y);
+        y = (l == j) ? xj : ((l < j) ? y - Ljl * xj : y);
       }
 #pragma unroll
       for (int k = 5; k >= 0; k--) {
         const int jr = 6 + k, jl = k;
-        const float xr = swz(y, jr) * E.invd[jr];
-        const float xl = swz(y, jl) * E.invd[jl];
         const bool right = l >= 6 && l < 12;
         const int j = right ? jr : jl;
+        float Ljl = E.L[j][lc];
+        asm volatile("" : "+v"(Ljl));
+        const float xr = swz(y, jr) * E.invd[jr];
+        const float xl = swz(y, jl) * E.invd[jl];
         const float xj = right ? xr : xl;
         const int lo = right ? 6 : 0;
-        y = (l == j) ? xj : ((l >= lo && l < j) ? y - E.L[j][l < 18 ? l : 0] * xj : y);
+        y = (l == j) ? xj : ((l >= lo && l < j) ? y - Ljl * xj : y);
       }
       __syncthreads();
       float nu_new = 0.f;
