@@ -34,15 +34,14 @@ constexpr int LAM_LIM = LAM_PAIR + HG_MAX_PAIRS * 3;
 constexpr int LAM_FRIC = LAM_LIM + HG_ND;
 constexpr float BIG = 3.0e38f;
 
-struct __align__(16) GroupC {  // PGS constants of one 3-slot group (a, b, c): five 16-byte reads
+struct __align__(16) GroupC {  // PGS constants of one 3-slot group (a, b, c): four 16-byte reads
   float invD[3];
   float Wba, Wca, Wcb;     // W[b][a], W[c][a], W[c][b]
   float tgt[3], lo[3], hi[3];
-  float mu;
-  int contact;             // 1: (a, b, c) = a contact's normal and tangent pair; 0: single rows
-  int pad[3];
+  float mu;                // >= 0: (a, b, c) = a contact's normal and tangent pair (friction
+                           // coefficient); -1: single rows (the group kind rides in the same read)
 };
-static_assert(sizeof(GroupC) == 80, "GroupC is five 16-byte LDS reads");
+static_assert(sizeof(GroupC) == 64, "GroupC is four 16-byte LDS reads");
 
 struct ContactC {  // one active contact: points on the two bodies (base-centred), normal + tangents
   float xP[3], xN[3];
@@ -709,7 +708,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
       if (l == 0) { E.nrows = nrows; E.npts = npts; }
       // group-level fields and empty slots
-      if (l < NGRP) { E.grp[l].contact = l < npts ? 1 : 0; E.grp[l].mu = 0.f; }
+      if (l < NGRP) E.grp[l].mu = -1.f;  // single rows unless a contact claims the group below
       for (int r = l; r < 3 * NGRP; r += 32) {
         if (r >= nrows) {
           const int g = r / 3, k = r % 3;
@@ -938,7 +937,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
               const float dbs = nbs - lb;
               const float vc2 = vc1 + G.Wcb * dbs;
               const float ncs = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
-              const bool ct = G.contact != 0;
+              const bool ct = G.mu >= 0.f;
               db = ct ? l1 * sc - lb : dbs;
               dc = ct ? l2 * sc - lc : ncs - lc;
             }
