@@ -739,8 +739,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
       }
       if (l < 12) {
-        if (has_f) {  // joint friction: |lambda| <= f dt
-          const int r = 3 * npts + __popc(mf & ((1u << l) - 1u));
+        const int rf = 3 * npts + __popc(mf & ((1u << l) - 1u));
+        if (has_f && rf < RMAX) {  // joint friction: |lambda| <= f dt (rows past RMAX dropped)
+          const int r = rf;
           E.rd[r][0] = 1.f; E.rbP[r] = -1 - l; E.rbN[r] = -1;
           E.rlam[r] = LAM_FRIC + l;
           E.rLam[r] = E.lamst[LAM_FRIC + l];

@@ -250,7 +250,9 @@ def load_model(path=MODEL_PATH, armature=0.0, joint_friction=True, self_collisio
     armature: joint-space inertia added to every leg joint; the Isaac Gym asset option is 0
     (humanoid_config.py:118), which the simulator runs stably by treating the PD damping term
     implicitly.  0.01 kg m^2 is the robot's MJCF value (XBot-L.xml:37-39).
-    joint_friction: apply the URDF's joint friction (0.1 N m on the ankles, XBot-L.urdf:1675-1677).
+    joint_friction: apply the URDF's joint friction (0.1 N m on the ankles, XBot-L.urdf:1675-1677);
+    or a dict {joint-name substring: friction N m} (last match wins, as the PD gain keys) that
+    replaces it — the MJCF profile of scripts/sim2sim.py (frictionloss, XBot-L.xml:37-39,426).
     self_collisions: leg-vs-leg capsule pairs (asset.self_collisions = 0 enables them, :103).
     """
     with open(path) as f:
@@ -277,7 +279,14 @@ def load_model(path=MODEL_PATH, armature=0.0, joint_friction=True, self_collisio
             m.lower[b] = j["lower"]
             m.upper[b] = j["upper"]
             m.armature[b] = armature
-            m.joint_friction[b] = j.get("friction", 0.0) if joint_friction else 0.0
+            if isinstance(joint_friction, dict):
+                f = 0.0
+                for key, val in joint_friction.items():
+                    if key in j["name"]:
+                        f = float(val)
+                m.joint_friction[b] = f
+            else:
+                m.joint_friction[b] = j.get("friction", 0.0) if joint_friction else 0.0
         else:
             for i in range(9):
                 m.joint_rot[b][i] = 1.0 if i in (0, 4, 8) else 0.0

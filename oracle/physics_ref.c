@@ -525,7 +525,7 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
   }
   for (int j = 0; j < ND; j++) {
     const real f = m->jfric[j + 1];
-    if (!(f > 0)) { lamst[LAM_FRIC + j] = 0; continue; }
+    if (!(f > 0) || nr >= MAX_ROWS) { lamst[LAM_FRIC + j] = 0; continue; }
     Row* r = &rows[nr++];
     memset(r, 0, sizeof(*r));
     r->kind = 4; r->lam_idx = LAM_FRIC + j; r->bpos = r->bneg = -1;

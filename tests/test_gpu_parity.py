@@ -1206,3 +1206,66 @@ def test_play_script(tmp_path, monkeypatch):
     st = np.load(root / "openloop_action" / "states.npz")
     assert st["dof_pos"].shape == (40, 12) and np.isfinite(st["dof_pos"]).all()
     np.testing.assert_array_equal(np.load(root / "openloop_action" / "openloop_action.npz")["action"], actions)
+
+
+def test_sim2sim_obs_matches_env_obs():
+    """humanoid/scripts/sim2sim.py builds the policy input from the raw simulator state as the
+    reference's sim2sim.py does (get_obs + the frame of sim2sim.py:186-202); on the training
+    (URDF) profile with noise off, every column of that frame except the gait phase equals the
+    newest frame of the env's own observation (K_post), step after step."""
+    _need_gpu()
+    import humanoid.scripts.sim2sim as S2S
+    env = S2S.make_env("urdf", 64, duration=5.0)
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    cmd = torch.tensor([[0.4, 0.1, -0.2]], device="cuda:0").repeat(64, 1)
+    act = torch.zeros(64, 12, device="cuda:0")
+    nso = env.cfg.env.num_single_obs
+    worst = 0.0
+    for k in range(30):
+        env.commands[:, :3] = cmd
+        act = torch.randn(64, 12, device="cuda:0", generator=g) * 0.5
+        _, _, _, reset, _ = S2S.step_direct(env, act)
+        env.commands[:, :3] = cmd
+        frame = S2S.obs_frame(env, cmd, act, (k + 1) * env.dt)
+        ours = env.obs_buf[:, -nso:]
+        # envs reset by this step start over with zeroed actions in their frame (reset_idx); the
+        # rest must agree.  Euler yaw: the two wraps agree except at +-pi exactly (never reached)
+        keep = ~reset.bool()
+        assert int(keep.sum()) >= 48
+        d = (frame[keep, 2:] - ours[keep, 2:]).abs()
+        worst = max(worst, float(d.max()))
+        assert float(d.max()) < 2e-5, (k, int(d.max(0).values.argmax()) + 2, float(d.max()))
+    assert worst < 2e-5
+
+
+def test_sim2sim_mjcf_profile(tmp_path):
+    """sim2sim.py end to end on the MJCF parameter profile: an exported TorchScript actor driven by
+    the sim2sim loop for 1 s at three commands; the profile reached the simulator (friction 0.9,
+    200 N m torque clip, 50 solver sweeps, lighter trunk, leg-joint frictionloss) and the summary /
+    traces are written and finite."""
+    _need_gpu()
+    import json
+    import humanoid.scripts.sim2sim as S2S
+    from humanoid.algo.ppo import ActorCritic
+    from humanoid.utils.helpers import export_policy_as_jit
+    torch.manual_seed(0)
+    ac = ActorCritic(705, 219, 12, [512, 256, 128], [768, 256, 128]).to("cuda:0")
+    export_policy_as_jit(ac, str(tmp_path))
+    env = S2S.make_env("mjcf", 8, duration=1.0)
+    assert torch.allclose(env.env_frictions, torch.full_like(env.env_frictions, 0.9))
+    assert float(env.body_mass[0]) == pytest.approx(env._model.mass[0] - 0.951, abs=1e-4)
+    assert [env._hgcfg.torque_limit[j] for j in range(12)] == [200.0] * 12
+    assert env._hgcfg.pgs_iterations == 50
+    fr = [env._model.joint_friction[b] for b in range(1, 13)]
+    assert fr == pytest.approx([0.01, 0.01, 0.01, 0.01, 0.05, 0.05] * 2)
+    del env
+    out = tmp_path / "s2s"
+    summary = S2S.main(["--load_model", str(tmp_path / "policy_1.pt"), "--duration", "1", "--vx", "-0.25", "0.0",
+                        "0.4", "--envs_per_command", "2", "--out", str(out)])
+    js = json.load(open(out / "sim2sim.json"))
+    assert js["profile"] == "mjcf" and js["pgs_iterations"] == 50 and len(js["commands"]) == 3
+    assert js == json.loads(json.dumps(summary))
+    for c in js["commands"]:
+        assert np.isfinite(c["lin_vel_error"]) and np.isfinite(c["yaw_rate_error"])
+    tr = np.load(out / "sim2sim_traces.npz")
+    assert tr["q"].shape == (100, 12) and np.isfinite(tr["q"]).all() and np.isfinite(tr["target_q"]).all()
