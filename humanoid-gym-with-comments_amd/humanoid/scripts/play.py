@@ -6,6 +6,12 @@ Loads the checkpoint, exports the actor (TorchScript policy_1.pt + base_lin_vel.
 policy.onnx), runs the policy on a single environment with the reference's play settings and
 writes the open-loop action trace (openloop_action.npz) plus per-step state logs (states.npz) and
 the mean episode rewards.  There is no viewer or video: hg_sim has no renderer.
+
+Reference defect fixed: play.py:77 sets ``train_cfg.runner.resume = True``, but
+``make_alg_runner`` resets it to False before reading it (task_registry.py:137), so without an
+explicit ``--resume`` the reference exports and plays the randomly initialised policy.  Here the
+resume request travels in ``args``, which make_alg_runner honours: play always loads the
+checkpoint (``--load_run`` / ``--checkpoint``, default the newest).
 """
 import argparse
 import os
@@ -38,6 +44,7 @@ def play(args, steps=100):
     env, _ = task_registry.make_env(name=args.task, args=args, env_cfg=env_cfg)
     obs = env.get_observations()
     train_cfg.runner.resume = True
+    args.resume = True  # see the module docstring (task_registry.py:137 would drop the line above)
     runner, train_cfg = task_registry.make_alg_runner(env=env, name=args.task, args=args, train_cfg=train_cfg)
     policy = runner.get_inference_policy(device=env.device)
     root = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", train_cfg.runner.experiment_name)

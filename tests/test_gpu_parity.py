@@ -1195,6 +1195,7 @@ def test_play_script(tmp_path, monkeypatch):
     runner.learn(1, init_at_random_ep_len=True)
     exp = tcfg.runner.experiment_name
     assert os.path.isdir(tmp_path / "logs" / exp)
+    trained = {k: v.detach().cpu().clone() for k, v in runner.alg.actor_critic.actor.state_dict().items()}
     del runner, env
     torch.cuda.synchronize()
     actions = play_mod.play(get_args(["--task", "humanoid_ppo", "--headless"]), steps=40)
@@ -1206,6 +1207,10 @@ def test_play_script(tmp_path, monkeypatch):
     st = np.load(root / "openloop_action" / "states.npz")
     assert st["dof_pos"].shape == (40, 12) and np.isfinite(st["dof_pos"]).all()
     np.testing.assert_array_equal(np.load(root / "openloop_action" / "openloop_action.npz")["action"], actions)
+    # the exported actor is the trained one (play resumes the checkpoint without --resume, see play.py)
+    jit = torch.jit.load(str(root / "exported" / "policies" / "policy_1.pt"))
+    for k, v in trained.items():
+        assert torch.equal(jit.state_dict()[k], v), k
 
 
 def test_sim2sim_obs_matches_env_obs():
