@@ -239,6 +239,10 @@ def main():
     ap.add_argument("--no-gemm-table", action="store_true", help="hipBLASLt default GEMM heuristics")
     ap.add_argument("--terrain", default="plane", choices=["plane", "heightfield"],
                     help="plane = config 2; heightfield = config 3 (2100x2100 generated terrain)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 5],
                     help="BASELINE.json configs: 2 plane (default), 3 heightfield, 5 push-recovery curriculum "
                          "with 8192 envs/GPU, fp16 observation storage and a bf16 policy")
@@ -252,9 +256,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     device = f"cuda:{local}"
     # one seed for every rank: the env draws and the action noise are keyed by the global env id
     # (rank r holds envs [r * envs, (r + 1) * envs)), so N ranks run the single N * envs job, split
