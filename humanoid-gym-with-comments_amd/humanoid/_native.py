@@ -103,7 +103,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_mlp_act_backward", "hg_mlp_act_backward_scratch", "hg_colsum_jobs", "hg_linear_skinny_supported",
            "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch",
            "hg_mlp_act_backward_bf16", "hg_linear_skinny_forward_bf16", "hg_linear_skinny_backward_bf16",
-           "hg_cast_bf16_jobs", "hg_version"]
+           "hg_cast_bf16_jobs", "hg_linear_act_forward", "hg_linear_act_tile", "hg_version"]
 
 _LIB = None
 
@@ -194,6 +194,11 @@ def load_library(path=LIB_PATH):
                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int, vp]
     L.hg_mlp_act_backward_scratch.restype = ctypes.c_int64
     L.hg_mlp_act_backward_scratch.argtypes = [ctypes.c_int64, ctypes.c_int]
+    L.hg_linear_act_forward.restype = ctypes.c_int
+    L.hg_linear_act_forward.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
+    L.hg_linear_act_tile.restype = ctypes.c_int
+    L.hg_linear_act_tile.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]
     L.hg_linear_skinny_supported.restype = ctypes.c_int
     L.hg_linear_skinny_supported.argtypes = [ctypes.c_int, ctypes.c_int]
     L.hg_linear_skinny_forward.restype = ctypes.c_int

@@ -142,6 +142,37 @@ def _weight_grad(gh, x, red=None):
     return dw
 
 
+# Hidden layers y = elu(x W^T + b) on the fused f32-MFMA kernel (hg_linear_act_forward,
+# csrc/hg_linear.hip: bias + ELU applied to the accumulators, one store) where it beats torch's
+# addmm + ELU, i.e. the small, latency-bound products; hipBLASLt's tuned kernels stay on the large
+# ones.  (k, n) -> largest row count routed to the fused kernel.  Measured on MI355X
+# (scripts/linear_probe.py, profiles/r2_v3/linear_probe.jsonl; torch addmm + ELU -> fused, us):
+# 4096 rows: 512x256 24.5 -> 21.0, 256x128 24.4 -> 13.4, 128x128 24.2 -> 9.9; 24576 rows:
+# 128x128 24.7 -> 20.2; 705x512, 705x128, 219x768, 768x256 and every larger row count stay on torch.
+_FUSED_FWD_ROWS = {(512, 256): 8192, (256, 128): 8192, (128, 128): 32768}
+FUSED_FORWARD = os.environ.get("HG_FUSED_FORWARD", "1") != "0"
+
+
+def _fused_ok(h, W, b):
+    rows = h.shape[0]
+    k = W.shape[1]
+    return (FUSED_FORWARD and rows <= _FUSED_FWD_ROWS.get((k, W.shape[0]), 0) and h.dim() == 2 and h.stride(1) == 1
+            and h.dtype == torch.float32 and W.is_contiguous() and b is not None and b.is_contiguous())
+
+
+def linear_act(h, W, b, elu=True, out=None, tile=0):
+    """y = elu(h W^T + b) (``elu`` False: h W^T + b) in one HIP launch on the f32 matrix cores."""
+    rows, n = h.shape[0], W.shape[0]
+    y = torch.empty(rows, n, dtype=torch.float32, device=h.device) if out is None else out
+    if y.shape != (rows, n) or y.stride(1) != 1 or y.dtype != torch.float32:
+        raise RuntimeError("linear_act: out must be a float32 [rows, n] tensor with unit column stride")
+    rc = N.lib().hg_linear_act_forward(h.data_ptr(), h.stride(0), W.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                       y.stride(0), rows, n, W.shape[1], 1 if elu else 0, tile, _stream(h.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_linear_act_forward failed ({rc})")
+    return y
+
+
 # the per-layer column sums of the backward run as one batched launch at its end (hg_colsum_jobs)
 DEFER_REDUCTIONS = os.environ.get("HG_DEFER_REDUCTIONS", "1") != "0"
 
@@ -156,10 +187,12 @@ class _MLP(torch.autograd.Function):
             W, b = params[2 * i], params[2 * i + 1]
             if i == n - 1 and _skinny_ok(h, W):
                 h = _skinny_forward(h, W, b)
+            elif i < n - 1 and _fused_ok(h, W, b):
+                h = linear_act(h, W, b)
             else:
                 h = torch.addmm(b, h, W.t())
-            if i < n - 1:
-                h = F.elu(h)
+                if i < n - 1:
+                    h = F.elu(h)
             acts.append(h)
         # inputs of every layer (x, y_0 .. y_{n-2}) and the weights
         ctx.save_for_backward(*acts[:-1], *params[0::2])
@@ -212,12 +245,17 @@ def mlp_forward(net, x):
 
 
 def mlp_infer(net, x, out=None):
-    """net(x) without autograd (rollout inference): torch's Linear/ELU for the hidden layers, the
-    skinny HIP kernel for the output layer (written into ``out`` when given)."""
+    """net(x) without autograd (rollout inference): hidden layers on the fused Linear + ELU kernel
+    where ``_FUSED_FWD_ROWS`` routes them, torch's Linear/ELU otherwise; the skinny HIP kernel for
+    the output layer (written into ``out`` when given)."""
     mods = list(net)
     h = x
-    for m in mods[:-1]:
-        h = m(h)
+    for j in range(0, len(mods) - 1, 2):
+        lin = mods[j]
+        if _fused_ok(h, lin.weight, lin.bias) and isinstance(mods[j + 1], nn.ELU) and mods[j + 1].alpha == 1.0:
+            h = linear_act(h, lin.weight, lin.bias)
+        else:
+            h = mods[j + 1](lin(h))
     last = mods[-1]
     if _skinny_ok(h, last.weight):
         return _skinny_forward(h, last.weight, last.bias, out)
