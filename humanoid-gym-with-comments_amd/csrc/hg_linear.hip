@@ -89,7 +89,7 @@ __device__ __forceinline__ void mma_chunk(const float a[TM][16], const float w[T
 
 // VEC: x and W rows 16-byte aligned (k % 4 == 0); otherwise 16-byte loads at 4-byte alignment and a
 // scalar tail.
-template <int TM, int TN, bool VEC, bool ELU>
+template <int TM, int TN, int S, bool VEC, bool ELU>
 __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act(const float* __restrict__ x, int64_t ldx,
                                                                const float* __restrict__ W,
                                                                const float* __restrict__ b, float* __restrict__ y,
@@ -127,25 +127,25 @@ __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act(const float* __re
     for (int n = 0; n < TN; n++) acc[m][n] = (f32x16)0.f;
 
   const int kfull = K & ~31;  // chunks with all 32 k in range
-  float a0[TM][16], w0[TN][16], a1[TM][16], w1[TN][16];
-  int kc = 0;
-  if (kfull > 0) {
-    load_chunk<TM, TN, VEC, false>(xr, wr, 0, K, a0, w0);
-    // ping-pong over the full chunks: the next chunk's loads are in flight during this one's MFMAs
-    for (; kc + 64 <= kfull; kc += 64) {
-      load_chunk<TM, TN, VEC, false>(xr, wr, kc + 32, K, a1, w1);
-      mma_chunk<TM, TN>(a0, w0, acc);
-      if (kc + 64 < kfull) load_chunk<TM, TN, VEC, false>(xr, wr, kc + 64, K, a0, w0);
-      mma_chunk<TM, TN>(a1, w1, acc);
-    }
-    if (kc + 32 <= kfull) {  // odd number of full chunks: the last one is in a0
-      mma_chunk<TM, TN>(a0, w0, acc);
-      kc += 32;
+  // S-stage register pipeline over the full chunks: chunk c's loads are issued S - 1 chunks ahead
+  // of its MFMAs (buffer indices are compile-time: the stage loop is fully unrolled).  S = 2: three
+  // and four stages measured no faster (scripts/linear_probe.py), the register cost drops occupancy
+  float a[S][TM][16], w[S][TN][16];
+#pragma unroll
+  for (int j = 0; j < S - 1; j++)
+    if (32 * j < kfull) load_chunk<TM, TN, VEC, false>(xr, wr, 32 * j, K, a[j], w[j]);
+  for (int kb = 0; kb < kfull; kb += 32 * S) {
+#pragma unroll
+    for (int j = 0; j < S; j++) {
+      const int kn = kb + 32 * (j + S - 1);
+      if (kn < kfull) load_chunk<TM, TN, VEC, false>(xr, wr, kn, K, a[(j + S - 1) % S], w[(j + S - 1) % S]);
+      if (kb + 32 * j < kfull) mma_chunk<TM, TN>(a[j], w[j], acc);
     }
   }
+  const int kc = kfull;
   if (kc < K) {  // partial chunk: k = kc + 16h + j valid while < K
-    load_chunk<TM, TN, VEC, true>(xr, wr, kc, K - 16 * h, a0, w0);
-    mma_chunk<TM, TN>(a0, w0, acc);
+    load_chunk<TM, TN, VEC, true>(xr, wr, kc, K - 16 * h, a[0], w[0]);
+    mma_chunk<TM, TN>(a[0], w[0], acc);
   }
 
   // epilogue: + bias, ELU, one store.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2)
@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act(const float* __re
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, int S>
 int launch_linear(const float* x, int64_t ldx, const float* W, const float* b, float* y, int64_t ldy, int64_t rows,
                   int n, int k, bool vec, bool elu, hipStream_t s) {
   const int tiles_n = (n + 32 * TN - 1) / (32 * TN);
@@ -179,7 +179,7 @@ int launch_linear(const float* x, int64_t ldx, const float* W, const float* b, f
   if (blocks > 0x7fffffff) return HG_ERR_ARG;
   const dim3 grid((unsigned)blocks), block(64 * LIN_WAVES);
 #define HG_LIN(V, E) \
-  hipLaunchKernelGGL((k_linear_act<TM, TN, V, E>), grid, block, 0, s, x, ldx, W, b, y, ldy, rows, n, k, tiles_n, tiles)
+  hipLaunchKernelGGL((k_linear_act<TM, TN, S, V, E>), grid, block, 0, s, x, ldx, W, b, y, ldy, rows, n, k, tiles_n, tiles)
   if (vec && elu) HG_LIN(true, true);
   else if (vec) HG_LIN(true, false);
   else if (elu) HG_LIN(false, true);
@@ -210,9 +210,9 @@ extern "C" int hg_linear_act_forward(const float* x, int64_t ldx, const float* W
   if (tile == 0) tile = hg_linear_act_tile(rows, n, k);
   hipStream_t s = (hipStream_t)stream;
   switch (tile) {
-    case 1: return launch_linear<2, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
-    case 2: return launch_linear<2, 1>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
-    case 3: return launch_linear<1, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
-    default: return launch_linear<1, 1>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
+    case 1: return launch_linear<2, 2, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
+    case 2: return launch_linear<2, 1, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
+    case 3: return launch_linear<1, 2, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
+    default: return launch_linear<1, 1, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
   }
 }

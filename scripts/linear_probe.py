@@ -27,6 +27,7 @@ SHAPES = [("actor0_mb", 24576, 705, 512), ("actor1_mb", 24576, 512, 256), ("acto
           ("linvel0_roll", 4096, 705, 128), ("linvel1_roll", 4096, 128, 128),
           ("critic0_vals", 98304, 219, 768), ("critic1_vals", 98304, 768, 256), ("critic2_vals", 98304, 256, 128)]
 ITERS = int(os.environ.get("ITERS", 50))
+TILES = [int(t) for t in os.environ.get("TILES", "1,2,3,4").split(",")]
 
 
 def ours(x, W, b, y, tile):
@@ -65,7 +66,7 @@ for tag, rows, k, n in SHAPES:
            "auto_tile": int(L.hg_linear_act_tile(rows, n, k))}
     flop = 2.0 * rows * k * n
     best = None
-    for tile in (1, 2, 3, 4):
+    for tile in TILES:
         y = torch.empty(rows, n, device=dev)
         ours(x, W, b, y, tile)
         torch.cuda.synchronize()
