@@ -272,14 +272,20 @@ __global__ void __launch_bounds__(256) k_skinny_fwd(const TX* __restrict__ x, in
   (void)groups;
 }
 
+// dX and dW/db of a 64-row tile run on 4 waves (16 rows each): the per-lane serial chains are 4x
+// shorter than one wave walking all 64 rows (skinny dW 17 -> ? us at 24576 rows).
+constexpr int SK_WAVES = 4;
+constexpr int SK_WROWS = SK_ROWS / SK_WAVES;
+
 template <int N, typename TD>
-__global__ void __launch_bounds__(64) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
-                                                 TD* __restrict__ dx, int64_t rows) {
+__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
+                                                             TD* __restrict__ dx, int64_t rows) {
   __shared__ float g_s[SK_ROWS * N];
   const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
   const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
-  for (int i = threadIdx.x; i < nr * N; i += 64) g_s[i] = gh[r0 * N + i];
-  const int c = 2 * threadIdx.x;
+  for (int i = threadIdx.x; i < nr * N; i += 64 * SK_WAVES) g_s[i] = gh[r0 * N + i];
+  const int c = 2 * (threadIdx.x & 63);
+  const int wv = threadIdx.x >> 6;
   float w0[N], w1[N];
 #pragma unroll
   for (int n = 0; n < N; n++) {
@@ -288,7 +294,8 @@ __global__ void __launch_bounds__(64) k_skinny_dx(const float* __restrict__ gh, 
     w1[n] = t.y;
   }
   __syncthreads();
-  for (int r = 0; r < nr; r++) {
+  const int re = min(nr, SK_WROWS * (wv + 1));
+  for (int r = SK_WROWS * wv; r < re; r++) {
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
     for (int n = 0; n < N; n++) {
@@ -301,20 +308,24 @@ __global__ void __launch_bounds__(64) k_skinny_dx(const float* __restrict__ gh, 
 }
 
 template <int N, typename TH>
-__global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, const TH* __restrict__ h,
-                                                 int64_t ldh, float* __restrict__ partial, int64_t rows) {
+__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dw(const float* __restrict__ gh, const TH* __restrict__ h,
+                                                             int64_t ldh, float* __restrict__ partial, int64_t rows) {
   __shared__ float g_s[SK_ROWS * N];
+  __shared__ float2 red[SK_WAVES - 1][N][64];
   const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
   const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
-  for (int i = threadIdx.x; i < nr * N; i += 64) g_s[i] = gh[r0 * N + i];
+  for (int i = threadIdx.x; i < nr * N; i += 64 * SK_WAVES) g_s[i] = gh[r0 * N + i];
   __syncthreads();
-  const int c = 2 * threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int c = 2 * lane;
   float a0[N], a1[N];
 #pragma unroll
   for (int n = 0; n < N; n++) a0[n] = a1[n] = 0.f;
+  const int rb = SK_WROWS * wv, re = min(nr, rb + SK_WROWS);
   const TH* hr = h + r0 * ldh + c;
-  int r = 0;
-  for (; r + 8 <= nr; r += 8) {
+  int r = rb;
+  for (; r + 8 <= re; r += 8) {
     float2 v[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) v[u] = ld2(hr + (int64_t)(r + u) * ldh);
@@ -328,7 +339,7 @@ __global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, 
       }
     }
   }
-  for (; r < nr; r++) {
+  for (; r < re; r++) {
     const float2 v = ld2(hr + (int64_t)r * ldh);
 #pragma unroll
     for (int n = 0; n < N; n++) {
@@ -337,13 +348,29 @@ __global__ void __launch_bounds__(64) k_skinny_dw(const float* __restrict__ gh, 
       a1[n] = fmaf(g, v.y, a1[n]);
     }
   }
+  // fixed-order sum of the 4 waves' 16-row partials (wave 0 + 1 + 2 + 3)
+  if (wv > 0) {
+#pragma unroll
+    for (int n = 0; n < N; n++) red[wv - 1][n][lane] = make_float2(a0[n], a1[n]);
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int q = 0; q < SK_WAVES - 1; q++) {
+#pragma unroll
+    for (int n = 0; n < N; n++) {
+      const float2 t = red[q][n][lane];
+      a0[n] += t.x;
+      a1[n] += t.y;
+    }
+  }
   float* out = partial + (int64_t)blockIdx.x * (N * SK_K + N);
 #pragma unroll
   for (int n = 0; n < N; n++) *reinterpret_cast<float2*>(out + n * SK_K + c) = make_float2(a0[n], a1[n]);
-  if (threadIdx.x < N) {
+  if (lane < N) {
     float gb = 0.f;
-    for (int rr = 0; rr < nr; rr++) gb += g_s[rr * N + threadIdx.x];
-    out[N * SK_K + threadIdx.x] = gb;
+    for (int rr = 0; rr < nr; rr++) gb += g_s[rr * N + lane];
+    out[N * SK_K + lane] = gb;
   }
 }
 }  // namespace
@@ -394,7 +421,7 @@ int skinny_backward(const float* gh, const TH* h, int64_t ldh, const float* W, T
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (int)((rows + SK_ROWS - 1) / SK_ROWS);
   const dim3 grid((unsigned)tiles);
-#define HG_SK_DW(NN) hipLaunchKernelGGL((k_skinny_dw<NN, TH>), grid, dim3(64), 0, s, gh, h, ldh, scratch, rows)
+#define HG_SK_DW(NN) hipLaunchKernelGGL((k_skinny_dw<NN, TH>), grid, dim3(64 * SK_WAVES), 0, s, gh, h, ldh, scratch, rows)
   HG_SKINNY_SWITCH(n, HG_SK_DW)
 #undef HG_SK_DW
   const int width = n * k + n;
@@ -402,7 +429,7 @@ int skinny_backward(const float* gh, const TH* h, int64_t ldh, const float* W, T
   if (grad_wb)
     hipLaunchKernelGGL(k_colsum_final, dim3((width + FC - 1) / FC), dim3(TPB), 0, s, scratch, tiles, width, grad_wb);
   if (dx) {
-#define HG_SK_DX(NN) hipLaunchKernelGGL((k_skinny_dx<NN, TH>), grid, dim3(64), 0, s, gh, W, dx, rows)
+#define HG_SK_DX(NN) hipLaunchKernelGGL((k_skinny_dx<NN, TH>), grid, dim3(64 * SK_WAVES), 0, s, gh, W, dx, rows)
     HG_SKINNY_SWITCH(n, HG_SK_DX)
 #undef HG_SK_DX
   }
