@@ -447,11 +447,15 @@ class XBotLFreeEnv(BaseTask):
     def _publish_extras(self):
         # the latest post/reset launch left its EP_STATS snapshot in ring row hg_ep_stats_slot: a
         # view, intact for the next EP_RING - 1 launches (no copy kernel per step)
-        stats = self._ep_ring[self.hg.hg_ep_stats_slot(self.sim)]
-        self.extras = {
-            "episode": {"rew_" + n: stats[REWARD_NAMES.index(n)] for n in self.reward_names},
-            "time_outs": self.time_out_buf,
-        }
+        # the per-term views of each ring row are built once and reused (22 fresh tensor views per
+        # step cost ≈85 us of host time, a quarter of a policy step's GPU time)
+        slot = self.hg.hg_ep_stats_slot(self.sim)
+        cache = self.__dict__.setdefault("_ep_views", {})
+        views = cache.get(slot)
+        if views is None:
+            stats = self._ep_ring[slot]
+            views = cache[slot] = {"rew_" + n: stats[REWARD_NAMES.index(n)] for n in self.reward_names}
+        self.extras = {"episode": dict(views), "time_outs": self.time_out_buf}
 
     def update_push_curriculum(self, iteration):
         """Push-recovery curriculum (config 5, BUILD-DEFINED): max push velocities ramp linearly
