@@ -266,6 +266,9 @@ class XBotLFreeEnv(BaseTask):
         self.commands = self._view(T["COMMANDS"])
         self._obs2 = self._view(T["OBS_BUF"])
         self._priv2 = self._view(T["PRIV_BUF"])
+        # the two halves of each double buffer as fixed views (no tensor indexing per access)
+        self._obs2v = tuple(self._obs2.unbind(0))
+        self._priv2v = tuple(self._priv2.unbind(0))
         self._parity = 0
         self.rew_buf = self._view(T["REW_BUF"])
         self._reset_u8 = self._view(T["RESET_BUF"])
@@ -425,11 +428,11 @@ class XBotLFreeEnv(BaseTask):
 
     @property
     def obs_buf(self):
-        return self._obs2[self._parity]
+        return self._obs2v[self._parity]
 
     @property
     def privileged_obs_buf(self):
-        return self._priv2[self._parity]
+        return self._priv2v[self._parity]
 
     @property
     def dof_state(self):
