@@ -81,7 +81,37 @@ __global__ void __launch_bounds__(TPB) k_act_bwd_vec(const T* __restrict__ gy, c
   const int64_t r0 = (int64_t)blockIdx.x * RT;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool colok = col < width;
-  if (colok) {
+  const int nr = RT / L;  // rows per lane of a full tile (L = 4..8)
+  if (colok && r0 + RT <= rows && RT % L == 0 && nr <= 8) {
+    // full tile: every load of the lane's rows issued before the first store (one memory latency
+    // per tile instead of one per row), rows summed in the same order as the loop below
+    float4 a[8], o[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (u < nr) {
+        const int64_t i = (r0 + rho + (int64_t)u * L) * width + col;
+        a[u] = ld4(gy + i);
+        if (y) o[u] = ld4(y + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (u < nr) {
+        float4 v = a[u];
+        if (y) {
+          v.x = o[u].x > 0.f ? v.x : v.x * (o[u].x + 1.0f);
+          v.y = o[u].y > 0.f ? v.y : v.y * (o[u].y + 1.0f);
+          v.z = o[u].z > 0.f ? v.z : v.z * (o[u].z + 1.0f);
+          v.w = o[u].w > 0.f ? v.w : v.w * (o[u].w + 1.0f);
+          st4(gh + (r0 + rho + (int64_t)u * L) * width + col, v);
+        }
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+    }
+  } else if (colok) {
     for (int64_t r = r0 + rho; r < r0 + RT && r < rows; r += L) {
       const int64_t i = r * width + col;
       float4 v = ld4(gy + i);
