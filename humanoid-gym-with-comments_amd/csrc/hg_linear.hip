@@ -170,6 +170,113 @@ __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act(const float* __re
   }
 }
 
+// Small-output variant: one wave per 16 x 16 tile on v_mfma_f32_16x16x4_f32 (A[i = l & 15][k = l >> 4],
+// B[k = l >> 4][j = l & 15], C row 4 (l >> 4) + q, column l & 15).  Lane group g = l >> 4 owns the 8
+// consecutive k [8g, 8g + 8) of each 32-wide chunk; MFMA step s takes k = 8g + s.  Four times the
+// waves of the 32 x 32 tile for the same output, for the latency-bound 4096-row rollout layers.
+// Two accumulators (even / odd steps) cover the 40-cycle dependent-accumulator latency.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool VEC, bool TAIL>
+__device__ __forceinline__ void ld8k(const float* __restrict__ p, int k0, int K, float v[8]) {
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (!TAIL) {
+      if (VEC) {
+        const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      } else {
+        const f32x4u t = *reinterpret_cast<const f32x4u*>(p + 4 * q);
+        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[4 * q + j] = (k0 + 4 * q + j < K) ? p[4 * q + j] : 0.f;
+    }
+  }
+}
+
+template <bool VEC, bool ELU>
+__global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act16(const float* __restrict__ x, int64_t ldx,
+                                                                 const float* __restrict__ W,
+                                                                 const float* __restrict__ b, float* __restrict__ y,
+                                                                 int64_t ldy, int64_t rows, int N, int K,
+                                                                 int tiles_n, int64_t tiles) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const unsigned nb = gridDim.x;
+  unsigned L = blockIdx.x;
+  if ((nb & 7u) == 0) L = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+  const int64_t t = (int64_t)L * LIN_WAVES + (threadIdx.x >> 6);
+  if (t >= tiles) return;
+  const int64_t r0 = (t / tiles_n) * 16;
+  const int c0 = (int)(t % tiles_n) * 16;
+  const float* xr = x + min<int64_t>(r0 + i, rows - 1) * ldx + 8 * g;
+  const float* wr = W + (int64_t)min(c0 + i, N - 1) * K + 8 * g;
+  f32x4 acc0 = (f32x4)0.f, acc1 = (f32x4)0.f;
+  const int kfull = K & ~31;
+  float a[2][8], w[2][8];
+  if (kfull > 0) {
+    ld8k<VEC, false>(xr, 0, K, a[0]);
+    ld8k<VEC, false>(wr, 0, K, w[0]);
+  }
+  for (int kb = 0; kb < kfull; kb += 64) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int kn = kb + 32 * (j + 1);
+      if (kn < kfull) {
+        ld8k<VEC, false>(xr + kn, kn, K, a[j ^ 1]);
+        ld8k<VEC, false>(wr + kn, kn, K, w[j ^ 1]);
+      }
+      if (kb + 32 * j < kfull) {
+#pragma unroll
+        for (int s2 = 0; s2 < 8; s2 += 2) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s2], w[j][s2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s2 + 1], w[j][s2 + 1], acc1, 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (kfull < K) {
+    ld8k<VEC, true>(xr + kfull, kfull, K - 8 * g, a[0]);
+    ld8k<VEC, true>(wr + kfull, kfull, K - 8 * g, w[0]);
+#pragma unroll
+    for (int s2 = 0; s2 < 8; s2 += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2], w[0][s2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2 + 1], w[0][s2 + 1], acc1, 0, 0, 0);
+    }
+  }
+  const int c = c0 + i;
+  if (c >= N) return;
+  const float bc = b ? b[c] : 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int64_t r = r0 + 4 * g + q;
+    if (r < rows) {
+      float v = acc0[q] + acc1[q] + bc;
+      if (ELU) v = v > 0.f ? v : expm1f(v);
+      y[r * ldy + c] = v;
+    }
+  }
+}
+
+int launch_linear16(const float* x, int64_t ldx, const float* W, const float* b, float* y, int64_t ldy, int64_t rows,
+                    int n, int k, bool vec, bool elu, hipStream_t s) {
+  const int tiles_n = (n + 15) / 16;
+  const int64_t tiles = ((rows + 15) / 16) * tiles_n;
+  const int64_t blocks = (tiles + LIN_WAVES - 1) / LIN_WAVES;
+  if (blocks > 0x7fffffff) return HG_ERR_ARG;
+  const dim3 grid((unsigned)blocks), block(64 * LIN_WAVES);
+#define HG_LIN16(V, E) \
+  hipLaunchKernelGGL((k_linear_act16<V, E>), grid, block, 0, s, x, ldx, W, b, y, ldy, rows, n, k, tiles_n, tiles)
+  if (vec && elu) HG_LIN16(true, true);
+  else if (vec) HG_LIN16(true, false);
+  else if (elu) HG_LIN16(false, true);
+  else HG_LIN16(false, false);
+#undef HG_LIN16
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
 template <int TM, int TN, int S>
 int launch_linear(const float* x, int64_t ldx, const float* W, const float* b, float* y, int64_t ldy, int64_t rows,
                   int n, int k, bool vec, bool elu, hipStream_t s) {
@@ -190,19 +297,22 @@ int launch_linear(const float* x, int64_t ldx, const float* W, const float* b, f
 
 }  // namespace
 
-// Wave-tile choice (32 TM x 32 TN; scripts/linear_probe.py on MI355X over the policy MLPs' shapes):
-// 64 x 32 while that still gives >= 2048 waves (2 per SIMD), else 32 x 32 (the small rollout
-// shapes are latency-bound: more, shorter waves win).  tile 1..4 forces 64x64, 64x32, 32x64, 32x32.
+// Wave-tile choice (scripts/linear_probe.py on MI355X over the policy MLPs' shapes,
+// profiles/r2_v3/linear_probe*.jsonl): 64 x 32 while that still gives >= 2048 waves (2 per SIMD);
+// below one 32 x 32 wave per SIMD the 16 x 16 tile (4x the waves: 4096-row 256 -> 128 layer
+// 13.8 -> 10.6 us, 128 -> 128 10.5 -> 7.6 us); 32 x 32 otherwise.  tile 1..5 forces 64x64, 64x32,
+// 32x64, 32x32, 16x16.
 extern "C" int hg_linear_act_tile(int64_t rows, int n, int k) {
   (void)k;
   const int64_t waves21 = ((rows + 63) / 64) * ((n + 31) / 32);
-  return waves21 >= 2048 ? 2 : 4;
+  const int64_t waves11 = ((rows + 31) / 32) * ((n + 31) / 32);
+  return waves21 >= 2048 ? 2 : (waves11 < 1024 ? 5 : 4);
 }
 
 extern "C" int hg_linear_act_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y,
                                      int64_t ldy, int64_t rows, int n, int k, int act, int tile, void* stream) {
   if (!x || !W || !y || rows <= 0 || n <= 0 || k <= 0 || ldx < k || ldy < n || (act != 0 && act != 1) || tile < 0 ||
-      tile > 4)
+      tile > 5)
     return HG_ERR_ARG;
   if ((uintptr_t)x % 4 != 0 || (uintptr_t)W % 4 != 0) return HG_ERR_ARG;
   const bool vec = ldx % 4 == 0 && k % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)W % 16 == 0;
@@ -213,6 +323,7 @@ extern "C" int hg_linear_act_forward(const float* x, int64_t ldx, const float* W
     case 1: return launch_linear<2, 2, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
     case 2: return launch_linear<2, 1, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
     case 3: return launch_linear<1, 2, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
-    default: return launch_linear<1, 1, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
+    case 4: return launch_linear<1, 1, 2>(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
+    default: return launch_linear16(x, ldx, W, b, y, ldy, rows, n, k, vec, elu, s);
   }
 }

@@ -146,9 +146,10 @@ def _weight_grad(gh, x, red=None):
 # csrc/hg_linear.hip: bias + ELU applied to the accumulators, one store) where it beats torch's
 # addmm + ELU, i.e. the small, latency-bound products; hipBLASLt's tuned kernels stay on the large
 # ones.  (k, n) -> largest row count routed to the fused kernel.  Measured on MI355X
-# (scripts/linear_probe.py, profiles/r2_v3/linear_probe.jsonl; torch addmm + ELU -> fused, us):
-# 4096 rows: 512x256 24.5 -> 21.0, 256x128 24.4 -> 13.4, 128x128 24.2 -> 9.9; 24576 rows:
-# 128x128 24.7 -> 20.2; 705x512, 705x128, 219x768, 768x256 and every larger row count stay on torch.
+# (scripts/linear_probe.py, profiles/r2_v3/linear_probe*.jsonl; torch addmm + ELU -> fused, us):
+# 4096 rows: 512x256 24.5 -> 21.0, 256x128 24.4 -> 10.6, 128x128 24.2 -> 7.6 (16x16 wave tiles);
+# 24576 rows: 128x128 24.7 -> 20.2; 705x512, 705x128, 219x768, 768x256 and every larger row count
+# stay on torch.
 _FUSED_FWD_ROWS = {(512, 256): 8192, (256, 128): 8192, (128, 128): 32768}
 FUSED_FORWARD = os.environ.get("HG_FUSED_FORWARD", "1") != "0"
 

@@ -408,7 +408,8 @@ int hg_colsum_jobs(const float* const* src, float* const* dst, const int64_t* wi
  * actor_critic.py:36-149, torch's addmm + ELU): y[r][c] = act(sum_k x[r][k] W[c][k] + b[c]) for
  * r < rows, c < n; act 0 = identity, 1 = ELU(alpha 1).  x rows of stride ldx, W contiguous
  * [n, k] (both 4-byte aligned; 16-byte rows take the vector-load variant), b may be NULL, y rows
- * of stride ldy.  tile 0 = automatic wave tile, 1..4 = 64x64, 64x32, 32x64, 32x32.  One launch,
+ * of stride ldy.  tile 0 = automatic wave tile, 1..5 = 64x64, 64x32, 32x64, 32x32 (32x32x2 MFMA),
+ * 16x16 (16x16x4 MFMA).  One launch,
  * no host synchronisation, exact f32 products with f32 accumulation. */
 int hg_linear_act_forward(const float* x, int64_t ldx, const float* W, const float* b, float* y, int64_t ldy,
                           int64_t rows, int n, int k, int act, int tile, void* stream);

@@ -27,7 +27,7 @@ SHAPES = [("actor0_mb", 24576, 705, 512), ("actor1_mb", 24576, 512, 256), ("acto
           ("linvel0_roll", 4096, 705, 128), ("linvel1_roll", 4096, 128, 128),
           ("critic0_vals", 98304, 219, 768), ("critic1_vals", 98304, 768, 256), ("critic2_vals", 98304, 256, 128)]
 ITERS = int(os.environ.get("ITERS", 50))
-TILES = [int(t) for t in os.environ.get("TILES", "1,2,3,4").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "1,2,3,4,5").split(",")]
 
 
 def ours(x, W, b, y, tile):

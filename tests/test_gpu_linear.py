@@ -39,7 +39,7 @@ CASES = [(3001, 705, 512, 0), (4096, 512, 256, 0), (4096, 256, 128, 0), (24576, 
 
 
 @pytest.mark.parametrize("rows,k,n,pad", CASES)
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
 def test_linear_act_matches_fp64(rows, k, n, pad, tile):
     _need_gpu()
     from humanoid import _native as N
@@ -79,7 +79,7 @@ def test_linear_act_rejects_bad_arguments():
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     args = [x.data_ptr(), 16, W.data_ptr(), None, y.data_ptr(), 4, 8, 4, 16, 1, 0, s]
     assert L.hg_linear_act_forward(*args) == 0
-    for i, bad in ((1, 15), (5, 3), (9, 2), (10, 5), (6, 0)):  # ldx < k, ldy < n, act, tile, rows
+    for i, bad in ((1, 15), (5, 3), (9, 2), (10, 6), (6, 0)):  # ldx < k, ldy < n, act, tile, rows
         a = list(args)
         a[i] = bad
         assert L.hg_linear_act_forward(*a) != 0
