@@ -225,9 +225,52 @@ def cpu_baseline(n_envs=256, T=24, threads=None, iterations=3):
     return n_envs * T * iterations / dt, threads, dt
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run (one
+    process per GPU, rendezvous on 127.0.0.1) from this parent, which has not touched the GPU, and
+    return their exit code.  The ranks see WORLD_SIZE and run the benchmark themselves."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the multi-rank bookkeeping of a bench run (process group, barriers,
+    max-over-ranks time, rank 0's JSON line) with no GPU work, on gloo — the CPU test of the
+    launcher (tests/test_bench_launch.py)."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.time()
+    time.sleep(0.01 * (rank + 1))
+    elapsed = time.time() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "value": None, "ms_per_step": round(elapsed * 1e3, 3),
+                          "config": {"parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the run; without WORLD_SIZE in the environment, N > 1 launches "
+                         "N ranks itself")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher / rank-bookkeeping check only (no GPU work, gloo)")
     ap.add_argument("--steps", type=int, default=10, help="timed PPO iterations")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
@@ -248,14 +291,26 @@ def main():
                          "with 8192 envs/GPU, fp16 observation storage and a bf16 policy")
     args = ap.parse_args()
 
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus is not None and args.gpus > 1:
+        # no launcher: start the ranks from here, before anything initialises the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(world_env or "1")
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report a {world}-rank run as "
+              f"{args.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        launch_check(args, world, rank)
+        return
+
     if args.config == 3:
         args.terrain = "heightfield"
     c5 = args.config == 5
     if c5 and args.envs == 4096:
         args.envs = 8192
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.same_device:
         local = 0
     if world > 1:

@@ -96,11 +96,12 @@ __global__ void __launch_bounds__(256) k_gae_norm(float* __restrict__ adv, const
 }
 
 extern "C" int hg_gae_scan(const float* rewards, const uint8_t* dones, const float* values, const float* last_values,
-                           float* returns, float* advantages, double* stats, int T, int N, float gamma, float lam,
-                           int zero_stats, void* stream) {
+                           float* returns, float* advantages, double* stats, int64_t stats_len, int T, int N,
+                           float gamma, float lam, int zero_stats, void* stream) {
   if (T <= 0 || N <= 0 || !rewards || !dones || !values || !last_values || !returns || !advantages || !stats) return 1;
-  hipStream_t s = (hipStream_t)stream;
   const int nblocks = (N + 255) / 256;
+  if (stats_len < 2 + 2 * (int64_t)nblocks) return 1;  // the block partials would not fit
+  hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_gae_scan, dim3(nblocks), dim3(256), 0, s, rewards, dones, values, last_values, returns,
                      advantages, stats, T, N, gamma, lam);
   hipLaunchKernelGGL(k_gae_stats_final, dim3(1), dim3(64), 0, s, stats, nblocks, zero_stats);

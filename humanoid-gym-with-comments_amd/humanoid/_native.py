@@ -155,7 +155,7 @@ def load_library(path=LIB_PATH):
     L.hg_set_env_props.restype = ctypes.c_int
     L.hg_set_env_props.argtypes = [vp, vp, vp, vp]
     L.hg_gae_scan.restype = ctypes.c_int
-    L.hg_gae_scan.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+    L.hg_gae_scan.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                               ctypes.c_float, ctypes.c_int, vp]
     L.hg_gae_stats_len.restype = ctypes.c_int64
     L.hg_gae_stats_len.argtypes = [ctypes.c_int]

@@ -17,6 +17,7 @@ once per update.  The host therefore never waits for the GPU inside the minibatc
 CPU the reference's host-side arithmetic is kept verbatim (this is what the golden tests pin).
 """
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -35,6 +36,16 @@ def _world():
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size()
     return 1
+
+
+def _data_parallel():
+    """True when the update all-reduces its gradients: world size > 1, or (HG_DP_FORCE=1) an
+    initialised world-size-1 group, which runs the multi-rank code path — flat gradient buffer, the
+    per-minibatch collective between the two captured graphs — on one device (test of the RCCL path
+    on a one-GPU box)."""
+    if _world() > 1:
+        return True
+    return (os.environ.get("HG_DP_FORCE") == "1" and dist.is_available() and dist.is_initialized())
 
 
 
@@ -80,17 +91,18 @@ class PPO:
         self.actor_critic.to(self.device)
         self.storage = None
         self.world_size = _world()
+        self._dp = _data_parallel()
         self._params = list(self.actor_critic.parameters())
         self._on_device = torch.device(device).type == "cuda"
         self.use_graphs = self._on_device
         self._graphs = None
         self._graph_warm = False
         self._flat_grad = None
-        if self.world_size > 1:
+        if self._dp:
             with torch.no_grad():
                 for p in self._params:
                     dist.broadcast(p.data, src=0)
-        if self.world_size > 1:
+        if self._dp:
             # persistent flat gradient buffer: one all-reduce per minibatch, no pack/unpack copies
             numel = sum(p.numel() for p in self._params)
             # + one trailing slot: the minibatch KL mean rides along with the gradient all-reduce
@@ -338,7 +350,7 @@ class PPO:
         self._adapt_lr_from_kl(self._kl_mean(mu, sigma, old_mu, old_sigma))
 
     def _adapt_lr_from_kl(self, kl_mean):
-        if self.world_size > 1:
+        if self._dp:
             with torch.inference_mode():
                 dist.all_reduce(kl_mean)
                 kl_mean /= self.world_size
@@ -453,7 +465,7 @@ class PPO:
             if self._flat_grad is not None:
                 self._flat_grad.zero_()
                 loss.backward()
-                if self.world_size > 1:
+                if self._dp:
                     dist.all_reduce(self._flat_grad)
                     self._flat_grad /= self.world_size
             else:
@@ -537,7 +549,7 @@ class PPO:
         # world size 1: the whole update (epochs x minibatches, each with its LR rule and Adam step)
         # is ONE graph reading its row indices from a static permutation buffer; with ranks to
         # all-reduce between the backward and the step, two graphs per minibatch
-        self._whole = self.world_size == 1 and self._flat_grad is None
+        self._whole = not self._dp and self._flat_grad is None
         if self._whole:
             nmb = self.num_mini_batches
             self._perm = torch.zeros(nmb * mb, dtype=torch.int64, device=dev)
@@ -579,14 +591,14 @@ class PPO:
                 ac = self.actor_critic
                 self._kl_mean(ac.action_mean, ac.action_std, b["mu"], b["sigma"], out=self._kl)
             self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
-        if self.world_size > 1 and self._adaptive:
+        if self._dp and self._adaptive:
             self._kl_slot.copy_(self._kl)
         loss.backward()
 
     def _mb_step(self):
         """Captured minibatch step: adaptive learning rate, global-norm clip, fused Adam."""
         kl = self._kl
-        if self.world_size > 1:
+        if self._dp:
             # gradients and the KL mean were summed over ranks in ONE all-reduce
             self._flat_grad.div_(self.world_size)
             kl = self._kl_slot
@@ -624,7 +636,7 @@ class PPO:
                 for i in range(nmb):
                     self._idx.copy_(indices[i * mb:(i + 1) * mb])
                     ga.replay()
-                    if self.world_size > 1:
+                    if self._dp:
                         dist.all_reduce(self._flat_grad)  # gradients + the KL slot
                     gb.replay()
         num_updates = self.num_learning_epochs * nmb

@@ -10,6 +10,7 @@ There is no CPU path: GAE needs the HIP kernel (tensors on a ROCm device).  Test
 ``storage.gae_fn`` to an oracle explicitly.
 """
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -114,18 +115,22 @@ class RolloutStorage:
             L.hg_gae_stats_len.restype = ctypes.c_int64
             L.hg_gae_stats_len.argtypes = [ctypes.c_int]
             self._stats_buf = torch.zeros(int(L.hg_gae_stats_len(Nn)), dtype=torch.float64, device=self.rewards.device)
-            self._stats = self._stats_buf[:2]
+        # the kernel writes its block partials past stats[0..1]: always hand it the whole buffer
+        # (the gae_fn hook rebinds self._stats to a fresh 2-element tensor)
+        self._stats = self._stats_buf[:2]
         s = ctypes.c_void_p(torch.cuda.current_stream(self.rewards.device).cuda_stream)
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         N.check(L.hg_gae_scan(p(self.rewards), p(self.dones), p(self.values), p(lv), p(self.returns),
-                              p(self.advantages), p(self._stats), T, Nn, ctypes.c_float(gamma), ctypes.c_float(lam), 1, s))
+                              p(self.advantages), p(self._stats_buf), ctypes.c_int64(self._stats_buf.numel()), T, Nn,
+                              ctypes.c_float(gamma), ctypes.c_float(lam), 1, s))
         count = self._reduce_stats(T * Nn)
         N.check(L.hg_gae_normalize(p(self.advantages), p(self._stats), ctypes.c_int64(count),
                                    ctypes.c_int64(T * Nn), s))
 
     def _reduce_stats(self, count):
         """All-reduce (sum A, sum A^2) over the data-parallel group; returns the global count."""
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1
+                                                              or os.environ.get("HG_DP_FORCE") == "1"):
             dist.all_reduce(self._stats)
             count *= dist.get_world_size()
         return count

@@ -160,13 +160,47 @@ def command_grid(vx, vy, wz):
     return np.array(list(itertools.product(vx, vy, wz)), dtype=np.float32)
 
 
+def load_policy(path, device="cuda:0"):
+    """The actor to drive: a TorchScript export (policy_1.pt), an ONNX actor (Gemm/Elu chain, e.g.
+    the reference's humanoid/OnnxTest.onnx) or a weights npz (W0, b0, ..., W3, b3 in nn.Linear
+    layout; tests/golden/onnx_actor.npz).  ONNX and npz files are read as numbers only."""
+    if path.endswith(".onnx"):
+        from humanoid.utils.onnx_io import load_onnx_mlp
+        return load_onnx_mlp(path).to(device).eval()
+    if path.endswith(".npz"):
+        return mlp_from_weights(np.load(path, allow_pickle=False)).to(device).eval()
+    return torch.jit.load(path, map_location=device)
+
+
+def mlp_from_weights(w):
+    """nn.Sequential(Linear, ELU, ..., Linear) from a W0, b0, W1, b1, ... dict."""
+    import torch.nn as nn
+    layers, k = [], 0
+    while f"W{k}" in w:
+        W, b = np.asarray(w[f"W{k}"], np.float32), np.asarray(w[f"b{k}"], np.float32)
+        lin = nn.Linear(W.shape[1], W.shape[0])
+        with torch.no_grad():
+            lin.weight.copy_(torch.from_numpy(W))
+            lin.bias.copy_(torch.from_numpy(b))
+        if layers:
+            layers.append(nn.ELU())
+        layers.append(lin)
+        k += 1
+    return nn.Sequential(*layers)
+
+
 def run(policy, profile="mjcf", commands=((0.4, 0.0, 0.0),), duration=10.0, envs_per_command=4,
-        device="cuda:0", trace_env=0):
+        device="cuda:0", trace_env=0, env=None, record_q=False):
     """Drive ``policy`` (TorchScript or any callable [N, 705] -> [N, 12]) in the sim2sim loop.
+    ``env``: an env made by make_env(profile, len(commands) * envs_per_command, duration) whose
+    initial state the caller has read (the oracle comparison starts from it).  ``record_q``: keep
+    every env's joint positions per step (traces["q_all"], [steps, N, 12]).
     Returns (summary dict, traces dict)."""
     cmds = np.asarray(commands, dtype=np.float32).reshape(-1, 3)
     n = len(cmds) * envs_per_command
-    env = make_env(profile, n, duration, device)
+    if env is None:
+        env = make_env(profile, n, duration, device)
+    assert env.num_envs == n
     cmd = torch.tensor(np.repeat(cmds, envs_per_command, axis=0), device=env.device)
     cfg = env.cfg
     stack, nso = cfg.env.frame_stack, cfg.env.num_single_obs
@@ -178,8 +212,10 @@ def run(policy, profile="mjcf", commands=((0.4, 0.0, 0.0),), duration=10.0, envs
     err_w = torch.zeros(n, dtype=torch.float64, device=env.device)
     alive_steps = torch.zeros(n, dtype=torch.float64, device=env.device)
     falls = torch.zeros(n, dtype=torch.int64, device=env.device)
+    fall_step = torch.full((n,), -1, dtype=torch.int64, device=env.device)
     alive = torch.ones(n, dtype=torch.bool, device=env.device)
     tr = {k: [] for k in ("base_vel", "base_wz", "target_q", "q", "height")}
+    q_all = []
     with torch.no_grad():
         for k in range(steps):
             env.commands[:, :3] = cmd
@@ -191,7 +227,10 @@ def run(policy, profile="mjcf", commands=((0.4, 0.0, 0.0),), duration=10.0, envs
             wz = env.base_ang_vel[:, 2]
             fell = reset.bool()
             falls += fell.long()
+            fall_step = torch.where(fell & alive, torch.full_like(fall_step, k + 1), fall_step)
             alive &= ~fell
+            if record_q:
+                q_all.append(env.dof_pos.clone())
             live = alive.double()
             err_v += live * torch.linalg.vector_norm(vb[:, :2] - cmd[:, :2], dim=1).double()
             err_w += live * (wz - cmd[:, 2]).abs().double()
@@ -217,14 +256,18 @@ def run(policy, profile="mjcf", commands=((0.4, 0.0, 0.0),), duration=10.0, envs
     summary = dict(profile=profile, duration_s=duration, envs=n, envs_per_command=envs_per_command,
                    policy_dt=env.dt, sim_dt=env.sim_dt, pgs_iterations=int(env._hgcfg.pgs_iterations),
                    commands=per, falls=int(falls.sum()),
-                   survived_fraction=float((falls == 0).double().mean()))
+                   survived_fraction=float((falls == 0).double().mean()),
+                   fall_step=fall_step.cpu().tolist())
     traces = {k: np.asarray(v) for k, v in tr.items()}
+    if record_q:
+        traces["q_all"] = torch.stack(q_all).cpu().numpy()
     return summary, traces
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--load_model", required=True, help="TorchScript actor (exported policy_1.pt)")
+    ap.add_argument("--load_model", required=True,
+                    help="TorchScript actor (exported policy_1.pt), ONNX actor (.onnx) or weights (.npz)")
     ap.add_argument("--profile", default="mjcf", choices=["mjcf", "urdf"])
     ap.add_argument("--duration", type=float, default=20.0, help="seconds of simulated time")
     ap.add_argument("--vx", type=float, nargs="+", default=[-0.25, 0.0, 0.4])
@@ -233,7 +276,7 @@ def main(argv=None):
     ap.add_argument("--envs_per_command", type=int, default=16)
     ap.add_argument("--out", default=None, help="output directory (default: next to the policy)")
     a = ap.parse_args(argv)
-    policy = torch.jit.load(a.load_model, map_location="cuda:0")
+    policy = load_policy(a.load_model)
     summary, traces = run(policy, a.profile, command_grid(a.vx, a.vy, a.wz), a.duration, a.envs_per_command)
     out = a.out or os.path.join(os.path.dirname(os.path.abspath(a.load_model)), f"sim2sim_{a.profile}")
     os.makedirs(out, exist_ok=True)

@@ -232,12 +232,13 @@ int hg_measure_heights(void* sim, const float* points_xy, int num_points, float*
  * humanoid/algo/ppo/rollout_storage.py:122-143) ---- */
 /* Pass 1: reverse-time scan.  rewards/values/returns/advantages [T,N] f32, dones [T,N] u8,
  * last_values [N].  Writes returns and raw advantages, and adds (sum A, sum A^2) in float64 to
- * stats[0..1] (set instead of added when zero_stats != 0).  stats holds hg_gae_stats_len(N)
- * doubles: stats[2..] is scratch for the per-block partials, which are summed in a fixed order
- * (bitwise reproducible; no atomics).  Two launches. */
+ * stats[0..1] (set instead of added when zero_stats != 0).  stats holds stats_len doubles, at
+ * least hg_gae_stats_len(N): stats[2..] is scratch for the per-block partials, which are summed
+ * in a fixed order (bitwise reproducible; no atomics).  Returns HG_ERR_ARG (1) without launching
+ * when stats_len is too small.  Two launches. */
 int hg_gae_scan(const float* rewards, const uint8_t* dones, const float* values,
                 const float* last_values, float* returns, float* advantages, double* stats,
-                int T, int N, float gamma, float lam, int zero_stats, void* stream);
+                int64_t stats_len, int T, int N, float gamma, float lam, int zero_stats, void* stream);
 int64_t hg_gae_stats_len(int N);
 /* Pass 2: advantages = (A - mean) / (std_unbiased + 1e-8) with mean/std from stats over
  * `count` elements (count = T*N*world_size after an all-reduce of stats). */

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU session: the -m gpu suite (all tests, per-test timeout), then a short bench.  Stops at a
+# crash / timeout (pytest exit codes other than 0/1), never retries.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+  > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_gpu.log | grep -v PASSED | head -30
+tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ -n "$SKIP_BENCH" ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --steps ${STEPS:-10} --warmup 3 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+brc=$?
+echo "bench rc=$brc"
+tail -2 gpurun_out/bench.log
+exit $brc

@@ -103,17 +103,24 @@ def _global_batch():
                 dones=(rs.uniform(size=(T_STEPS, n, 1)) < 0.05).astype(np.uint8), last_critic=f(n, 219))
 
 
-def _worker(rank, world, port, out_path):
-    """world > 1: rank of a gloo group on cuda:0; world == 1: the single process on everything."""
+def _worker(rank, world, port, out_path, rccl=False):
+    """world > 1: rank of a gloo group on cuda:0; world == 1: the single process on everything;
+    rccl: the single process in a world-size-1 RCCL ("nccl") group with HG_DP_FORCE=1, i.e. the
+    multi-rank update (flat gradient, two graphs per minibatch, all-reduce between them) on RCCL."""
     import sys
     for p in (os.path.join(REPO, "humanoid-gym-with-comments_amd"), REPO):
         sys.path.insert(0, p)
     import torch.distributed as dist
     torch.cuda.set_device(0)
-    if world > 1:
+    if world > 1 or rccl:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
+    if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    elif rccl:
+        os.environ["HG_DP_FORCE"] = "1"
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        assert dist.get_backend() == "nccl"
     import bench
     from humanoid.algo.ppo import ActorCritic, PPO
     dev = "cuda:0"
@@ -165,9 +172,10 @@ def _worker(rank, world, port, out_path):
         torch.randperm = real_randperm
     flat = torch.cat([p.detach().reshape(-1) for p in ac.parameters()]).cpu()
     torch.save({"flat": flat, "lr": float(ppo.learning_rate), "losses": losses, "graphed": ppo._graphs is not None,
-                "whole": bool(getattr(ppo, "_whole", False)), "calls": calls[0],
+                "whole": bool(getattr(ppo, "_whole", False)), "calls": calls[0], "dp": bool(ppo._dp),
+                "backend": dist.get_backend() if dist.is_initialized() else None,
                 "accumulate_grad_warnings": sum("AccumulateGrad" in str(w.message) for w in caught)}, out_path)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -220,3 +228,29 @@ def test_dp_graphed_update_matches_single_process(tmp_path):
     for i, b in enumerate(S["losses"][-1]):
         a = sum(float(r["losses"][-1][i]) for r in R) / WORLD
         assert abs(a - float(b)) <= 1e-5 * max(1.0, abs(float(b)))
+
+
+def test_rccl_two_graph_update_matches_single_process(tmp_path):
+    """The RCCL code path executed: a world-size-1 "nccl" group with the
+    multi-rank update forced (HG_DP_FORCE=1) — parameter broadcast, the flat gradient buffer, the
+    backward graph -> dist.all_reduce on RCCL -> step graph per minibatch, the advantage-statistics
+    all-reduce.  At world size 1 the all-reduce is the identity, so the parameters must equal the
+    one-graph single-process update bit for bit."""
+    _need_gpu()
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    runs = {}
+    for name, rccl in (("rccl", True), ("single", False)):
+        p = ctx.Process(target=_worker, args=(0, 1, _port(), str(tmp_path / f"{name}.pt"), rccl))
+        p.start()
+        p.join(240)
+        assert p.exitcode == 0, f"{name} process exit code {p.exitcode}"
+        runs[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
+    R, S = runs["rccl"], runs["single"]
+    assert R["backend"] == "nccl" and R["dp"] and R["graphed"] and not R["whole"]
+    assert S["backend"] is None and not S["dp"] and S["whole"]
+    assert R["calls"] == S["calls"] == 3
+    assert R["lr"] == S["lr"]
+    assert torch.equal(R["flat"], S["flat"]), f"max |d| {(R['flat'] - S['flat']).abs().max().item():.3e}"
+    for a, b in zip(R["losses"], S["losses"]):
+        assert [float(x) for x in a] == [float(x) for x in b]

@@ -1,0 +1,44 @@
+"""The reference's trained actor (humanoid/OnnxTest.onnx -> tests/golden/onnx_actor.npz) driven
+closed-loop on hg_sim and on the CPU reference physics from the same initial state
+(scripts/onnx_closed_loop.py; reference loop humanoid/scripts/sim2sim.py:185-280).
+
+Stated agreement:
+  * while every run's env still stands, the GPU's closed-loop joint trajectory stays within
+    2 x the CPU fp32 ensemble's divergence from f64 (+1e-4 rad) at every policy step: the policy
+    in the loop amplifies fp32 rounding like any chaotic system, and the GPU may not amplify it
+    faster than fp32 arithmetic itself does;
+  * identical fall counts per command over the run, and each command's mean fall time within
+    0.25 s (or 15 %) of the f64 oracle's.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "scripts"))
+
+
+@pytest.mark.parametrize("profile", ["urdf"])
+def test_onnx_actor_closed_loop_gpu_vs_oracle(profile):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import onnx_closed_loop as OC
+    r = OC.compare(profile, envs_per_command=4, duration=2.0, ensemble=2)
+    div_gpu, div_f32 = np.array(r["div_gpu"]), np.array(r["div_f32"])
+    ok = ~np.isnan(div_gpu)
+    assert ok[:20].all(), "the envs must stand for the first 0.2 s"
+    run_gpu = np.maximum.accumulate(div_gpu[ok])
+    run_f32 = np.maximum.accumulate(div_f32[ok])
+    bad = run_gpu > 2.0 * run_f32 + 1e-4
+    print("closed-loop divergence (GPU / fp32 ensemble), every 10 steps:",
+          [f"{a:.1e}/{b:.1e}" for a, b in zip(run_gpu[::10], run_f32[::10])])
+    assert not bad.any(), f"first excess at step {int(np.argmax(bad))}: {run_gpu[bad][0]:.3e} vs {run_f32[bad][0]:.3e}"
+    for cg, co in zip(r["gpu"], r["oracle_f64"]):
+        assert cg["falls"] == co["falls"], (cg, co)
+        tol = max(0.25, 0.15 * co["mean_fall_time_s"])
+        assert abs(cg["mean_fall_time_s"] - co["mean_fall_time_s"]) <= tol, (cg, co)

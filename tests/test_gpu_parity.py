@@ -176,9 +176,9 @@ def test_post_parity_heightfield(terrain_env):
     _post_parity(terrain_env)
 
 
-def _post_parity(env):
+def _post_parity(env, steps=3):
     import pipeline_ref as PR
-    for _ in range(3):
+    for _ in range(steps):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.5)
     torch.cuda.synchronize()
     # force the branches: base contact on some envs, timeouts, command resample
@@ -250,16 +250,16 @@ def _step_only(env, actions, counter):
     torch.cuda.synchronize()
 
 
-def test_step_physics_parity(physics_env):
-    """One K_step (prologue + 10 substeps + rigid states) vs the C reference simulator."""
+def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), scale=0.5):
+    """One K_step (prologue + 10 substeps + rigid states) from the env's current state vs the C
+    reference simulator (f64, f32) on the identical state and preprocessed actions.  Stated fp32
+    tolerance: 20 x the larger of the CPU f32-vs-f64 gap and the local conditioning spread of the
+    f64 step, plus fp32 rounding (2^-20 relative, ~8 ulp); no absolute floor.
+    Returns the reference f64 sim."""
     import pipeline_ref as PR
-    env = physics_env
-    for _ in range(5):
-        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
     S, _, _ = snapshot(env)
     cfg = _oracle_cfg(env)
-    actions = torch.randn(env.num_envs, 12, device="cuda:0") * 0.5
-    counter = 77
+    actions = torch.randn(env.num_envs, 12, device="cuda:0") * scale
     a_ref = PR.preprocess_actions(cfg, actions.cpu().numpy(), S["actions"], counter)
     _step_only(env, actions, counter)
     g = lambda t: t.detach().cpu().numpy()  # noqa: E731
@@ -267,16 +267,88 @@ def test_step_physics_parity(physics_env):
     r64, r32 = _ref_sim(env, S, "f64"), _ref_sim(env, S, "f32")
     r64.step(a_ref)
     r32.step(a_ref)
-    sp = _ref_spread(env, S, a_ref, ("q", "qd", "root", "torques", "rigid"))
-    for name, gpu, a64, a32 in (("q", g(env.dof_pos), r64.q, r32.q), ("qd", g(env.dof_vel), r64.qd, r32.qd),
-                                ("root", g(env.root_states), r64.root, r32.root),
-                                ("torques", g(env.torques), r64.torques, r32.torques),
-                                ("rigid", g(env.rigid_state), r64.rigid, r32.rigid)):
-        # stated fp32 tolerance: 20 x the larger of the CPU f32-vs-f64 gap and the local
-        # conditioning spread of the f64 step, plus fp32 rounding (2^-20 relative, ~8 ulp)
+    sp = _ref_spread(env, S, a_ref, fields)
+    gpu = {"q": g(env.dof_pos), "qd": g(env.dof_vel), "root": g(env.root_states), "torques": g(env.torques),
+           "rigid": g(env.rigid_state)}
+    for name in fields:
+        a64, a32, x = getattr(r64, name), getattr(r32, name), gpu[name]
         tol = 20 * np.maximum(np.abs(a32 - a64), sp[name]) + 2.0 ** -20 * (1 + np.abs(a64))
-        bad = np.abs(gpu - a64) > tol
-        assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}"
+        bad = np.abs(x - a64) > tol
+        detail = "; ".join(f"{tuple(int(i) for i in ix)} gpu {x[tuple(ix)]:+.6f} f32 {a32[tuple(ix)]:+.6f} "
+                           f"f64 {a64[tuple(ix)]:+.6f} spread {sp[name][tuple(ix)]:.2e}"
+                           for ix in np.argwhere(bad)[:6])
+        assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(x - a64).max()}: {detail}"
+    assert not r64.nonfinite.any() and not g(env.nonfinite_count).any()
+    return r64
+
+
+def test_step_physics_parity(physics_env):
+    """One K_step (prologue + 10 substeps + rigid states) vs the C reference simulator."""
+    env = physics_env
+    for _ in range(5):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    _step_parity(env, 77)
+
+
+@pytest.fixture(scope="module")
+def bench_env():
+    """The bench's size (4096 envs: 2048 blocks, 256 per XCD, the full XCD-aware block -> env-pair
+    map of K_step and K_post's full grid)."""
+    _need_gpu()
+    return _make_env(4096)
+
+
+@pytest.fixture(scope="module")
+def bench_terrain_env():
+    _need_gpu()
+    return _make_env(4096, terrain__mesh_type="heightfield")
+
+
+@pytest.mark.parametrize("which", ["plane", "heightfield"])
+def test_step_and_post_parity_4096_envs(which, request):
+    """K_step and K_post against the oracle at the bench's 4096 envs (config 2 plane, config 3
+    heightfield): the same stated tolerances as the 64-env tests, every env checked."""
+    env = request.getfixturevalue("bench_env" if which == "plane" else "bench_terrain_env")
+    for _ in range(4):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    _step_parity(env, 131)
+    _post_parity(env, steps=0)
+
+
+def test_nonfinite_guard_resets_and_counts():
+    """Fault injection into the non-finite guard (csrc/hg_physics.hip epilogue): NaN joint
+    velocities in two envs make their substeps non-finite; K_step keeps their pre-step pose, counts
+    the event in HG_T_NONFINITE and pushes the base below ground with a base contact, so K_post's
+    termination resets them.  Every other env must be bit-identical to an untouched twin."""
+    _need_gpu()
+    env, twin = _make_env(N_ENVS), _make_env(N_ENVS)
+    for e in (env, twin):  # the same run twice (same seeds, same actions): bitwise-equal states
+        gen = torch.Generator(device="cpu").manual_seed(21)
+        for _ in range(3):
+            e.step((torch.randn(N_ENVS, 12, generator=gen) * 0.3).to("cuda:0"))
+    torch.cuda.synchronize()
+    assert torch.equal(env.dof_vel, twin.dof_vel) and torch.equal(env.root_states, twin.root_states)
+    bad = [5, 40]
+    before = env.nonfinite_count.clone()
+    env.dof_vel[bad, 3] = float("nan")
+    a = torch.randn(N_ENVS, 12, device="cuda:0") * 0.3
+    counter = 1000 + env.common_step_counter
+    _step_only(env, a, counter)
+    _step_only(twin, a, counter)
+    g = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    cnt = g(env.nonfinite_count - before)
+    assert cnt[bad].tolist() == [1, 1] and cnt.sum() == 2
+    assert (g(env.root_states)[bad, 2] < -5).all() and (g(env.contact_forces)[bad, 0, 2] > 1.0).all()
+    assert np.isfinite(g(env.dof_vel)[bad]).all()
+    others = np.setdiff1d(np.arange(N_ENVS), bad)
+    for k in ("root_states", "dof_pos", "dof_vel", "torques", "contact_forces", "rigid_state"):
+        np.testing.assert_array_equal(g(getattr(env, k))[others], g(getattr(twin, k))[others], err_msg=k)
+    # K_post terminates and resets exactly the faulted envs; their state is finite again
+    _post_once(env, counter + 1)
+    reset = g(env.reset_buf).astype(bool)
+    assert reset[bad].all()
+    assert np.isfinite(g(env.root_states)).all() and np.isfinite(g(env.dof_vel)).all()
+    assert (g(env.root_states)[bad, 2] > 0.5).all()
 
 
 # Stated fp32 tolerances of the SURVEY §8d parity trajectory (1000 policy steps = 10,000
@@ -496,40 +568,15 @@ def terrain_env():
 
 def test_step_physics_parity_heightfield(terrain_env):
     """K_step on the generated heightfield (config 3 terrain) vs the C reference simulator
-    colliding against the same int16 samples."""
+    colliding against the same int16 samples, at the plane test's stated tolerance (no absolute
+    floor)."""
     env = terrain_env
     assert env._hgcfg.terrain_type == 1 and tuple(env.height_samples.shape) == (2100, 2100)
     for _ in range(30):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
-    S, _, _ = snapshot(env)
-    import pipeline_ref as PR
-    cfg = _oracle_cfg(env)
-    actions = torch.randn(env.num_envs, 12, device="cuda:0") * 0.5
-    a_ref = PR.preprocess_actions(cfg, actions.cpu().numpy(), S["actions"], 91)
-    _step_only(env, actions, 91)
-    g = lambda t: t.detach().cpu().numpy()  # noqa: E731
-    r64, r32 = _ref_sim(env, S, "f64"), _ref_sim(env, S, "f32")
-    r64.step(a_ref)
-    r32.step(a_ref)
-    dump = os.environ.get("HG_FAIL_DUMP")
-    if dump:  # the pre-step state and both results, for offline diagnosis
-        from humanoid import _native as N
-        np.savez(dump, a_ref=a_ref, gpu_q=g(env.dof_pos), gpu_qd=g(env.dof_vel), gpu_root=g(env.root_states),
-                 gpu_cf=g(env.contact_forces), gpu_lam=g(env._view(N.T["CONTACT_LAMBDA"])), r64_lam=r64.lam,
-                 r64_cf=r64.contact, **{"S_" + k: v for k, v in S.items()})
-    sp = _ref_spread(env, S, a_ref, ("q", "qd", "root"))
-    # the spread widens the tolerance only where the reference itself is ill-conditioned
-    assert np.median(sp["qd"]) < 1e-3 and np.mean(sp["qd"] > 1e-2) < 0.05, np.percentile(sp["qd"], [50, 95, 100])
-    for name, gpu, a64, a32 in (("q", g(env.dof_pos), r64.q, r32.q), ("qd", g(env.dof_vel), r64.qd, r32.qd),
-                                ("root", g(env.root_states), r64.root, r32.root)):
-        tol = 20 * np.maximum(np.abs(a32 - a64), sp[name]) + 1e-3 * (1 + np.abs(a64))
-        bad = np.abs(gpu - a64) > tol
-        detail = "; ".join(f"[{e},{j}] gpu {gpu[e, j]:+.5f} f32 {a32[e, j]:+.5f} f64 {a64[e, j]:+.5f} "
-                           f"spread {sp[name][e, j]:.2e} root_z {S['root_states'][e, 2]:.3f}"
-                           for e, j in np.argwhere(bad)[:6])
-        assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(gpu - a64).max()}: {detail}"
+    _step_parity(env, 91, fields=("q", "qd", "root", "torques"))
     # the robots stand on terrain: base heights follow the sub-terrain origins, not z = 0
-    assert np.isfinite(g(env.root_states)).all()
+    assert np.isfinite(env.root_states.cpu().numpy()).all()
 
 
 def test_measured_heights(terrain_env):
