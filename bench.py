@@ -34,11 +34,11 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) dense peak
 HBM_PEAK_GBS = 8000.0
-# K_step algorithmic HBM bytes per env and launch: 732 B read (policy actions,
-# previous actions, dof pos / vel, root, 120 warm-start impulses, mass, friction) + 1748 B written
-# (actions, rigid 13x13, contacts 13x3, root, dof pos / vel, torques, 120 warm-start impulses, and
+# K_step algorithmic HBM bytes per env and launch: 828 B read (policy actions,
+# previous actions, dof pos / vel, root, 144 warm-start impulses, mass, friction) + 1844 B written
+# (actions, rigid 13x13, contacts 13x3, root, dof pos / vel, torques, 144 warm-start impulses, and
 # the next post launch's 48 observation-noise normals)
-KSTEP_BYTES_PER_ENV = 732 + 1748
+KSTEP_BYTES_PER_ENV = 828 + 1844
 PROFILE_DIR = "r2_v3"  # the committed rocprofv3 summaries of the current kernels
 PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
@@ -115,13 +115,15 @@ def physics_flops_per_env_step(rows, decimation=10, sweeps=5, nf=18):
 
 def active_rows(env):
     """Mean constraint rows per env of the last solve, from the warm-start impulse table
-    (HG_LAMW layout, csrc/hg_physics.hip: [0, 72) ground contacts x 3, [72, 96) leg-pair contacts
-    x 3, [96, 108) joint limits, [108, 120) joint-friction rows): a contact with a positive
-    normal impulse holds 3 rows, an active limit 1, every joint with friction 1 (always solved)."""
+    (HG_LAMW layout, csrc/hg_physics.hip: [0, 72) ground contacts x 3, [72, 120) self-collision
+    pair contacts x 3, [120, 132) joint limits, [132, 144) joint-friction rows): a contact with a
+    positive normal impulse holds 3 rows, an active limit 1, every joint with friction 1 (always
+    solved)."""
     from humanoid import _native as N
     lam = env._view(N.T["CONTACT_LAMBDA"])
-    contacts = (lam[:, 0:96:3] > 0).sum(dim=1).float()
-    limits = (lam[:, 96:108] != 0).sum(dim=1).float()
+    nc3 = (N.HG_MAX_CONTACTS + N.HG_MAX_PAIRS) * 3
+    contacts = (lam[:, 0:nc3:3] > 0).sum(dim=1).float()
+    limits = (lam[:, nc3:nc3 + N.HG_MAX_DOF] != 0).sum(dim=1).float()
     fric = sum(1 for b in range(len(env._model.joint_friction)) if env._model.joint_friction[b] > 0)
     return float((3 * contacts + limits).mean().item() + fric)
 

@@ -51,7 +51,7 @@ int soa_rows(int id) {
     case HG_T_COMMANDS: return 4;
     case HG_T_REW_BUF: case HG_T_RESET_BUF: case HG_T_TIME_OUT_BUF: case HG_T_EPISODE_LENGTH:
     case HG_T_ENV_FRICTION: case HG_T_BODY_MASS: case HG_T_NONFINITE: case HG_T_TERRAIN_LEVEL:
-    case HG_T_TERRAIN_TYPE: return 1;
+    case HG_T_TERRAIN_TYPE: case HG_T_ROWS_DROPPED: return 1;
     case HG_T_EPISODE_SUMS: return HG_NUM_REWARDS;
     case HG_T_FEET_AIR_TIME: case HG_T_LAST_CONTACTS: case HG_T_FEET_HEIGHT: case HG_T_LAST_FEET_Z: return 2;
     case HG_T_PUSH_FORCE: case HG_T_PUSH_TORQUE: case HG_T_BASE_LIN_VEL: case HG_T_BASE_ANG_VEL:
@@ -64,7 +64,7 @@ int dtype_of(int id) {
   switch (id) {
     case HG_T_RESET_BUF: case HG_T_TIME_OUT_BUF: case HG_T_LAST_CONTACTS: return 2;
     case HG_T_EPISODE_LENGTH: return 1;
-    case HG_T_NONFINITE: case HG_T_TERRAIN_LEVEL: case HG_T_TERRAIN_TYPE: return 3;
+    case HG_T_NONFINITE: case HG_T_TERRAIN_LEVEL: case HG_T_TERRAIN_TYPE: case HG_T_ROWS_DROPPED: return 3;
     default: return 0;
   }
 }
@@ -153,13 +153,18 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
     return fail(nullptr, HG_ERR_ARG, "model must have 13 bodies / 12 dofs (XBot-L profile)");
   if (model->num_contacts <= 0 || model->num_contacts > HG_MAX_CONTACTS) return fail(nullptr, HG_ERR_ARG, "bad contact count");
   if (model->num_pairs < 0 || model->num_pairs > HG_MAX_PAIRS || model->num_capsules < 0 ||
-      model->num_capsules > HG_MAX_CAPSULES || model->num_contacts + model->num_pairs > 32 ||
+      model->num_capsules > HG_MAX_CAPSULES || model->num_contacts + model->num_pairs > 64 ||
       model->num_leg_contacts < 0 || model->num_leg_contacts > model->num_contacts)
-    return fail(nullptr, HG_ERR_ARG, "bad collision model (<= 32 contact candidates + pairs)");
-  for (int p = 0; p < model->num_pairs; p++)
+    return fail(nullptr, HG_ERR_ARG, "bad collision model (<= 64 contact candidates + pairs)");
+  for (int p = 0; p < model->num_pairs; p++) {
     for (int s = 0; s < 2; s++)
       if (model->pair[p][s] < 0 || model->pair[p][s] >= model->num_capsules)
         return fail(nullptr, HG_ERR_ARG, "pair names a missing capsule");
+    if (model->capsule_kind[model->pair[p][1]] != 0 || model->capsule_kind[model->pair[p][0]] < 0 ||
+        model->capsule_kind[model->pair[p][0]] > 1 ||
+        (model->capsule_kind[model->pair[p][0]] == 1 && model->capsule_body[model->pair[p][0]] != 0))
+      return fail(nullptr, HG_ERR_ARG, "a box-face primitive (kind 1, on the base) may only be a pair's first shape");
+  }
   for (int b = 1; b < HG_NB; b++)  // two 6-link leg chains off the base (XBot-L topology)
     if (model->parent[b] != ((b == 1 || b == 7) ? 0 : b - 1))
       return fail(nullptr, HG_ERR_ARG, "model topology must be base + two 6-link leg chains (bodies 1-6, 7-12)");
@@ -228,6 +233,7 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   S.nonfinite = (int32_t*)P(HG_T_NONFINITE);
   S.terrain_level = (int32_t*)P(HG_T_TERRAIN_LEVEL);
   S.terrain_type = (int32_t*)P(HG_T_TERRAIN_TYPE);
+  S.rows_dropped = (int32_t*)P(HG_T_ROWS_DROPPED);
   S.cfg = (const hg_cfg*)(s->arena + s->L.cfg);
   S.model = (const hg_model*)(s->arena + s->L.model);
   S.obs_noise = (float*)(s->arena + s->L.obs_noise);

@@ -54,6 +54,7 @@ struct HgState {
   int32_t* nonfinite;     // [np]
   int32_t* terrain_level; // [np]
   int32_t* terrain_type;  // [np]
+  int32_t* rows_dropped;  // [np] rows / contact points the row budget dropped (K_step, summed over substeps)
   float* obs_noise;       // [np][48] N(0,1) observation noise of the next post launch (K_step epilogue;
                           // per-env rows, so each wave writes whole cache lines)
   uint64_t* noise_counter;// [1] the post counter obs_noise was drawn for (~0: none)

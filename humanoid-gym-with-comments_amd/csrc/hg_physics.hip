@@ -12,8 +12,11 @@
 //   * Cholesky of M in registers (lane i = row i, legs-first order, arrow structure skipped), with
 //     g = L^-1 (tau - h) carried along as an extra column; no explicit inverse.
 //   * Contacts: one candidate per lane — sole points / capsule end spheres vs plane or
-//     heightfield, leg-vs-leg capsule pairs (segment closest points) — ranked by ballot/popcount;
-//     at most 9 points (27 rows), then the ankle joint-friction rows, then joint limits (<= 32).
+//     heightfield, self-collision pairs (leg-vs-leg capsules, hands vs thigh / shin, base-box
+//     bottom face vs thighs; segment closest points) — items past lane 31 in a second round;
+//     ranked by ballot/popcount; at most 9 points (27 rows), then joint limits, then the
+//     joint-friction rows, largest bound first, left / right alike (<= 32; dropped rows counted
+//     per env).
 //   * Lane r owns constraint row r: Jacobian row in registers, z_r = L^-1 J_r^T by a per-lane
 //     forward solve (L broadcast from LDS), the Delassus matrix W = Z^T Z on the matrix cores
 //     (v_mfma_f32_32x32x2f32, 9 per env; the wave's two envs interleaved with v_permlane32_swap).
@@ -84,6 +87,7 @@ struct __align__(16) EnvSh {
   float base_cm, base_cs[3], base_cJ[6];
   float mass0, fric;
   int nrows, npts, bad;
+  int drop;                // rows / contact points over the budget this launch (HG_T_ROWS_DROPPED)
 };
 static_assert(offsetof(EnvSh, L) % 16 == 0 && offsetof(EnvSh, invd) % 16 == 0 && offsetof(EnvSh, gv) % 16 == 0 &&
               offsetof(EnvSh, u) % 16 == 0, "16-byte LDS row accesses (ld_vec / st_vec)");
@@ -420,6 +424,130 @@ __device__ __forceinline__ void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3& c1, f3& 
   c2 = p2 + t * d2;
 }
 
+// ---- contact candidates (A9).  One candidate per lane: a ground candidate c (sole point /
+// capsule end sphere on body b0 vs plane or heightfield) or a self-collision pair p of capsules
+// (a on b0, b on b1; normal from a to b; +lambda d on b1, -lambda d on b0).  Per-lane model
+// constants k: ground [0..2] point, [3] radius; pair [0..5] a's segment, [6..11] b's segment,
+// [12] a's radius (< 0: a is the base-box bottom face, [0..5] its corner extremes in the base
+// frame), [13] b's radius.  As oracle/physics_ref.c substep's detection loop.
+struct Cand {
+  f3 cn, xP, xN;
+  float phi, mu;
+  int bP, bN, lam_base;
+  bool act;
+};
+
+// item -> (pair?, ground index c, pair index p, bodies, constants), in the oracle's item order
+__device__ __forceinline__ bool load_item(const hg_model* M, int item, int nleg, int npair, int& c, int& p, int& b0,
+                                          int& b1, float* k) {
+  const bool pr = item >= nleg && item < nleg + npair;
+  c = min(item < nleg ? item : item - npair, HG_MAX_CONTACTS - 1);
+  p = min(max(item - nleg, 0), HG_MAX_PAIRS - 1);
+  if (!pr) {
+    b0 = M->contact_body[c];
+    b1 = -1;
+    k[0] = M->contact_pos[c][0]; k[1] = M->contact_pos[c][1]; k[2] = M->contact_pos[c][2];
+    k[3] = M->contact_radius[c];
+#pragma unroll
+    for (int i = 4; i < 14; i++) k[i] = 0.f;
+  } else {
+    const int ca = M->pair[p][0], cb = M->pair[p][1];
+    b0 = M->capsule_body[ca];
+    b1 = M->capsule_body[cb];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      k[i] = M->capsule_p0[ca][i]; k[3 + i] = M->capsule_p1[ca][i];
+      k[6 + i] = M->capsule_p0[cb][i]; k[9 + i] = M->capsule_p1[cb][i];
+    }
+    k[12] = M->capsule_kind[ca] == 1 ? -1.f : M->capsule_radius[ca];
+    k[13] = M->capsule_radius[cb];
+  }
+  return pr;
+}
+
+__device__ __forceinline__ Cand detect(const EnvSh& E, const hg_cfg* cfg, bool is_pair, int c, int p, int b0, int b1,
+                                       const float* k, bool fixed) {
+  Cand C;
+  C.cn = mk(0, 0, 1); C.xP = mk(0, 0, 0); C.xN = mk(0, 0, 0);
+  C.phi = 0.f; C.mu = 0.f; C.bP = -1; C.bN = -1; C.lam_base = 0; C.act = false;
+  if (!is_pair) {
+    const f3 x = ld3(E.o[b0]) + mv3(E.R[b0], mk(k[0], k[1], k[2]));
+    float hg;
+    ground(cfg, x.x + E.root[0], x.y + E.root[1], &hg, &C.cn);
+    const float r = k[3];
+    C.phi = (x.z + E.root[2] - hg) * C.cn.z - r;
+    C.xP = x - r * C.cn;
+    C.bP = b0;
+    C.mu = 0.5f * (E.fric + cfg->ground_friction);
+    C.lam_base = 3 * c;
+    C.act = !fixed && C.phi < cfg->contact_offset;
+    return C;
+  }
+  const f3 ob = ld3(E.o[b1]);
+  const f3 q0 = ob + mv3(E.R[b1], mk(k[6], k[7], k[8])), q1 = ob + mv3(E.R[b1], mk(k[9], k[10], k[11]));
+  const float rb = k[13];
+  f3 pa, pb;
+  float dist, ra;
+  if (k[12] < 0.f) {
+    // base-box bottom face (base frame z = k[2] over [k0, k3] x [k1, k4], outward normal -z of
+    // the base) vs the closer end sphere of capsule b
+    const float* R0 = E.R[0];
+    const float h0 = k[2] - (R0[2] * q0.x + R0[5] * q0.y + R0[8] * q0.z);
+    const float h1 = k[2] - (R0[2] * q1.x + R0[5] * q1.y + R0[8] * q1.z);
+    const bool s1 = h1 < h0;
+    const f3 e = s1 ? q1 : q0;
+    const float h = s1 ? h1 : h0;
+    const float ex = R0[0] * e.x + R0[3] * e.y + R0[6] * e.z, ey = R0[1] * e.x + R0[4] * e.y + R0[7] * e.z;
+    const bool inside = ex >= k[0] && ex <= k[3] && ey >= k[1] && ey <= k[4];
+    C.cn = mk(-R0[2], -R0[5], -R0[8]);
+    pb = e;
+    pa = e - h * C.cn;
+    ra = 0.f;
+    dist = inside ? h : 1e3f;
+  } else {
+    const f3 oa = ld3(E.o[b0]);
+    seg_seg(oa + mv3(E.R[b0], mk(k[0], k[1], k[2])), oa + mv3(E.R[b0], mk(k[3], k[4], k[5])), q0, q1, pa, pb);
+    const f3 dv = pb - pa;
+    dist = sqrtf(dot(dv, dv));
+    C.cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);
+    ra = k[12];
+  }
+  C.phi = dist - ra - rb;
+  C.xP = pb - rb * C.cn;
+  C.xN = pa + ra * C.cn;
+  C.bP = b1;
+  C.bN = b0;
+  C.mu = E.fric;
+  C.lam_base = LAM_PAIR + 3 * p;
+  C.act = C.phi < cfg->contact_offset;
+  return C;
+}
+
+// an active candidate of contact rank `rank` (< npts kept): its contact record (the three rows
+// read it in A10) and its PGS group; otherwise its warm-start slots are cleared
+__device__ __forceinline__ void place_contact(EnvSh& E, const Cand& C, bool act, int rank, int npts, float inv_dt,
+                                              float beta, float vmax) {
+  if (act && rank < npts) {
+    const float tgt = C.phi >= 0.f ? -C.phi * inv_dt : fminf(-beta * C.phi * inv_dt, vmax);
+    // tangent basis (reference axis x, or y when the normal is close to x)
+    const f3 ref = fabsf(C.cn.x) < 0.9f ? mk(1, 0, 0) : mk(0, 1, 0);
+    f3 t1 = ref - dot(ref, C.cn) * C.cn;
+    t1 = rsqrtf(dot(t1, t1)) * t1;
+    const f3 t2 = cross(C.cn, t1);
+    ContactC& R = E.ct[rank];
+    st3(R.xP, C.xP); st3(R.xN, C.xN);
+    st3(R.dir[0], C.cn); st3(R.dir[1], t1); st3(R.dir[2], t2);
+    R.bP = C.bP; R.bN = C.bN; R.lam_base = C.lam_base;
+    GroupC& G = E.grp[rank];
+    G.mu = C.mu;
+    G.tgt[0] = tgt; G.tgt[1] = 0.f; G.tgt[2] = 0.f;
+    G.lo[0] = 0.f; G.lo[1] = -BIG; G.lo[2] = -BIG;
+    G.hi[0] = BIG; G.hi[1] = BIG; G.hi[2] = BIG;
+  } else {
+    E.lamst[C.lam_base + 0] = E.lamst[C.lam_base + 1] = E.lamst[C.lam_base + 2] = 0.f;
+  }
+}
+
 }  // namespace
 
 // FIXED = asset.fix_base_link, a compile-time constant so the factorised size and every
@@ -470,6 +598,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     E.mass0 = S.body_mass[e];
     E.fric = S.friction[e];
     E.bad = 0;
+    E.drop = 0;
   }
   __syncthreads();
   const float scale0 = E.mass0 / M->mass[0];
@@ -488,33 +617,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // (body, sole point / sphere centre, radius) or capsule pair (bodies, segment ends, radii),
   // and its joint's limits and friction
   const int nleg = M->num_leg_contacts, npair = M->num_pairs, nitems = M->num_contacts + npair;
-  const bool det_pair = l >= nleg && l < nleg + npair;
-  const int det_c = min(l < nleg ? l : l - npair, HG_MAX_CONTACTS - 1);
-  const int det_p = min(max(l - nleg, 0), HG_MAX_PAIRS - 1);
-  int det_b0, det_b1;
+  int det_c, det_p, det_b0, det_b1;
   float det_k[14];
-  if (!det_pair) {
-    det_b0 = M->contact_body[det_c];
-    det_b1 = -1;
-    const f3 cp = ld3(M->contact_pos[det_c]);
-    det_k[0] = cp.x; det_k[1] = cp.y; det_k[2] = cp.z;
-    det_k[3] = M->contact_radius[det_c];
-#pragma unroll
-    for (int i = 4; i < 14; i++) det_k[i] = 0.f;
-  } else {
-    const int ca = M->pair[det_p][0], cb = M->pair[det_p][1];
-    det_b0 = M->capsule_body[ca];
-    det_b1 = M->capsule_body[cb];
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      det_k[i] = M->capsule_p0[ca][i]; det_k[3 + i] = M->capsule_p1[ca][i];
-      det_k[6 + i] = M->capsule_p0[cb][i]; det_k[9 + i] = M->capsule_p1[cb][i];
-    }
-    det_k[12] = M->capsule_radius[ca];
-    det_k[13] = M->capsule_radius[cb];
-  }
+  const bool det_pair = load_item(M, min(l, nitems - 1), nleg, npair, det_c, det_p, det_b0, det_b1, det_k);
   const int lj = l < 12 ? l + 1 : 1;
   const float lim_lo = M->lower[lj], lim_hi = M->upper[lj], jfric = M->joint_friction[lj];
+  // this joint's slot among the friction rows: larger friction bounds first, then the joint
+  // within its leg, left before right (the rows the budget drops are the smallest bounds, from
+  // both legs alike)
+  int frank = 0;
+  for (int j = 0; j < 12; j++) {
+    const float fj = M->joint_friction[j + 1];
+    const bool before = fj > jfric || (fj == jfric && (j % 6 < l % 6 || (j % 6 == l % 6 && j < l)));
+    frank += (fj > 0.f && before) ? 1 : 0;
+  }
 
   for (int sub = 0; sub < decimation; sub++) {
     // lane masks are rebuilt per substep (v_cmp) instead of living across the loop in SGPR pairs
@@ -647,48 +763,38 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     __syncthreads();
     // ---- A9: contact detection (one candidate per lane, in priority order: ground candidates
-    // [0, num_leg_contacts), the leg-vs-leg capsule pairs, the remaining ground candidates),
-    // joint limits, and row allocation by ballot / popcount
+    // [0, num_leg_contacts), the self-collision pairs, the remaining ground candidates; items
+    // 32.. run as a second round on lanes 0..), joint limits, and row allocation by ballot /
+    // popcount: contacts (<= 9 points), then joint limits, then joint friction (<= 32 rows; the
+    // rest dropped and counted)
     {
-      bool act_c = false;
-      f3 cn = mk(0, 0, 1), xP = mk(0, 0, 0), xN = mk(0, 0, 0);
-      float phi = 0.f, mu = 0.f;
-      int bP = -1, bN = -1, lam_base = 0;
-      if (l < nitems) {
-        if (!det_pair) {
-          const int c = det_c;
-          const int b = det_b0;
-          const f3 x = ld3(E.o[b]) + mv3(E.R[b], mk(det_k[0], det_k[1], det_k[2]));
-          float hg;
-          ground(cfg, x.x + E.root[0], x.y + E.root[1], &hg, &cn);
-          const float r = det_k[3];
-          phi = (x.z + E.root[2] - hg) * cn.z - r;
-          xP = x - r * cn;
-          bP = b;
-          mu = 0.5f * (E.fric + cfg->ground_friction);
-          lam_base = 3 * c;
-          act_c = !fixed && phi < cfg->contact_offset;
-        } else {
-          const int p = det_p;
-          const int ba = det_b0, bb = det_b1;
-          const f3 oa = ld3(E.o[ba]), ob = ld3(E.o[bb]);
-          f3 pa, pb;
-          seg_seg(oa + mv3(E.R[ba], mk(det_k[0], det_k[1], det_k[2])), oa + mv3(E.R[ba], mk(det_k[3], det_k[4], det_k[5])),
-                  ob + mv3(E.R[bb], mk(det_k[6], det_k[7], det_k[8])), ob + mv3(E.R[bb], mk(det_k[9], det_k[10], det_k[11])),
-                  pa, pb);
-          const f3 dv = pb - pa;
-          const float dist = sqrtf(dot(dv, dv));
-          cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);
-          const float ra = det_k[12], rb = det_k[13];
-          phi = dist - ra - rb;
-          xP = pb - rb * cn;
-          xN = pa + ra * cn;
-          bP = bb;
-          bN = ba;
-          mu = E.fric;
-          lam_base = LAM_PAIR + 3 * p;
-          act_c = phi < cfg->contact_offset;
-        }
+      const uint32_t lt = (1u << l) - 1u;
+      const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
+      if (l < NGRP) E.grp[l].mu = -1.f;  // single rows unless a contact claims the group below
+      // round 1: items 0..31 (model constants in registers for the whole launch); round 2 (when
+      // the model has more than 32 items): items 32 + l, constants read here.  A contact's rank
+      // among the active candidates decides its slot; round 2 ranks after all of round 1, so each
+      // round places its contacts before the next runs.  One loop body (not unrolled): one copy of
+      // the detection code.
+      int npts_all = 0;
+      const int rounds = nitems > 32 ? 2 : 1;
+#pragma unroll 1
+      for (int rnd = 0; rnd < rounds; rnd++) {
+        const int item = 32 * rnd + l;
+        bool pr = det_pair;
+        int cc = det_c, pp = det_p, b0 = det_b0, b1 = det_b1;
+        float k[14];
+#pragma unroll
+        for (int i = 0; i < 14; i++) k[i] = det_k[i];
+        if (rnd) pr = load_item(M, min(item, nitems - 1), nleg, npair, cc, pp, b0, b1, k);
+        Cand c;
+        if (item < nitems) c = detect(E, cfg, pr, cc, pp, b0, b1, k, fixed);
+        const bool act = item < nitems && c.act;
+        const uint32_t mc = (uint32_t)(__ballot(act) >> (32 * half));
+        const int n = __popc(mc);
+        if (item < nitems)
+          place_contact(E, c, act, npts_all + __popc(mc & lt), min(npts_all + n, MAX_PTS), inv_dt, beta, vmax);
+        npts_all += n;
       }
       bool act_l = false, has_f = false;
       float gapv = 0.f, sgnv = 1.f, ffric = 0.f;
@@ -699,57 +805,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         ffric = jfric;
         has_f = ffric > 0.f;
       }
-      const uint32_t mc = (uint32_t)(__ballot(act_c) >> (32 * half));
       const uint32_t ml = (uint32_t)(__ballot(act_l) >> (32 * half)) & 0xFFFu;
       const uint32_t mf = (uint32_t)(__ballot(has_f) >> (32 * half)) & 0xFFFu;
-      const int npts = min(__popc(mc), MAX_PTS);
-      const int nfr = __popc(mf);
-      const int nrows = min(RMAX, 3 * npts + nfr + __popc(ml));
-      const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
-      if (l == 0) { E.nrows = nrows; E.npts = npts; }
-      // group-level fields and empty slots
-      if (l < NGRP) E.grp[l].mu = -1.f;  // single rows unless a contact claims the group below
+      const int npts = min(npts_all, MAX_PTS);
+      const int nlim = __popc(ml), nfr = __popc(mf);
+      const int wanted = 3 * npts + nlim + nfr;
+      const int nrows = min(RMAX, wanted);
+      if (l == 0) {
+        E.nrows = nrows;
+        E.npts = npts;
+        E.drop += (wanted - nrows) + 3 * (npts_all - npts);
+      }
+      // empty slots
       for (int r = l; r < 3 * NGRP; r += 32) {
         if (r >= nrows) {
           const int g = r / 3, k = r % 3;
           E.grp[g].tgt[k] = 0.f; E.grp[g].lo[k] = 0.f; E.grp[g].hi[k] = 0.f;
         }
       }
-      const int rank = __popc(mc & ((1u << l) - 1u));
-      if (l < nitems) {
-        if (act_c && rank < npts) {
-          const float tgt = phi >= 0.f ? -phi * inv_dt : fminf(-beta * phi * inv_dt, vmax);
-          // tangent basis (reference axis x, or y when the normal is close to x)
-          const f3 ref = fabsf(cn.x) < 0.9f ? mk(1, 0, 0) : mk(0, 1, 0);
-          f3 t1 = ref - dot(ref, cn) * cn;
-          t1 = rsqrtf(dot(t1, t1)) * t1;
-          const f3 t2 = cross(cn, t1);
-          // one record per contact (its three rows read it in A10)
-          ContactC& C = E.ct[rank];
-          st3(C.xP, xP); st3(C.xN, xN);
-          st3(C.dir[0], cn); st3(C.dir[1], t1); st3(C.dir[2], t2);
-          C.bP = bP; C.bN = bN; C.lam_base = lam_base;
-          GroupC& G = E.grp[rank];
-          G.mu = mu;
-          G.tgt[0] = tgt; G.tgt[1] = 0.f; G.tgt[2] = 0.f;
-          G.lo[0] = 0.f; G.lo[1] = -BIG; G.lo[2] = -BIG;
-          G.hi[0] = BIG; G.hi[1] = BIG; G.hi[2] = BIG;
-        } else {
-          E.lamst[lam_base + 0] = E.lamst[lam_base + 1] = E.lamst[lam_base + 2] = 0.f;
-        }
-      }
       if (l < 12) {
-        const int rf = 3 * npts + __popc(mf & ((1u << l) - 1u));
-        if (has_f && rf < RMAX) {  // joint friction: |lambda| <= f dt (rows past RMAX dropped)
-          const int r = rf;
-          E.rd[r][0] = 1.f; E.rbP[r] = -1 - l; E.rbN[r] = -1;
-          E.rlam[r] = LAM_FRIC + l;
-          E.rLam[r] = E.lamst[LAM_FRIC + l];
-          E.grp[r / 3].tgt[r % 3] = 0.f; E.grp[r / 3].lo[r % 3] = -ffric * dt; E.grp[r / 3].hi[r % 3] = ffric * dt;
-        } else {
-          E.lamst[LAM_FRIC + l] = 0.f;
-        }
-        const int r = 3 * npts + nfr + __popc(ml & ((1u << l) - 1u));
+        const int r = 3 * npts + __popc(ml & lt);
         if (act_l && r < RMAX) {
           E.rd[r][0] = sgnv; E.rbP[r] = -1 - l; E.rbN[r] = -1;
           E.rlam[r] = LAM_LIM + l;
@@ -758,6 +833,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
           E.grp[r / 3].lo[r % 3] = 0.f; E.grp[r / 3].hi[r % 3] = BIG;
         } else {
           E.lamst[LAM_LIM + l] = 0.f;
+        }
+        const int rf = 3 * npts + nlim + frank;
+        if (has_f && rf < RMAX) {  // joint friction: |lambda| <= f dt
+          E.rd[rf][0] = 1.f; E.rbP[rf] = -1 - l; E.rbN[rf] = -1;
+          E.rlam[rf] = LAM_FRIC + l;
+          E.rLam[rf] = E.lamst[LAM_FRIC + l];
+          E.grp[rf / 3].tgt[rf % 3] = 0.f; E.grp[rf / 3].lo[rf % 3] = -ffric * dt; E.grp[rf / 3].hi[rf % 3] = ffric * dt;
+        } else {
+          E.lamst[LAM_FRIC + l] = 0.f;
         }
       }
     }
@@ -1089,6 +1173,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   for (int i = l; i < 13 * 3; i += 32) E.u.out.cf[i] = (&E.cf[0][0])[i];
   __syncthreads();
   if (!valid) return;
+  if (l == 0 && E.drop != 0) S.rows_dropped[e] += E.drop;
   if (bad) {
     // non-finite recovery: keep the pre-step state, push the base below ground so the
     // termination check resets the env; count the event

@@ -19,8 +19,8 @@ MODEL_PATH = os.path.join(PKG_ROOT, "model", "xbotl_model.json")
 HG_MAX_BODIES = 16
 HG_MAX_DOF = 12
 HG_MAX_CONTACTS = 24
-HG_MAX_CAPSULES = 8
-HG_MAX_PAIRS = 8
+HG_MAX_CAPSULES = 12
+HG_MAX_PAIRS = 16
 HG_NUM_REWARDS = 22
 HG_LAMW = HG_MAX_CONTACTS * 3 + HG_MAX_PAIRS * 3 + 2 * HG_MAX_DOF
 
@@ -33,7 +33,8 @@ class HgModel(ctypes.Structure):
         ("num_bodies", i32), ("num_dof", i32), ("num_contacts", i32), ("num_foot_contacts", i32),
         ("num_leg_contacts", i32), ("num_capsules", i32), ("num_pairs", i32), ("_pad", i32),
         ("parent", i32 * HG_MAX_BODIES), ("contact_body", i32 * HG_MAX_CONTACTS),
-        ("capsule_body", i32 * HG_MAX_CAPSULES), ("pair", (i32 * 2) * HG_MAX_PAIRS),
+        ("capsule_body", i32 * HG_MAX_CAPSULES), ("capsule_kind", i32 * HG_MAX_CAPSULES),
+        ("pair", (i32 * 2) * HG_MAX_PAIRS),
         ("joint_pos", (f32 * 3) * HG_MAX_BODIES), ("joint_rot", (f32 * 9) * HG_MAX_BODIES),
         ("axis", (f32 * 3) * HG_MAX_BODIES), ("mass", f32 * HG_MAX_BODIES),
         ("com", (f32 * 3) * HG_MAX_BODIES), ("inertia", (f32 * 6) * HG_MAX_BODIES),
@@ -89,7 +90,7 @@ TENSOR_IDS = [
     "FEET_AIR_TIME", "LAST_CONTACTS", "FEET_HEIGHT", "LAST_FEET_Z", "ENV_FRICTION", "BODY_MASS",
     "PUSH_FORCE", "PUSH_TORQUE", "BASE_LIN_VEL", "BASE_ANG_VEL", "PROJ_GRAVITY", "BASE_EULER",
     "REF_DOF_POS", "ENV_ORIGINS", "EP_STATS", "CONTACT_LAMBDA", "NONFINITE", "TERRAIN_LEVEL", "TERRAIN_TYPE",
-    "EP_STATS_RING",
+    "EP_STATS_RING", "ROWS_DROPPED",
 ]
 EP_RING = 64  # HG_EP_RING
 T = {name: i for i, name in enumerate(TENSOR_IDS)}
@@ -258,7 +259,9 @@ def load_model(path=MODEL_PATH, armature=0.0, joint_friction=True, self_collisio
     joint_friction: apply the URDF's joint friction (0.1 N m on the ankles, XBot-L.urdf:1675-1677);
     or a dict {joint-name substring: friction N m} (last match wins, as the PD gain keys) that
     replaces it — the MJCF profile of scripts/sim2sim.py (frictionloss, XBot-L.xml:37-39,426).
-    self_collisions: leg-vs-leg capsule pairs (asset.self_collisions = 0 enables them, :103).
+    self_collisions: the self-collision pairs (asset.self_collisions = 0 enables them, :103):
+    leg-vs-leg capsules, hands vs the thigh / shin of their side, the base-box bottom face vs the
+    thighs.
     """
     with open(path) as f:
         js = json.load(f)
@@ -310,6 +313,7 @@ def load_model(path=MODEL_PATH, armature=0.0, joint_friction=True, self_collisio
     m.num_capsules = len(caps)
     for k, cd in enumerate(caps):
         m.capsule_body[k] = cd["body"]
+        m.capsule_kind[k] = cd.get("kind", 0)
         m.capsule_radius[k] = cd["radius"]
         for i in range(3):
             m.capsule_p0[k][i] = cd["p0"][i]

@@ -294,6 +294,9 @@ class XBotLFreeEnv(BaseTask):
         self._ep_stats = self._view(T["EP_STATS"])
         self._ep_ring = self._view(T["EP_STATS_RING"])
         self.nonfinite_count = self._view(T["NONFINITE"])
+        # constraint rows / contact points the solver's row budget dropped, per env, summed over
+        # substeps (diagnostic; 0 in normal operation)
+        self.rows_dropped = self._view(T["ROWS_DROPPED"])
 
     def _global_ids(self):
         """(offset, total): this shard's envs are global ids [offset, offset + num_envs) of total."""

@@ -257,7 +257,7 @@ def run(policy, profile="mjcf", commands=((0.4, 0.0, 0.0),), duration=10.0, envs
                    policy_dt=env.dt, sim_dt=env.sim_dt, pgs_iterations=int(env._hgcfg.pgs_iterations),
                    commands=per, falls=int(falls.sum()),
                    survived_fraction=float((falls == 0).double().mean()),
-                   fall_step=fall_step.cpu().tolist())
+                   fall_step=fall_step.cpu().tolist(), rows_dropped=int(env.rows_dropped.sum()))
     traces = {k: np.asarray(v) for k, v in tr.items()}
     if record_q:
         traces["q_all"] = torch.stack(q_all).cpu().numpy()

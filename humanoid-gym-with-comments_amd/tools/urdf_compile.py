@@ -22,7 +22,13 @@ What it does
         axial extent shrunk by the radius) for the thigh, shin and foot of each leg;
       - self-collision pairs (self_collisions = 0 enables them, humanoid_config.py:103): every
         left-leg capsule against every right-leg capsule except foot-thigh, with the contact
-        normal from the left capsule to the right one;
+        normal from the left capsule to the right one; then the shapes merged into
+        ``base_link`` against the legs: each hand (one capsule fitted to the ``*_wrist_yaw`` +
+        ``*_hand`` hulls, fixed in the base frame: the arm's parts at thigh height, z < -0.16;
+        radius = half the hull's lateral (base y) extent, the direction a thigh approaches from)
+        against the thigh and shin of its own side, and the bottom face of the base-link box against each
+        thigh (a "box-face" primitive: kind 1, p0 / p1 = the face's corner extremes, normal
+        -z of the base frame);
   * records each joint's URDF ``dynamics friction`` (0.1 N m on the four ankle joints), which the
     simulator applies as a Coulomb friction bound on the joint.
 
@@ -174,6 +180,27 @@ def compile_urdf(robot_dir):
     base_col = links["base_link"].find("collision")
     bp, _ = parse_origin(base_col.find("origin"))
     size = [float(s) for s in base_col.find("geometry").find("box").get("size").split()]
+    # base-link shapes vs the legs (the collapsed base carries the arm, hand and box shapes,
+    # XBot-L.urdf:37-42, :87-1156; PhysX filters only the jointed parent-child pairs)
+    cap_index = {(c["side"], c["part"]): k for k, c in enumerate(capsules)}
+    for side in ("left", "right"):
+        verts = []
+        for part in ("wrist_yaw", "hand"):
+            name = f"{side}_{part}_link"
+            b, T_b_l = link_body[name]
+            assert b == 0, name  # fixed joints: merged into the base
+            v = load_stl(os.path.join(robot_dir, "meshes", name + ".STL"))
+            verts.append(v @ T_b_l[:3, :3].T + T_b_l[:3, 3])
+        capsules.append(dict(body=0, part="hand", side=side, **fit_capsule(np.concatenate(verts), lateral_axis=1)))
+        h = len(capsules) - 1
+        pairs.append([h, cap_index[(side, "leg_pitch")]])
+        pairs.append([h, cap_index[(side, "knee")]])
+    capsules.append(dict(body=0, part="box_bottom", side="base", kind=1,
+                         p0=[bp[0] - size[0] / 2, bp[1] - size[1] / 2, bp[2] - size[2] / 2],
+                         p1=[bp[0] + size[0] / 2, bp[1] + size[1] / 2, bp[2] - size[2] / 2], radius=0.0))
+    box = len(capsules) - 1
+    for side in ("left", "right"):
+        pairs.append([box, cap_index[(side, "leg_pitch")]])
     for sx in (-1, 1):
         for sy in (-1, 1):
             for sz in (-1, 1):
@@ -191,16 +218,17 @@ def compile_urdf(robot_dir):
     )
 
 
-def fit_capsule(v):
+def fit_capsule(v, lateral_axis=None):
     """Capsule along the hull's principal axis (link frame): radius = mean of the two transverse
-    half-extents (along the minor principal axes), segment = the axial extent shrunk by the
-    radius at both ends (so the end caps reach the hull's axial extremes)."""
+    half-extents (along the minor principal axes) — or, with ``lateral_axis``, half the extent
+    along that frame axis — segment = the axial extent shrunk by the radius at both ends (so the
+    end caps reach the hull's axial extremes)."""
     c = v.mean(0)
     _, _, vt = np.linalg.svd(v - c, full_matrices=False)
     ax = vt[0]
     t = (v - c) @ ax
     half = [0.5 * (np.ptp((v - c) @ vt[k])) for k in (1, 2)]
-    r = float(np.mean(half))
+    r = float(np.mean(half)) if lateral_axis is None else float(0.5 * np.ptp(v[:, lateral_axis]))
     lo, hi = t.min() + r, t.max() - r
     if hi < lo:
         lo = hi = 0.5 * (t.min() + t.max())

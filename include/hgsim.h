@@ -37,8 +37,8 @@ extern "C" {
 #define HG_MAX_BODIES 16
 #define HG_MAX_DOF 12
 #define HG_MAX_CONTACTS 24  /* ground contact candidates (points / spheres) */
-#define HG_MAX_CAPSULES 8
-#define HG_MAX_PAIRS 8      /* self-collision capsule pairs */
+#define HG_MAX_CAPSULES 12
+#define HG_MAX_PAIRS 16     /* self-collision capsule pairs */
 #define HG_NUM_REWARDS 22
 #define HG_MAX_TENSORS 32
 /* solver warm-start impulses per env: 3 per ground candidate, 3 per pair, joint limits, joint friction */
@@ -50,8 +50,12 @@ extern "C" {
  * Collision model (BUILD-DEFINED fits of the URDF collision meshes): ground contact candidates
  * are points (radius 0: sole corners, base-box corners) or spheres (capsule end caps); capsules
  * collide pairwise (self-collision, humanoid_config.py:103) with the normal from capsule
- * pair[p][0] to pair[p][1].  Contact priority (the solver keeps at most 9 contact points per env):
- * ground candidates [0, num_leg_contacts), then the pairs, then the remaining candidates. */
+ * pair[p][0] to pair[p][1]; a capsule of kind 1 is the bottom face of the base-link box
+ * (capsule_p0 / capsule_p1 = the face's corner extremes in the base frame, normal -z of the
+ * base; it is only ever pair[p][0]), colliding with the closer end sphere of the other capsule.
+ * Contact priority (the solver keeps at most 9 contact points per env): ground candidates
+ * [0, num_leg_contacts), then the pairs, then the remaining candidates; num_contacts + num_pairs
+ * <= 64 (detection runs one candidate per lane, two rounds over the env's 32 lanes). */
 typedef struct hg_model {
   int32_t num_bodies;
   int32_t num_dof;
@@ -64,6 +68,7 @@ typedef struct hg_model {
   int32_t parent[HG_MAX_BODIES];
   int32_t contact_body[HG_MAX_CONTACTS];
   int32_t capsule_body[HG_MAX_CAPSULES];
+  int32_t capsule_kind[HG_MAX_CAPSULES];  /* 0 capsule, 1 base-box bottom face */
   int32_t pair[HG_MAX_PAIRS][2];
   float joint_pos[HG_MAX_BODIES][3];   /* joint origin in parent-body frame */
   float joint_rot[HG_MAX_BODIES][9];   /* parent-body -> joint frame rotation, row-major */
@@ -174,6 +179,7 @@ enum hg_tensor_id {
   HG_T_EP_STATS_RING,    /* [HG_EP_RING, 24] EP_STATS as left by each post/reset launch, launch k in row
                             k % HG_EP_RING (hg_ep_stats_slot): the per-step extras["episode"] snapshot
                             without a copy launch */
+  HG_T_ROWS_DROPPED,     /* [N] int32: constraint rows / contact points the row budget dropped, summed over substeps */
   HG_T_COUNT
 };
 

@@ -28,10 +28,13 @@
  *   6. nu* = nu + dt M^-1 (tau - h),
  *   7. constraint rows, at most 32 per env, in this order:
  *        contacts (normal + 2 tangents each, at most 9 points, in priority order: foot-sole points,
- *        shin and thigh capsule end spheres vs the ground, then the leg-vs-leg capsule pairs
- *        (self-collision, humanoid_config.py:103), then the base-box corners; speculative within
- *        contact_offset, Baumgarte-corrected below zero), then the joint friction rows (URDF
- *        dynamics friction, 0.1 N m on the ankles: |lambda| <= f dt), then joint limits;
+ *        shin and thigh capsule end spheres vs the ground, then the self-collision pairs
+ *        (humanoid_config.py:103: leg-vs-leg capsules, each hand vs its side's thigh and shin, the
+ *        base-box bottom face vs the thighs), then the base-box corners; speculative within
+ *        contact_offset, Baumgarte-corrected below zero), then joint limits, then the joint
+ *        friction rows (URDF dynamics friction, 0.1 N m on the ankles: |lambda| <= f dt; larger
+ *        bounds first, then the joint within its leg, left before right); rows past the budget
+ *        (and contact points past 9) are dropped and counted;
  *      solved by projected Gauss-Seidel on impulses with Y = M^-1 J^T (warm-started from the
  *      previous substep); friction cone |lambda_t| <= mu lambda_n with mu = mean(env friction,
  *      ground friction) against the ground (PhysX average combine) and the env friction between
@@ -74,7 +77,7 @@ typedef double real;
 typedef struct {
   int nb, nc, nfoot, nleg, ncap, npair;
   int parent[NB];
-  int cbody[NC_MAX], capbody[NCAP], pair[NP_MAX][2];
+  int cbody[NC_MAX], capbody[NCAP], capkind[NCAP], pair[NP_MAX][2];
   real jpos[NB][3], jrot[NB][9], axis[NB][3];
   real mass[NB], com[NB][3], inertia[NB][6], armature[NB], lower[NB], upper[NB], jfric[NB];
   real cpos[NC_MAX][3], crad[NC_MAX];
@@ -164,6 +167,7 @@ static void load_model(const hg_model* hm, Model* m) {
   }
   for (int k = 0; k < NCAP; k++) {
     m->capbody[k] = hm->capsule_body[k];
+    m->capkind[k] = hm->capsule_kind[k];
     m->caprad[k] = hm->capsule_radius[k];
     for (int i = 0; i < 3; i++) { m->cap0[k][i] = hm->capsule_p0[k][i]; m->cap1[k][i] = hm->capsule_p1[k][i]; }
   }
@@ -421,7 +425,7 @@ typedef struct {
 
 static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* root, real* q,
                     real* qd, real* lamst, const real* act, real* tau, real mass0, real fric, real* cf_out,
-                    int* nonfinite) {
+                    int* nonfinite, int* dropped) {
   const real dt = cfg->sim_dt;
   /* 1. PD torques; implicit damping on the joints whose torque is not clipped */
   real madd[ND];
@@ -486,12 +490,37 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
       mat3_vec(k.Rb[ba], m->cap0[ca], a0); mat3_vec(k.Rb[ba], m->cap1[ca], a1);
       mat3_vec(k.Rb[bb], m->cap0[cb], b0); mat3_vec(k.Rb[bb], m->cap1[cb], b1);
       for (int i = 0; i < 3; i++) { a0[i] += k.o[ba][i]; a1[i] += k.o[ba][i]; b0[i] += k.o[bb][i]; b1[i] += k.o[bb][i]; }
-      seg_seg(a0, a1, b0, b1, pa, pb);
-      for (int i = 0; i < 3; i++) dv[i] = pb[i] - pa[i];
-      const real dist = sqrt(v3_dot(dv, dv));
-      if (dist > R(1e-9)) for (int i = 0; i < 3; i++) ct->n[i] = dv[i] / dist;
-      else { ct->n[0] = 0; ct->n[1] = -1; ct->n[2] = 0; }  /* left -> right is -y in the base frame */
-      const real ra = m->caprad[ca], rb = m->caprad[cb];
+      const real rb = m->caprad[cb];
+      real ra = m->caprad[ca], dist;
+      if (m->capkind[ca] == 1) {
+        /* base-box bottom face (base frame: z = cap0.z over [cap0.x, cap1.x] x [cap0.y, cap1.y],
+           outward normal -z) vs the end sphere of capsule cb that lies closer to it */
+        const real* R0 = k.Rb[0];
+        real h[2], xy[2][2];
+        const real* ends[2] = {b0, b1};
+        for (int s = 0; s < 2; s++) {  /* end sphere in the base frame: R0^T x */
+          const real* x = ends[s];
+          xy[s][0] = R0[0] * x[0] + R0[3] * x[1] + R0[6] * x[2];
+          xy[s][1] = R0[1] * x[0] + R0[4] * x[1] + R0[7] * x[2];
+          h[s] = m->cap0[ca][2] - (R0[2] * x[0] + R0[5] * x[1] + R0[8] * x[2]);  /* depth below the face */
+        }
+        const int s = h[1] < h[0] ? 1 : 0;
+        const int inside = xy[s][0] >= m->cap0[ca][0] && xy[s][0] <= m->cap1[ca][0] &&
+                           xy[s][1] >= m->cap0[ca][1] && xy[s][1] <= m->cap1[ca][1];
+        for (int i = 0; i < 3; i++) {
+          ct->n[i] = -R0[i * 3 + 2];
+          pb[i] = ends[s][i];
+          pa[i] = ends[s][i] - h[s] * ct->n[i];
+        }
+        ra = 0;
+        dist = inside ? h[s] : R(1e3);
+      } else {
+        seg_seg(a0, a1, b0, b1, pa, pb);
+        for (int i = 0; i < 3; i++) dv[i] = pb[i] - pa[i];
+        dist = sqrt(v3_dot(dv, dv));
+        if (dist > R(1e-9)) for (int i = 0; i < 3; i++) ct->n[i] = dv[i] / dist;
+        else { ct->n[0] = 0; ct->n[1] = -1; ct->n[2] = 0; }  /* left -> right is -y in the base frame */
+      }
       ct->phi = dist - ra - rb;
       for (int i = 0; i < 3; i++) { ct->xpos[i] = pb[i] - rb * ct->n[i]; ct->xneg[i] = pa[i] + ra * ct->n[i]; }
       ct->bpos = bb; ct->bneg = ba;
@@ -500,11 +529,12 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
       ct->active = ct->phi < off_c;
     }
   }
-  /* ---- rows: contacts (<= MAX_CONTACT_POINTS), joint friction, joint limits ---- */
+  /* ---- rows: contacts (<= MAX_CONTACT_POINTS), joint limits, joint friction; the rest dropped ---- */
   static __thread Row rows[MAX_ROWS];
   int nr = 0, npts = 0;
   for (int ci = 0; ci < ncand; ci++) {
     Contact* ct = &cand[ci];
+    if (ct->active && npts >= MAX_CONTACT_POINTS) *dropped += 3;
     if (!ct->active || npts >= MAX_CONTACT_POINTS) { for (int d = 0; d < 3; d++) lamst[ct->lam_base + d] = 0; continue; }
     npts++;
     real t1[3], t2[3];
@@ -523,16 +553,6 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
       r->lam = lamst[r->lam_idx];
     }
   }
-  for (int j = 0; j < ND; j++) {
-    const real f = m->jfric[j + 1];
-    if (!(f > 0) || nr >= MAX_ROWS) { lamst[LAM_FRIC + j] = 0; continue; }
-    Row* r = &rows[nr++];
-    memset(r, 0, sizeof(*r));
-    r->kind = 4; r->lam_idx = LAM_FRIC + j; r->bpos = r->bneg = -1;
-    r->J[6 + j] = 1;
-    r->lo = -f * dt; r->hi = f * dt;
-    r->lam = lamst[r->lam_idx];
-  }
   const real lim_margin = R(0.01);
   for (int j = 0; j < ND; j++) {
     real glo = q[j] - m->lower[j + 1], ghi = m->upper[j + 1] - q[j];
@@ -540,12 +560,35 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
     if (glo < lim_margin) { sgn = 1; gap = glo; }
     else if (ghi < lim_margin) { sgn = -1; gap = ghi; }
     else { lamst[LAM_LIM + j] = 0; continue; }
-    if (nr >= MAX_ROWS) { lamst[LAM_LIM + j] = 0; continue; }
+    if (nr >= MAX_ROWS) { lamst[LAM_LIM + j] = 0; *dropped += 1; continue; }
     Row* r = &rows[nr++];
     memset(r, 0, sizeof(*r));
     r->kind = 3; r->lam_idx = LAM_LIM + j; r->bpos = r->bneg = -1;
     r->J[6 + j] = sgn;
     r->target = gap >= 0 ? -gap / dt : fmin(-beta * gap / dt, vmax);
+    r->lam = lamst[r->lam_idx];
+  }
+  /* friction rows: larger bounds first, then the joint within its leg, left before right */
+  int forder[ND];
+  for (int j = 0; j < ND; j++) forder[j] = j;
+  for (int a = 1; a < ND; a++)
+    for (int b = a; b > 0; b--) {
+      const int x = forder[b - 1], y = forder[b];
+      const real fx = m->jfric[x + 1], fy = m->jfric[y + 1];
+      const int swap = fy > fx || (fy == fx && (y % 6 < x % 6 || (y % 6 == x % 6 && y < x)));
+      if (!swap) break;
+      forder[b - 1] = y; forder[b] = x;
+    }
+  for (int jj = 0; jj < ND; jj++) {
+    const int j = forder[jj];
+    const real f = m->jfric[j + 1];
+    if (!(f > 0)) { lamst[LAM_FRIC + j] = 0; continue; }
+    if (nr >= MAX_ROWS) { lamst[LAM_FRIC + j] = 0; *dropped += 1; continue; }
+    Row* r = &rows[nr++];
+    memset(r, 0, sizeof(*r));
+    r->kind = 4; r->lam_idx = LAM_FRIC + j; r->bpos = r->bneg = -1;
+    r->J[6 + j] = 1;
+    r->lo = -f * dt; r->hi = f * dt;
     r->lam = lamst[r->lam_idx];
   }
   for (int r = 0; r < nr; r++) {
@@ -640,7 +683,8 @@ static void rigid_states(const Model* m, const real* root, const real* q, const 
  *   root[n][13], q[n][12], qd[n][12], lam[n][LAMW] (in/out), actions[n][12] (already
  *   delayed/noised/clipped as in humanoid_env.py:620-635), mass0[n] (base mass after DR),
  *   fric[n];  outputs torques[n][12] (last substep), contact[n][13][3], rigid[n][13][13],
- *   nonfinite[n].  Returns 0. */
+ *   nonfinite[n], dropped[n] (+= rows / contact points over the budget, summed over the
+ *   substeps).  Returns 0. */
 #ifdef REF_FLOAT
 #define API(name) name##_f32
 #else
@@ -648,7 +692,8 @@ static void rigid_states(const Model* m, const real* root, const real* q, const 
 #endif
 int API(ref_step)(const hg_cfg* cfg, const hg_model* hm, const int16_t* hf, int n, real* root,
                   real* q, real* qd, real* lam, const real* actions, const real* mass0,
-                  const real* fric, real* torques, real* contact, real* rigid, int32_t* nonfinite) {
+                  const real* fric, real* torques, real* contact, real* rigid, int32_t* nonfinite,
+                  int32_t* dropped) {
   Model m;
   load_model(hm, &m);
 #pragma omp parallel for schedule(static)
@@ -658,10 +703,11 @@ int API(ref_step)(const hg_cfg* cfg, const hg_model* hm, const int16_t* hf, int 
     real* qde = qd + (size_t)e * ND;
     const real* ae = actions + (size_t)e * ND;
     real tau[ND];
-    int bad = 0;
+    int bad = 0, drop = 0;
     for (int s = 0; s < cfg->decimation && !bad; s++)
       substep(cfg, &m, hf, re, qe, qde, lam + (size_t)e * LAMW, ae, tau, mass0[e], fric[e],
-              contact + (size_t)e * NB * 3, &bad);
+              contact + (size_t)e * NB * 3, &bad, &drop);
+    dropped[e] += drop;
     for (int j = 0; j < ND; j++) torques[(size_t)e * ND + j] = tau[j];
     nonfinite[e] = bad;
     rigid_states(&m, re, qe, qde, mass0[e], rigid + (size_t)e * NB * 13);

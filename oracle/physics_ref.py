@@ -55,6 +55,7 @@ class RefSim:
         self.contact = np.zeros((n, 13, 3), self.dt)
         self.rigid = np.zeros((n, 13, 13), self.dt)
         self.nonfinite = np.zeros(n, np.int32)
+        self.dropped = np.zeros(n, np.int32)   # rows / contact points over the budget (cumulative)
         self.hf = None if heightfield is None else np.ascontiguousarray(heightfield, np.int16)
 
     def step(self, actions):
@@ -63,7 +64,7 @@ class RefSim:
         hf = None if self.hf is None else _p(self.hf)
         self.fn(ctypes.byref(self.cfg), ctypes.byref(self.model), hf, ctypes.c_int(self.n), _p(self.root),
                 _p(self.q), _p(self.qd), _p(self.lam), _p(a), _p(self.mass0), _p(self.fric), _p(self.torques),
-                _p(self.contact), _p(self.rigid), _p(self.nonfinite))
+                _p(self.contact), _p(self.rigid), _p(self.nonfinite), _p(self.dropped))
 
 
 def dynamics(model, root, q, qd, mass0=None, gz=-9.81):

@@ -299,7 +299,7 @@ def initial_state(cfg, env_origins, body_mass, frictions):
     return S, obs, priv
 
 
-LAMBDA_WIDTH = 24 * 3 + 8 * 3 + 2 * 12  # HG_LAMW (include/hgsim.h): solver warm-start slots per env; only their zeroing on reset matters here
+LAMBDA_WIDTH = 24 * 3 + 16 * 3 + 2 * 12  # HG_LAMW (include/hgsim.h): solver warm-start slots per env; only their zeroing on reset matters here
 
 
 def post(cfg, S, counter, hist_obs, hist_priv, draws=None, extras=None):

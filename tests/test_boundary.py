@@ -65,15 +65,27 @@ def test_struct_layouts_match_header(tmp_path):
 def test_model_table():
     m, js = N.load_model()
     assert m.num_bodies == 13 and m.num_dof == 12 and m.num_contacts == 24 and m.num_foot_contacts == 8
-    assert m.num_leg_contacts == 16 and m.num_capsules == 6 and m.num_pairs == 7
+    assert m.num_leg_contacts == 16 and m.num_capsules == 9 and m.num_pairs == 13
+    assert m.num_contacts + m.num_pairs == 37  # > 32: K_step's detection runs its second round
     # ankle pitch / roll joints carry the URDF's 0.1 N m friction; the asset armature is 0
     assert [round(m.joint_friction[b], 6) for b in range(1, 13)] == [0, 0, 0, 0, 0.1, 0.1] * 2
     assert all(m.armature[b] == 0.0 for b in range(13))
-    # pairs: left capsule -> right capsule, no foot-thigh pair
     caps = js["capsules"]
-    for a, b in js["pairs"]:
+    # pairs 0..6: left leg capsule -> right leg capsule, no foot-thigh pair
+    for a, b in js["pairs"][:7]:
         assert caps[a]["side"] == "left" and caps[b]["side"] == "right"
         assert {caps[a]["part"], caps[b]["part"]} != {"leg_pitch", "ankle_roll"}
+    # then the base-link shapes (body 0) vs the legs: each hand vs its side's thigh and shin, the
+    # base-box bottom face (kind 1) vs each thigh; the base shape is always the pair's first
+    base_pairs = [(caps[a]["part"], caps[a]["side"], caps[b]["part"], caps[b]["side"]) for a, b in js["pairs"][7:]]
+    assert base_pairs == [("hand", "left", "leg_pitch", "left"), ("hand", "left", "knee", "left"),
+                          ("hand", "right", "leg_pitch", "right"), ("hand", "right", "knee", "right"),
+                          ("box_bottom", "base", "leg_pitch", "left"), ("box_bottom", "base", "leg_pitch", "right")]
+    for a, _ in js["pairs"][7:]:
+        assert caps[a]["body"] == 0
+    assert [m.capsule_kind[k] for k in range(9)] == [0] * 8 + [1]
+    # the box face is the base-link box's bottom (XBot-L.urdf:37-42: 0.4 m cube centred 0.1 m up)
+    assert caps[8]["p0"] == [-0.2, -0.2, -0.1] and caps[8]["p1"] == [0.2, 0.2, -0.1]
     assert abs(js["total_mass"] - 53.036) < 0.01
     bodies = [b["name"] for b in js["bodies"]]
     assert bodies.index("left_ankle_roll_link") == 6 and bodies.index("right_ankle_roll_link") == 12

@@ -275,7 +275,7 @@ def _step_only(env, actions, counter):
     torch.cuda.synchronize()
 
 
-def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), scale=0.5):
+def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), scale=0.5, actions=None):
     """One K_step (prologue + 10 substeps + rigid states) from the env's current state vs the C
     reference simulator (f64, f32) on the identical state and preprocessed actions.  Stated fp32
     tolerance: 20 x the larger of the CPU f32-vs-f64 gap and the local conditioning spread of the
@@ -284,8 +284,10 @@ def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), s
     import pipeline_ref as PR
     S, _, _ = snapshot(env)
     cfg = _oracle_cfg(env)
-    actions = torch.randn(env.num_envs, 12, device="cuda:0") * scale
+    if actions is None:
+        actions = torch.randn(env.num_envs, 12, device="cuda:0") * scale
     a_ref = PR.preprocess_actions(cfg, actions.cpu().numpy(), S["actions"], counter)
+    dropped0 = env.rows_dropped.clone()
     _step_only(env, actions, counter)
     g = lambda t: t.detach().cpu().numpy()  # noqa: E731
     np.testing.assert_allclose(g(env.actions), a_ref, rtol=1e-5, atol=1e-6)
@@ -304,6 +306,8 @@ def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), s
                            for ix in np.argwhere(bad)[:6])
         assert not bad.any(), f"{name}: {bad.sum()} mismatches, max err {np.abs(x - a64).max()}: {detail}"
     assert not r64.nonfinite.any() and not g(env.nonfinite_count).any()
+    # rows / contact points over the budget: the same count per env
+    np.testing.assert_array_equal(g(env.rows_dropped - dropped0), r64.dropped)
     return r64
 
 
@@ -338,6 +342,59 @@ def test_step_and_post_parity_4096_envs(which, request):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
     _step_parity(env, 131)
     _post_parity(env, steps=0)
+
+
+def test_hand_thigh_self_collision_parity():
+    """Base-link shapes vs the legs (humanoid_config.py:103, XBot-L.urdf:37-42 +
+    the merged arm / hand shapes): fixed base, each hip rolled 0.34 rad outward so the thigh sits
+    in its hand capsule (contact at ~0.31 rad).  K_step vs the oracle at the stated tolerance, the
+    hand-thigh pair impulse positive in both, forces on base and thigh equal and opposite."""
+    _need_gpu()
+    from humanoid import _native as N
+    env = _make_env(N_ENVS, asset__fix_base_link=True)
+    js = env._model_js if hasattr(env, "_model_js") else N.load_model()[1]
+    caps, pairs = js["capsules"], js["pairs"]
+    hp = {caps[a]["side"]: p for p, (a, b) in enumerate(pairs) if caps[a]["part"] == "hand" and caps[b]["part"] == "leg_pitch"}
+    half = N_ENVS // 2
+    env.dof_pos[:half, 0] = 0.34
+    env.dof_pos[half:, 6] = -0.34
+    act = env.dof_pos / env.cfg.control.action_scale
+    r64 = _step_parity(env, 55, actions=act.contiguous())
+    lam = env._view(N.T["CONTACT_LAMBDA"]).cpu().numpy()
+    lp = N.HG_MAX_CONTACTS * 3
+    for rows, side in ((slice(0, half), "left"), (slice(half, N_ENVS), "right")):
+        k = lp + 3 * hp[side]
+        assert (lam[rows, k] > 0).all() and (r64.lam[rows, k] > 0).all(), side
+    cf = env.contact_forces.cpu().numpy()
+    np.testing.assert_allclose(cf[:half, 0], -cf[:half, 3], rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(cf[half:, 0], -cf[half:, 9], rtol=1e-4, atol=1e-3)
+
+
+def test_row_budget_parity_standing_mjcf_friction():
+    """Row budget order on the GPU: the MJCF friction profile (12 friction rows) on
+    robots standing on both soles (24 rows) with both hip yaws 0.01 rad past their lower limit:
+    38 rows wanted, 6 dropped per substep, and they are the 0.01 N m hip-yaw / hip-pitch / knee
+    friction rows of both legs — the same counts and the same kept / cleared warm-start slots as
+    the oracle, env for env."""
+    _need_gpu()
+    from humanoid import _native as N
+    from humanoid.scripts import sim2sim as S2
+    env = S2.make_env("mjcf", N_ENVS, 5.0)
+    for _ in range(80):
+        S2.step_direct(env, torch.zeros(N_ENVS, 12, device="cuda:0"))
+    torch.cuda.synchronize()
+    lo = torch.tensor([env._model.lower[b] for b in range(1, 13)], device="cuda:0")
+    env.dof_pos[:, [1, 7]] = lo[[1, 7]] - 0.01
+    act = torch.zeros(N_ENVS, 12, device="cuda:0")
+    act[:, [1, 7]] = (lo[[1, 7]] - 0.01) / env.cfg.control.action_scale
+    env.actions[:] = act
+    r64 = _step_parity(env, 300, fields=("q", "qd", "root", "torques"), actions=act)
+    assert (r64.dropped == 60).all()
+    lam = env._view(N.T["CONTACT_LAMBDA"]).cpu().numpy()
+    lf = (N.HG_MAX_CONTACTS + N.HG_MAX_PAIRS) * 3 + N.HG_MAX_DOF
+    for L in (lam, r64.lam):
+        assert (L[:, [lf + j for j in (4, 10, 5, 11, 0, 6)]] != 0).all()
+        assert (L[:, [lf + j for j in (1, 7, 2, 8, 3, 9)]] == 0).all()
 
 
 def test_nonfinite_guard_resets_and_counts():
@@ -1341,6 +1398,9 @@ def test_sim2sim_mjcf_profile(tmp_path):
                         "0.4", "--envs_per_command", "2", "--out", str(out)])
     js = json.load(open(out / "sim2sim.json"))
     assert js["profile"] == "mjcf" and js["pgs_iterations"] == 50 and len(js["commands"]) == 3
+    # rows over the solver budget are counted (double support on the MJCF profile wants 24 contact
+    # + 12 friction rows: the 0.01 N m pitch / knee friction rows of both legs are the ones dropped)
+    assert isinstance(js["rows_dropped"], int) and js["rows_dropped"] >= 0
     assert js == json.loads(json.dumps(summary))
     for c in js["commands"]:
         assert np.isfinite(c["lin_vel_error"]) and np.isfinite(c["yaw_rate_error"])

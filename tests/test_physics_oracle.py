@@ -274,3 +274,73 @@ def test_armature_zero_stands_stably():
         sim.step(np.zeros((n, 12)))
     assert sim.nonfinite[0] == 0
     assert np.abs(sim.qd).max() < 0.2
+
+
+LAM_PAIR = N.HG_MAX_CONTACTS * 3
+LAM_LIM = LAM_PAIR + N.HG_MAX_PAIRS * 3
+LAM_FRIC = LAM_LIM + N.HG_MAX_DOF
+
+
+def test_hand_thigh_contact_stops_hip_roll():
+    """Base-link shapes vs the legs (self-collision, humanoid_config.py:103): with the base fixed in
+    the air and the hip-roll PD target at 0.6 rad outward, each thigh swings into its hand capsule
+    (merged into base_link, XBot-L.urdf:728-742, :2979-2993) and stops there (0.2-0.36 rad); the pair
+    impulse is positive and its forces on the base and the thigh are equal and opposite."""
+    m, js = N.load_model()
+    caps, pairs = js["capsules"], js["pairs"]
+    hand_thigh = {caps[a]["side"]: p for p, (a, b) in enumerate(pairs)
+                  if caps[a]["part"] == "hand" and caps[b]["part"] == "leg_pitch"}
+    n = 2
+    cfg = make_cfg(n, fixed=True)
+    for j in range(12):
+        cfg.kp[j], cfg.kd[j] = [200, 200, 350, 350, 15, 15][j % 6], 10.0
+    cfg.decimation = 10
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 3.0
+    act = np.zeros((n, 12))
+    act[0, 0] = 0.6 / 0.25     # left hip roll outward (+)
+    act[1, 6] = -0.6 / 0.25    # right hip roll outward (-)
+    for _ in range(30):
+        sim.step(act)
+    assert abs(sim.q[0, 0]) < 0.36 and abs(sim.q[1, 6]) < 0.36
+    assert abs(sim.q[0, 0]) > 0.2 and abs(sim.q[1, 6]) > 0.2
+    for e, side, thigh in ((0, "left", 3), (1, "right", 9)):
+        p = hand_thigh[side]
+        assert sim.lam[e, LAM_PAIR + 3 * p] > 0.0, side
+        f = sim.contact[e]
+        assert np.linalg.norm(f[thigh]) > 50.0
+        np.testing.assert_allclose(f[0], -f[thigh], atol=1e-6 * np.abs(f[thigh]).max())
+    assert (sim.dropped == 0).all() and (sim.nonfinite == 0).all()
+
+
+def test_row_budget_keeps_joint_limits_before_friction():
+    """Row budget (32 rows: <= 9 contact points = 27 rows, then joint limits, then the joint
+    friction rows).  The robot stands on both soles (8 points = 24 rows) with friction
+    on all 12 joints (the MJCF profile's frictionloss) and both hip-yaw joints 0.01 rad past their
+    lower limit: 24 + 2 limit rows + 12 friction rows = 38 wanted, so 6 rows are dropped per
+    substep, never a joint limit, and they are the friction rows of smallest bound taken from both
+    legs alike: the 0.05 N m ankle rows and the hip-roll rows are kept, the 0.01 N m hip-yaw /
+    hip-pitch / knee rows of BOTH legs are dropped (warm-start slots cleared).  (Limits after
+    friction in joint order, round 2, dropped both limits and the whole right leg's friction.)"""
+    m, js = N.load_model(joint_friction={"joint": 0.01, "ankle": 0.05})
+    n = 1
+    cfg = make_cfg(n)
+    for j in range(12):
+        cfg.kp[j], cfg.kd[j] = [200, 200, 350, 350, 15, 15][j % 6], 10.0
+    cfg.decimation = 10
+    sim = P.RefSim(cfg, m, n)
+    sim.root[:, 2] = 0.87
+    for _ in range(80):                      # settle on both feet
+        sim.step(np.zeros((n, 12)))
+    assert sim.dropped[0] > 0                # 24 + 12 friction rows: the budget already overflows
+    lo = np.array([m.lower[b] for b in range(1, 13)])
+    sim.q[0, [1, 7]] = lo[[1, 7]] - 0.01     # hip yaw past its limit: the foot turns about z, the
+    act = np.zeros((n, 12))                  # soles stay on the ground
+    act[0, [1, 7]] = (lo[[1, 7]] - 0.01) / 0.25
+    cfg.decimation = 1
+    before = int(sim.dropped[0])
+    sim.step(act)
+    assert int(sim.dropped[0]) - before == 6
+    fr = sim.lam[0, LAM_FRIC:LAM_FRIC + 12]
+    assert (fr[[4, 10, 5, 11, 0, 6]] != 0).all() and (fr[[1, 7, 2, 8, 3, 9]] == 0).all()
+    assert sim.nonfinite[0] == 0
