@@ -4,8 +4,13 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
-  > gpurun_out/pytest_gpu.log 2>&1
+if [ -n "$PYTEST_K" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+    -k "$PYTEST_K" > gpurun_out/pytest_gpu.log 2>&1
+else
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+    > gpurun_out/pytest_gpu.log 2>&1
+fi
 rc=$?
 echo "pytest rc=$rc"
 grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_gpu.log | grep -v PASSED | head -30
