@@ -59,11 +59,14 @@ MJCF_PROFILE = dict(
 )
 
 
-def make_cfg(profile, num_envs, duration):
+def make_cfg(profile, num_envs, duration, self_collisions=True):
     """XBotLCfg for a sim2sim run: fixed commands, no randomisation/noise/pushes, the profile's
-    physics parameters (see the module docstring)."""
+    physics parameters (see the module docstring).  self_collisions=False drops every
+    self-collision pair (asset.self_collisions = 1; ablation runs only)."""
     from humanoid.envs import XBotLCfg
     cfg = XBotLCfg()
+    if not self_collisions:
+        cfg.asset.self_collisions = 1
     cfg.env.num_envs = num_envs
     cfg.env.episode_length_s = duration + 1.0
     cfg.terrain.mesh_type = "plane"
@@ -87,10 +90,10 @@ def make_cfg(profile, num_envs, duration):
     return cfg
 
 
-def make_env(profile, num_envs, duration, device="cuda:0"):
+def make_env(profile, num_envs, duration, device="cuda:0", self_collisions=True):
     from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
     from humanoid.utils.helpers import SimParams
-    cfg = make_cfg(profile, num_envs, duration)
+    cfg = make_cfg(profile, num_envs, duration, self_collisions)
     env = XBotLFreeEnv(cfg, SimParams(), "hg_sim", device, True)
     if profile == "mjcf":
         p = MJCF_PROFILE

@@ -75,7 +75,7 @@ class Sim2SimRef:
 
     def __init__(self, hc, model, policy, root, q, qd, mass0, fric, cmds, precision="f64", cycle_time=0.64,
                  obs_scales=(2.0, 1.0, 1.0, 0.05), clip_obs=18.0, clip_actions=18.0, frame_stack=15,
-                 default_dof_pos=None, lam=None):
+                 default_dof_pos=None, lam=None, cause_slots=None):
         n = root.shape[0]
         self.n, self.hc, self.policy = n, hc, policy
         self.sim = P.RefSim(hc, model, n, precision)
@@ -96,6 +96,10 @@ class Sim2SimRef:
         self.err_w = np.zeros(n)
         self.alive_steps = np.zeros(n)
         self.k = 0
+        # fall cause (which contacts put force on the base at the terminating step):
+        # {name: warm-start impulse slots}, e.g. base-box corners vs ground, hand / box pairs
+        self.cause_slots = cause_slots or {}
+        self.fall_cause = np.full(n, "", dtype=object)
 
     def frame(self):
         s = self.sim
@@ -123,6 +127,9 @@ class Sim2SimRef:
         fell = (np.linalg.norm(s.contact[:, 0, :], axis=1) > 1.0) | (s.nonfinite != 0)
         new = fell & self.alive
         self.fall_step[new] = self.k
+        for e in np.nonzero(new)[0]:
+            self.fall_cause[e] = "+".join(name for name, slots in self.cause_slots.items()
+                                          if (s.lam[e, slots] > 0).any()) or "other"
         self.alive &= ~fell
         quat = s.root[:, 3:7].astype(np.float64)
         vb = quat_rotate_inverse(quat, s.root[:, 7:10].astype(np.float64))
@@ -140,4 +147,5 @@ class Sim2SimRef:
     def summary(self):
         a = np.maximum(self.alive_steps, 1.0)
         return dict(fell=(self.fall_step >= 0), fall_step=self.fall_step.copy(), lin_vel_error=self.err_v / a,
-                    yaw_rate_error=self.err_w / a, survival_s=self.alive_steps * self.dt)
+                    yaw_rate_error=self.err_w / a, survival_s=self.alive_steps * self.dt,
+                    fall_cause=list(self.fall_cause))

@@ -27,7 +27,21 @@ FIXTURE = os.path.join(REPO, "tests", "golden", "onnx_actor.npz")
 COMMANDS = ((-0.25, 0.0, 0.0), (0.0, 0.0, 0.0), (0.3, 0.0, 0.0), (0.5, 0.0, 0.0))
 
 
-def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0, ensemble=3, device="cuda:0"):
+def cause_slots(js, model):
+    """Warm-start impulse slots of the contacts that put force on the base link: base-box corners
+    vs the ground, hand capsules vs the thighs / shins, the box bottom face vs the thighs."""
+    from humanoid import _native as N
+    lp = N.HG_MAX_CONTACTS * 3
+    corners = [3 * c for c, cd in enumerate(js["contacts"]) if cd["body"] == 0]
+    caps = js["capsules"]
+    pairs = js["pairs"][:model.num_pairs]
+    hand = [lp + 3 * p for p, (a, b) in enumerate(pairs) if caps[a]["part"] == "hand"]
+    box = [lp + 3 * p for p, (a, b) in enumerate(pairs) if caps[a]["part"] == "box_bottom"]
+    return {"base_ground": corners, "hand_leg": hand, "box_thigh": box}
+
+
+def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0, ensemble=3, device="cuda:0",
+            self_collisions=True):
     """GPU sim2sim and the CPU oracle (f64, plus an fp32 ensemble as the divergence yardstick)
     from the GPU env's initial state.  Returns a dict of numpy arrays / numbers."""
     import torch
@@ -38,13 +52,14 @@ def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0,
     cmds = np.asarray(commands, np.float32).reshape(-1, 3)
     n = len(cmds) * envs_per_command
     steps = int(round(duration / 0.01))
-    env = S2.make_env(profile, n, duration, device)
+    env = S2.make_env(profile, n, duration, device, self_collisions=self_collisions)
     torch.cuda.synchronize()
     g = lambda t: t.detach().cpu().numpy().copy()  # noqa: E731
     init = dict(root=g(env.root_states), q=g(env.dof_pos), qd=g(env.dof_vel), lam=g(env._view(N.T["CONTACT_LAMBDA"])),
                 mass=g(env.body_mass)[:, 0], fric=g(env.env_frictions)[:, 0])
     hc, model = env._hgcfg, env._model
     cyc = env.cfg.rewards.cycle_time
+    slots = cause_slots(env._model_js, model)
     summary, traces = S2.run(S2.mlp_from_weights(W).to(device).eval(), profile, cmds, duration, envs_per_command,
                              device, env=env, record_q=True)
     q_gpu = traces["q_all"]
@@ -58,7 +73,7 @@ def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0,
             qd = qd * (1 + pert * rng.standard_normal(qd.shape))
         dt = np.float64 if prec == "f64" else np.float32
         sim = SR.Sim2SimRef(hc, model, SR.mlp(W, dt), root, q, qd, init["mass"], init["fric"], per_cmd,
-                            precision=prec, cycle_time=cyc, lam=init["lam"])
+                            precision=prec, cycle_time=cyc, lam=init["lam"], cause_slots=slots)
         qs = []
         for _ in range(steps):
             sim.step()
@@ -93,10 +108,12 @@ def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0,
         return out
     gpu_lin = np.array([c["lin_vel_error"] for c in summary["commands"] for _ in range(envs_per_command)])
     gpu_yaw = np.array([c["yaw_rate_error"] for c in summary["commands"] for _ in range(envs_per_command)])
-    return dict(profile=profile, envs=n, steps=steps, duration_s=duration,
+    return dict(profile=profile, self_collisions=bool(self_collisions), envs=n, steps=steps, duration_s=duration,
                 gpu=stats(alive_gpu, gpu_lin, gpu_yaw),
                 oracle_f64=stats(ref64["fall_step"], ref64["lin_vel_error"], ref64["yaw_rate_error"]),
                 oracle_f32=[stats(e[0]["fall_step"], e[0]["lin_vel_error"], e[0]["yaw_rate_error"]) for e in ens],
+                fall_cause_f64={k: int(sum(1 for c in ref64["fall_cause"] if c == k))
+                                for k in sorted(set(ref64["fall_cause"]))},
                 fall_step_gpu=alive_gpu.tolist(), fall_step_f64=ref64["fall_step"].tolist(),
                 fall_step_f32=[e[0]["fall_step"].tolist() for e in ens],
                 div_gpu=div_gpu.tolist(), div_f32=div_f32.tolist())
@@ -108,19 +125,22 @@ def main():
     ap.add_argument("--duration", type=float, default=20.0)
     ap.add_argument("--envs_per_command", type=int, default=16)
     ap.add_argument("--ensemble", type=int, default=2)
+    ap.add_argument("--no-self-collisions", action="store_true", help="ablation: no self-collision pairs")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r3_onnx"))
     a = ap.parse_args()
     import physics_ref as P
     P.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
-    r = compare(a.profile, COMMANDS, a.envs_per_command, a.duration, a.ensemble)
+    r = compare(a.profile, COMMANDS, a.envs_per_command, a.duration, a.ensemble,
+                self_collisions=not a.no_self_collisions)
     os.makedirs(a.out, exist_ok=True)
-    path = os.path.join(a.out, f"onnx_closed_loop_{a.profile}.json")
+    path = os.path.join(a.out, f"onnx_closed_loop_{a.profile}{'_noself' if a.no_self_collisions else ''}.json")
     with open(path, "w") as f:
         json.dump(r, f, indent=1)
     for name in ("gpu", "oracle_f64"):
         for c in r[name]:
             print(f"{name:10s} cmd {c['command']}: falls {c['falls']}/{a.envs_per_command} mean fall time "
                   f"{c['mean_fall_time_s']:.2f} s |v - cmd| {c['lin_vel_error']:.3f} |wz| {c['yaw_rate_error']:.3f}")
+    print("oracle f64 termination causes (contacts on the base at the first terminating step):", r["fall_cause_f64"])
     print("->", path)
 
 
