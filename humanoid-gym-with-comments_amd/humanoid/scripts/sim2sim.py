@@ -12,7 +12,10 @@ policy trained on the URDF profile meets when it is transferred:
     humanoid_config.py:118);
   * joint frictionloss 0.01 N m on every leg joint, 0.05 N m on the ankles (:38, :426, :431, :476,
     :481; the URDF has 0.1 N m on the ankles only);
-  * joint damping 0.01 N m s/rad (:38), added to the PD damping;
+  * joint damping 0.01 N m s/rad (:38), added to the PD damping — a stated deviation: MuJoCo's
+    passive damping is never clipped, while the folded term is clipped with the PD torque at the
+    200 N m limit and loses its implicit integration on a saturated joint (0.01 against kd = 10:
+    0.1 % of the damping, and only on saturated joints);
   * ground/foot friction 0.9 (the default geom friction, :14; MuJoCo's max-combine of two 0.9
     geoms), no friction randomisation;
   * 50 solver iterations (``<option iterations='50' solver='PGS'>``, :3) instead of 4 + 1;
