@@ -2,11 +2,12 @@
 actor_critic.py:36-149) with the activation backward and bias gradient fused into one HIP pass
 per layer (``hg_mlp_act_backward``, csrc/hg_mlp.hip).
 
-The GEMMs are torch's (``addmm`` forward, ``mm`` for the weight and input gradients — the same
-hipBLASLt/rocBLAS calls nn.Linear makes, so the TunableOp table applies unchanged).  What changes
-is the per-layer elementwise/reduction tail of the backward: torch runs ELU-backward and a
-separate ``grad.sum(0)`` reduction over the [rows, width] gradient; here it is one pass that
-reads the incoming gradient and the layer's ELU output once.  The layer output y (not the
+The weight-gradient GEMMs are torch's (hipBLASLt/rocBLAS through the TunableOp table, split-K
+where it pays).  The hidden layers' forward and input-gradient products run on the build's own
+LDS-staged f32 MFMA GEMM where it was measured faster (``_GEMM_FWD`` / ``_GEMM_DX``), with the bias
++ ELU, respectively the lower layer's ELU backward + bias-gradient partials, in its epilogue; the
+other shapes keep torch's addmm / mm, and the ELU backward and the ``grad.sum(0)`` reduction then
+run as one pass that reads the incoming gradient and the layer's ELU output once.  The layer output y (not the
 pre-activation) is kept for the backward: elu'(h) = y + 1 for h <= 0.  Parameters stay in the
 nn.Sequential (state_dict keys unchanged).  Device float32 only.
 """
@@ -174,8 +175,96 @@ def linear_act(h, W, b, elu=True, out=None, tile=0):
     return y
 
 
+# LDS-staged f32 GEMM with the layer's elementwise work in its epilogue (hg_gemm_f32,
+# csrc/hg_gemm.hip): the hidden-layer forward with bias + ELU (no separate ELU pass), and the
+# input-gradient product of layer i fused with layer i-1's ELU backward and bias-gradient column
+# partials (no separate hg_mlp_act_backward pass).  Routing: (k, n) of the product -> [(max rows,
+# block tile)], first entry whose row bound covers the call; shapes absent from the table keep the
+# previous path.  Tiles measured on MI355X per shape against torch (addmm + ELU, mm + the fused
+# ELU-backward pass) and the register-operand kernel above (scripts/gemm_probe.py,
+# profiles/r3_gemm/gemm_probe.jsonl).
+_GEMM_FWD = {}
+_GEMM_DX = {}
+GEMM = os.environ.get("HG_GEMM", "1") != "0"
+
+
+def _route(table, rows, k, n):
+    if not GEMM:
+        return 0
+    for max_rows, tile in table.get((k, n), ()):
+        if rows <= max_rows:
+            return tile
+    return 0
+
+
+def _gemm_fwd_tile(h, W, b):
+    if not (h.dim() == 2 and h.stride(1) == 1 and h.dtype == torch.float32 and W.is_contiguous() and b is not None
+            and b.is_contiguous()):
+        return 0
+    return _route(_GEMM_FWD, h.shape[0], W.shape[1], W.shape[0])
+
+
+def gemm_forward(h, W, b, elu=True, tile=0, out=None):
+    """y = elu(h W^T + b) (``elu`` False: h W^T + b) on hg_gemm_f32 (mode 0)."""
+    rows, n, k = h.shape[0], W.shape[0], W.shape[1]
+    L = N.lib()
+    if tile == 0:
+        tile = int(L.hg_gemm_tile(0, rows, n, k))
+    y = torch.empty(rows, n, dtype=torch.float32, device=h.device) if out is None else out
+    if y.shape != (rows, n) or y.stride(1) != 1 or y.dtype != torch.float32:
+        raise RuntimeError("gemm_forward: out must be a float32 [rows, n] tensor with unit column stride")
+    rc = L.hg_gemm_f32(0, h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0, y.data_ptr(),
+                       y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_gemm_f32 (forward) failed ({rc})")
+    return y
+
+
+def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0):
+    """(gh W) * elu'(y_prev) — layer i's input gradient through layer i-1's ELU backward (its
+    pre-activation gradient) — with layer i-1's bias gradient gb = column sums, on hg_gemm_f32
+    (mode 1).  gh [rows, n_i] contiguous, W [n_i, k_i] (nn.Linear.weight), y_prev [rows, k_i]."""
+    rows, kr = gh.shape
+    n = W.shape[1]
+    L = N.lib()
+    if tile == 0:
+        tile = int(L.hg_gemm_tile(1, rows, n, kr))
+    out = torch.empty(rows, n, dtype=torch.float32, device=gh.device)
+    parts = int(L.hg_gemm_colpart_rows(rows, tile))
+    cp = torch.empty(parts, n, dtype=torch.float32, device=gh.device)
+    rc = L.hg_gemm_f32(1, gh.data_ptr(), gh.stride(0), W.data_ptr(), W.stride(0), None, y_prev.data_ptr(),
+                       y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
+                       _stream(gh.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_gemm_f32 (input grad) failed ({rc})")
+    if red is None:
+        r = _Reductions()
+        r.add(cp, gb, n, parts)
+        r.launch(gh.device)
+    else:
+        red.add(cp, gb, n, parts)
+    return out
+
+
+def _gemm_dx_tile(gh, W, y_prev):
+    if not (gh.is_contiguous() and W.is_contiguous() and y_prev.dim() == 2 and y_prev.stride(1) == 1
+            and y_prev.dtype == torch.float32):
+        return 0
+    return _route(_GEMM_DX, gh.shape[0], W.shape[0], W.shape[1])
+
+
 # the per-layer column sums of the backward run as one batched launch at its end (hg_colsum_jobs)
 DEFER_REDUCTIONS = os.environ.get("HG_DEFER_REDUCTIONS", "1") != "0"
+
+
+def _hidden_forward(h, W, b):
+    """One hidden layer: the LDS-staged GEMM, the register-operand fused kernel, or addmm + ELU."""
+    tile = _gemm_fwd_tile(h, W, b)
+    if tile:
+        return gemm_forward(h, W, b, True, tile)
+    if _fused_ok(h, W, b):
+        return linear_act(h, W, b)
+    return F.elu(torch.addmm(b, h, W.t()))
 
 
 class _MLP(torch.autograd.Function):
@@ -188,12 +277,10 @@ class _MLP(torch.autograd.Function):
             W, b = params[2 * i], params[2 * i + 1]
             if i == n - 1 and _skinny_ok(h, W):
                 h = _skinny_forward(h, W, b)
-            elif i < n - 1 and _fused_ok(h, W, b):
-                h = linear_act(h, W, b)
+            elif i < n - 1:
+                h = _hidden_forward(h, W, b)
             else:
                 h = torch.addmm(b, h, W.t())
-                if i < n - 1:
-                    h = F.elu(h)
             acts.append(h)
         # inputs of every layer (x, y_0 .. y_{n-2}) and the weights
         ctx.save_for_backward(*acts[:-1], *params[0::2])
@@ -209,26 +296,39 @@ class _MLP(torch.autograd.Function):
         g = g.contiguous()
         gx = None
         red = _Reductions() if DEFER_REDUCTIONS else None
+        pre = None  # (gh, gb) of layer i when the layer above produced them in its input-grad GEMM
         for i in range(n - 1, -1, -1):
             need_dx = i > 0 or ctx.needs_input_grad[0]
+            gnext = None
             if i == n - 1 and _skinny_ok(ins[i], Ws[i]):
                 # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
                 grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx, red)
             else:
-                rows, width = g.shape
-                gb = torch.empty(width, dtype=torch.float32, device=g.device)
-                # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
-                gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb, red)
+                if pre is not None:
+                    gh, gb = pre
+                    pre = None
+                else:
+                    rows, width = g.shape
+                    gb = torch.empty(width, dtype=torch.float32, device=g.device)
+                    # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
+                    gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb, red)
                 grads[2 * i + 1] = gb
                 grads[2 * i] = _weight_grad(gh, ins[i], red)
-                gnext = torch.mm(gh, Ws[i]) if need_dx else None
+                if need_dx:
+                    tile = _gemm_dx_tile(gh, Ws[i], ins[i]) if i > 0 else 0
+                    if tile:
+                        # layer i-1's pre-activation gradient and bias gradient straight from this GEMM
+                        gb_prev = torch.empty(Ws[i].shape[1], dtype=torch.float32, device=g.device)
+                        pre = (gemm_input_grad(gh, Ws[i], ins[i], gb_prev, red, tile), gb_prev)
+                    else:
+                        gnext = torch.mm(gh, Ws[i])
             if i > 0:
                 # the next (lower) layer's incoming gradient goes through its ELU backward
                 g = gnext
             else:
                 gx = gnext
         if red is not None:
-            red.launch(g.device)
+            red.launch(ins[0].device)
         return (gx, *grads)
 
 
@@ -246,15 +346,16 @@ def mlp_forward(net, x):
 
 
 def mlp_infer(net, x, out=None):
-    """net(x) without autograd (rollout inference): hidden layers on the fused Linear + ELU kernel
-    where ``_FUSED_FWD_ROWS`` routes them, torch's Linear/ELU otherwise; the skinny HIP kernel for
-    the output layer (written into ``out`` when given)."""
+    """net(x) without autograd (rollout inference): hidden layers on the LDS-staged GEMM or the
+    register-operand fused kernel where ``_GEMM_FWD`` / ``_FUSED_FWD_ROWS`` route them, torch's
+    Linear/ELU otherwise; the skinny HIP kernel for the output layer (written into ``out`` when
+    given)."""
     mods = list(net)
     h = x
     for j in range(0, len(mods) - 1, 2):
         lin = mods[j]
-        if _fused_ok(h, lin.weight, lin.bias) and isinstance(mods[j + 1], nn.ELU) and mods[j + 1].alpha == 1.0:
-            h = linear_act(h, lin.weight, lin.bias)
+        if isinstance(mods[j + 1], nn.ELU) and mods[j + 1].alpha == 1.0 and not mods[j + 1].inplace:
+            h = _hidden_forward(h, lin.weight, lin.bias)
         else:
             h = mods[j + 1](lin(h))
     last = mods[-1]

@@ -422,6 +422,23 @@ int hg_linear_act_forward(const float* x, int64_t ldx, const float* W, const flo
                           int64_t rows, int n, int k, int act, int tile, void* stream);
 int hg_linear_act_tile(int64_t rows, int n, int k);
 
+/* LDS-staged f32 GEMM of the hidden layers with the layer's elementwise work in the epilogue
+ * (replaces, per hidden layer of actor_critic.py:36-149, torch's addmm + ELU forward and, in the
+ * backward, the input-gradient mm + the next lower layer's ELU backward + its bias-gradient sum):
+ *   mode 0 (forward):    C[r][c] = act(sum_k A[r][k] B[c][k] + bias[c])      A [M, K] (lda), B [N, K] (ldb)
+ *   mode 1 (input grad): C[r][c] = (sum_k A[r][k] B[k][c]) * elu'(Y[r][c])  A [M, K] (lda), B [K, N] (ldb)
+ *     with elu'(from the ELU output y) = 1 for y > 0, y + 1 otherwise (act 1; act 0: no factor,
+ *     Y unused); colpart (may be NULL) receives the column sums of C per row tile,
+ *     [hg_gemm_colpart_rows(M, tile), N], reduced later in fixed order (hg_colsum_jobs).
+ * tile 1..4 = block tiles 128x128, 128x64, 64x128, 64x64 (hg_gemm_tile picks one); rows of A,
+ * B, C 4-byte aligned (16-byte rows take the vector-load staging).  One launch, no host
+ * synchronisation, exact f32 products with f32 accumulation (v_mfma_f32_32x32x2_f32). */
+int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, const float* Y,
+                int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K, int act, int tile,
+                void* stream);
+int hg_gemm_tile(int mode, int64_t M, int N, int K);
+int64_t hg_gemm_colpart_rows(int64_t M, int tile);
+
 /* library build info */
 const char* hg_version(void);
 
