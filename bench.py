@@ -52,6 +52,29 @@ def sq_issue(kernel_file=os.path.join(REPO, "profiles", PROFILE_DIR, "sq_counter
         return None
 
 
+def mfma_stats(rows, envs, decimation=10, nf=18,
+               kernel_file=os.path.join(REPO, "profiles", PROFILE_DIR, "sq_counters_k_step.json")):
+    """K_step's matrix-core use (the Delassus block W = Z^T Z, v_mfma_f32_32x32x2_f32: 32 x 32 x 2
+    per instruction = 4096 FLOP, 16 quad-cycles of the SIMD's MFMA pipe) from the committed SQ
+    counters: instructions per wave, issued vs useful FLOP (useful = rows^2 nf multiply-adds per env
+    and substep at the measured active rows; the 32 x 32 tile covers 32 rows) and the pipe busy
+    estimate 2 waves/SIMD x SQ_INSTS_MFMA x 16 / SQ_WAVE_CYCLES (quad-cycles)."""
+    try:
+        with open(kernel_file) as f:
+            pw = json.load(f)["per_wave"]
+        n_mfma, wave_cycles = float(pw["SQ_INSTS_MFMA"]), float(pw["SQ_WAVE_CYCLES"])
+    except (OSError, KeyError, ValueError):
+        return None
+    waves = (envs + 1) // 2
+    issued = n_mfma * 4096.0 * waves
+    useful = 2.0 * rows * rows * nf * decimation * envs
+    return {"instr": "v_mfma_f32_32x32x2_f32", "instructions_per_wave": n_mfma,
+            "issued_flop_per_launch": issued, "useful_flop_per_launch": round(useful, 1),
+            "tile_util": round(useful / issued, 4) if issued else None,
+            "pipe_busy_est": round(2.0 * n_mfma * 16.0 / wave_cycles, 4),
+            "source": os.path.relpath(kernel_file, REPO)}
+
+
 def pmc_traffic(kernel="k_step"):
     """HBM bytes per launch of `kernel` from the committed PMC summary (None if absent)."""
     try:
@@ -371,6 +394,7 @@ def main():
                 "avg_launch_ms": round(ms_step, 4), "launches": timer.count("k_step"),
                 "launch_sampling": f"HIP events on 1 in {timer.every} launches of the timed region",
                 "flops_per_launch": flops, "active_rows_per_env": round(rows, 2),
+                "mfma": mfma_stats(rows, args.envs),
                 "k_post_avg_ms": round(timer.mean_ms("k_post"), 4)}
     result = {
         "metric": "env-steps/sec (whole node) at 4096 envs + PPO iters/sec, 1/2/4/8 MI355X",

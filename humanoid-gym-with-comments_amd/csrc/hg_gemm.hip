@@ -358,9 +358,10 @@ int tile_bm(int tile) {
 extern "C" int hg_gemm_tile(int mode, int64_t M, int N, int K) {
   (void)mode;
   (void)K;
-  // >= 2 blocks per CU's worth of 128 x 64 tiles, else 64 x 64
-  const int64_t t2 = ((M + 127) / 128) * ((N + 63) / 64);
-  return t2 >= 512 ? 2 : 4;
+  // pipelined 128 x 64 tile on 8 waves while that gives >= 3 blocks per CU, else 64 x 64
+  // (scripts/gemm_probe.py, profiles/r3_gemm)
+  const int64_t t16 = ((M + 127) / 128) * ((N + 63) / 64);
+  return t16 >= 768 ? 16 : 5;
 }
 
 extern "C" int64_t hg_gemm_colpart_rows(int64_t M, int tile) {

@@ -183,8 +183,17 @@ def linear_act(h, W, b, elu=True, out=None, tile=0):
 # previous path.  Tiles measured on MI355X per shape against torch (addmm + ELU, mm + the fused
 # ELU-backward pass) and the register-operand kernel above (scripts/gemm_probe.py,
 # profiles/r3_gemm/gemm_probe.jsonl).
-_GEMM_FWD = {}
-_GEMM_DX = {}
+# profiles/r3_gemm/gemm_probe_variants.jsonl (us, torch -> this kernel): forward 24576 rows 705x512
+# 167 -> 160 (tile 17), 256x128 29.5 -> 22.4 (5), 128x128 fused 20.2 -> 15.0 (4); 4096 rows 512x256
+# fused 21 -> 17.5 (5), 705x128 25.3 -> 22.0 (5); the critic's 98304-row value pass 219x768 428 ->
+# 380 (9).  Input gradients (24576 rows, torch mm + ELU-backward pass -> fused): actor 256->512
+# 82.5 -> 71.6, 128->256 33.1 -> 25.0, critic 256->768 115 -> 103, 128->256 33.4 -> 25.1 (tile
+# 16), lin-vel 128->128 22.0 -> 17.7 (4).  512x256 and 705x128 at 24576 rows, 768x256 and 219x768
+# up to 32768 rows stay on torch (equal or faster there).
+_BIG = 1 << 40
+_GEMM_FWD = {(705, 512): [(8192, 0), (_BIG, 17)], (512, 256): [(8192, 5)], (256, 128): [(8192, 0), (_BIG, 5)],
+             (705, 128): [(8192, 5)], (128, 128): [(8192, 0), (_BIG, 4)], (219, 768): [(32768, 0), (_BIG, 9)]}
+_GEMM_DX = {(256, 512): [(_BIG, 16)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 16)], (128, 128): [(_BIG, 4)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
 
 
@@ -318,7 +327,7 @@ class _MLP(torch.autograd.Function):
                     tile = _gemm_dx_tile(gh, Ws[i], ins[i]) if i > 0 else 0
                     if tile:
                         # layer i-1's pre-activation gradient and bias gradient straight from this GEMM
-                        gb_prev = torch.empty(Ws[i].shape[1], dtype=torch.float32, device=g.device)
+                        gb_prev = torch.empty(Ws[i].shape[1], dtype=torch.float32, device=gh.device)
                         pre = (gemm_input_grad(gh, Ws[i], ins[i], gb_prev, red, tile), gb_prev)
                     else:
                         gnext = torch.mm(gh, Ws[i])

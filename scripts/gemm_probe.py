@@ -23,7 +23,7 @@ L = N.lib()
 print(json.dumps({"tunableop_table_loaded": use_tuned_gemms()}))
 torch.manual_seed(0)
 ITERS = int(os.environ.get("ITERS", 30))
-TILES = [int(t) for t in os.environ.get("TILES", "4,5,8,9,11,12,13,14").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "4,5,8,9,11,12,13,14,15,16,17,18").split(",")]
 
 FWD = [("actor0_mb", 24576, 705, 512), ("actor1_mb", 24576, 512, 256), ("actor2_mb", 24576, 256, 128),
        ("linvel0_mb", 24576, 705, 128), ("linvel1_mb", 24576, 128, 128),
@@ -88,7 +88,7 @@ for tag, rows, k, n in FWD:
     rec["best_tile"], rec["best_us"] = best[0], round(best[1], 2)
     rec["speedup_vs_torch"] = round(t_torch / best[1], 3)
     print(json.dumps(rec), flush=True)
-    summary[tag] = (rec["torch_us"], rec["best_us"], rec["best_tile"], rec[f"tile{rec['auto_tile']}_us"])
+    summary[tag] = (rec["torch_us"], rec["best_us"], rec["best_tile"], rec.get(f"tile{rec['auto_tile']}_us"))
 
 for tag, rows, kr, n in DX:
     g = torch.randn(rows, kr, device=dev)
@@ -131,5 +131,5 @@ for tag, rows, kr, n in DX:
     rec["best_tile"], rec["best_us"] = best[0], round(best[1], 2)
     rec["speedup_vs_torch"] = round(t_torch / best[1], 3)
     print(json.dumps(rec), flush=True)
-    summary[tag] = (rec["torch_us"], rec["best_us"], rec["best_tile"], rec[f"tile{rec['auto_tile']}_us"])
+    summary[tag] = (rec["torch_us"], rec["best_us"], rec["best_tile"], rec.get(f"tile{rec['auto_tile']}_us"))
 print(json.dumps({"summary_torch_best_tile_auto": summary}))

@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+if [ -z "$SKIP_PROBE" ]; then
 timeout -k 10 300 python -u scripts/gemm_probe.py > gpurun_out/gemm_probe.jsonl 2> gpurun_out/gemm_probe.err || { echo "probe failed"; tail -20 gpurun_out/gemm_probe.err; exit 1; }
 python -c "
 import json
@@ -11,5 +12,6 @@ for l in open('gpurun_out/gemm_probe.jsonl'):
     d=json.loads(l)
     if 'shape' in d: print(d['shape'], 'torch', d['torch_us'], 'best', d['best_us'], 'tile', d['best_tile'], 'x', d['speedup_vs_torch'], 'err', '%.2e'%d['tile%d_err'%d['best_tile']], 'terr', '%.2e'%d['torch_err'])
 "
+fi
 if [ -n "$RUN_TESTS" ]; then SKIP_BENCH=1 bash scripts/gpu_round3.sh || exit $?; fi
 if [ -n "$RUN_BENCH" ]; then timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1 || exit $?; tail -1 gpurun_out/bench.log; fi

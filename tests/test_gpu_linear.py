@@ -87,8 +87,9 @@ def test_linear_act_rejects_bad_arguments():
 
 
 def test_mlp_paths_use_fused_forward():
-    """The rollout inference and the training forward route the small hidden layers through the
-    fused kernel (and agree with torch's nn.Sequential)."""
+    """The rollout inference routes every small hidden layer through one of the build's fused
+    Linear + ELU kernels (the register-operand kernel or the LDS-staged GEMM, hg_mlp routing
+    tables) and agrees with torch's nn.Sequential."""
     _need_gpu()
     from humanoid.algo.ppo import ActorCritic, hg_mlp
     torch.manual_seed(4)
@@ -96,20 +97,24 @@ def test_mlp_paths_use_fused_forward():
                      base_lin_vel_hidden_dims=[128, 128]).cuda()
     obs = torch.randn(4096, 705, device="cuda:0")
     calls = []
-    orig = hg_mlp.linear_act
+    orig, orig_g = hg_mlp.linear_act, hg_mlp.gemm_forward
 
     def spy(h, W, b, **kw):
         calls.append(tuple(W.shape))
         return orig(h, W, b, **kw)
 
-    hg_mlp.linear_act = spy
+    def spy_g(h, W, b, *a, **kw):
+        calls.append(tuple(W.shape))
+        return orig_g(h, W, b, *a, **kw)
+
+    hg_mlp.linear_act, hg_mlp.gemm_forward = spy, spy_g
     try:
         with torch.no_grad():
             mu = ac._mlp(ac.actor, obs)
             lv = ac._mlp(ac.base_lin_vel, obs)
-        assert (256, 512) in calls and (128, 256) in calls and (128, 128) in calls
+        assert (256, 512) in calls and (128, 256) in calls and (128, 128) in calls and (128, 705) in calls, calls
         with torch.no_grad():
             torch.testing.assert_close(mu, ac.actor(obs), rtol=1e-5, atol=1e-5)
             torch.testing.assert_close(lv, ac.base_lin_vel(obs), rtol=1e-5, atol=1e-5)
     finally:
-        hg_mlp.linear_act = orig
+        hg_mlp.linear_act, hg_mlp.gemm_forward = orig, orig_g
