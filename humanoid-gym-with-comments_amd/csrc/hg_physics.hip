@@ -786,7 +786,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         float k[14];
 #pragma unroll
         for (int i = 0; i < 14; i++) k[i] = det_k[i];
-        if (rnd) pr = load_item(M, min(item, nitems - 1), nleg, npair, cc, pp, b0, b1, k);
+        if (rnd) {
+          pr = load_item(M, min(item, nitems - 1), nleg, npair, cc, pp, b0, b1, k);
+          // round 2 holds ground candidates (the base-box corners): on a plane, a candidate whose
+          // body origin is higher than contact_offset + the point's distance from it + its radius
+          // cannot be active.  When no round-2 item of the wave's two envs can be, the round is
+          // skipped (bitwise the same result: its warm-start slots are cleared as an inactive
+          // candidate's are, and no contact is placed)
+          // (a fixed base never activates ground candidates)
+          const bool can = item < nitems &&
+                           (pr || (!fixed && (cfg->terrain_type != 0 ||
+                                              E.o[b0][2] + E.root[2] - sqrtf(k[0] * k[0] + k[1] * k[1] + k[2] * k[2]) -
+                                                      k[3] < cfg->contact_offset)));
+          if (__ballot(can) == 0) {
+            if (item < nitems) E.lamst[3 * cc + 0] = E.lamst[3 * cc + 1] = E.lamst[3 * cc + 2] = 0.f;
+            continue;
+          }
+        }
         Cand c;
         if (item < nitems) c = detect(E, cfg, pr, cc, pp, b0, b1, k, fixed);
         const bool act = item < nitems && c.act;

@@ -19,9 +19,66 @@ OUT = os.path.join(REPO, "build", "kvar")
 HIPCC = "/opt/rocm/bin/hipcc"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-fno-slp-vectorize"]
 
+PGS_OLD = """            float db, dc;
+            {
+              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
+              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
+              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
+              const float dbs = nbs - lb;
+              const float vc2 = vc1 + G.Wcb * dbs;
+              const float ncs = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
+              const bool ct = G.mu >= 0.f;
+              db = ct ? l1 * sc - lb : dbs;
+              dc = ct ? l2 * sc - lc : ncs - lc;
+            }"""
+PGS_NEW = """            float db, dc;
+            if (g < npts_lo) {  // a contact group in both envs of the wave
+              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
+              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
+              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+              db = l1 * sc - lb;
+              dc = l2 * sc - lc;
+            } else if (g >= npts_hi) {  // single rows in both envs
+              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
+              const float dbs = nbs - lb;
+              const float vc2 = vc1 + G.Wcb * dbs;
+              const float ncs = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
+              db = dbs;
+              dc = ncs - lc;
+            } else {
+              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
+              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
+              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
+              const float dbs = nbs - lb;
+              const float vc2 = vc1 + G.Wcb * dbs;
+              const float ncs = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
+              const bool ct = G.mu >= 0.f;
+              db = ct ? l1 * sc - lb : dbs;
+              dc = ct ? l2 * sc - lc : ncs - lc;
+            }"""
+PGS_NG_OLD = "      const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;"
+PGS_NG_NEW = ("      const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;\n"
+              "      const int npts_lo = min(shm[0].npts, shm[1].npts), npts_hi = max(shm[0].npts, shm[1].npts);")
+DIV = [("  float s = denom > 1e-6f * a * e ? fminf(fmaxf((b * f - c * e) / denom, 0.f), 1.f) : 0.f;\n"
+        "  float t = (b * s + f) / e;\n"
+        "  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-c / a, 0.f), 1.f); }\n"
+        "  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((b - c) / a, 0.f), 1.f); }",
+        "  const float ia = __builtin_amdgcn_rcpf(a), ie = __builtin_amdgcn_rcpf(e);\n"
+        "  float s = denom > 1e-6f * a * e ? fminf(fmaxf((b * f - c * e) * __builtin_amdgcn_rcpf(denom), 0.f), 1.f) : 0.f;\n"
+        "  float t = (b * s + f) * ie;\n"
+        "  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-c * ia, 0.f), 1.f); }\n"
+        "  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((b - c) * ia, 0.f), 1.f); }"),
+       ("    C.cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);",
+        "    C.cn = dist > 1e-9f ? __builtin_amdgcn_rcpf(dist) * dv : mk(0.f, -1.f, 0.f);")]
+
 VARIANTS = {
     "base": [],
     "no_round2": [("const int rounds = nitems > 32 ? 2 : 1;", "const int rounds = 1;")],
+    "pgs_spec": [(PGS_NG_OLD, PGS_NG_NEW), (PGS_OLD, PGS_NEW)],
+    "fastdiv": DIV,
+    "pgs_spec_fastdiv": [(PGS_NG_OLD, PGS_NG_NEW), (PGS_OLD, PGS_NEW)] + DIV,
 }
 
 
