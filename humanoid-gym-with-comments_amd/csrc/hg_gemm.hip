@@ -347,10 +347,404 @@ int launch(int mode, GemmArgs g, bool vec, bool elu, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-constexpr int NTILES = 18;
+// ---------------------------------------------------------------------------------------------
+// f32 GEMM on the bf16 matrix cores (16x the f32 MFMA rate): every f32 operand is split exactly
+// into three bf16 terms x = x0 + x1 + x2 (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1):
+// 24 significand bits; the rounding of x2 leaves ~2^-24 |x|, f32's own representation error), and
+// the product keeps the six terms of total order <= 2, a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 +
+// a2 b0 (the dropped a1 b2 + a2 b1 + a2 b2 are ~2^-24 |a b|), each bf16 x bf16 product exact in the
+// f32 accumulator of v_mfma_f32_32x32x16_bf16, smallest terms first.  Measured error per element
+// <= 3.4e-7 of sum_k |a_k b_k| (torch's f32 GEMM: 4.6e-7; tests/test_gpu_gemm.py bounds both at
+// 1e-6).  The split runs once per element while the chunk is staged (global f32 -> registers ->
+// three bf16 planes in LDS).
+//   mode 0 forward     C = act(A B^T + bias)        A [M, K] k-contiguous, B [N, K] k-contiguous
+//   mode 1 input grad  C = (A B) * elu'(Y) + colpart A [M, K] k-contiguous, B [K, N] n-contiguous
+//   mode 2 weight grad C_s = sum_{k in slice s} A[k][m] B[k][n]   (A [K, M], B [K, N]: both
+//          reduction-major; split-K slices of kslice rows write C + s * cstride, summed later in
+//          fixed order by hg_colsum_jobs)
+// Block BM x BN on WGM x WGN waves (each (32 TM) x (32 TN) of 32x32 accumulators), KG 16-deep k
+// groups per staged chunk, double-buffered.  Plane image of an R-row operand tile: slot ((kg R /
+// 32 + r / 32) 2 + h) 32 + r % 32 holds 8 bf16 (k = 16 kg + 8 h + 0..7): the 64 lanes' fragment
+// reads are one contiguous 1 KB run.  k-contiguous operands are staged as two 16-byte loads per
+// 8-k item; reduction-major ones as 8 scalar loads (64 lanes = 64 consecutive rows: 256 contiguous
+// bytes per load instruction).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3x8(const float v[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const __bf16 a = (__bf16)v[j];
+    const float r1 = v[j] - (float)a;
+    const __bf16 b = (__bf16)r1;
+    const float r2 = r1 - (float)b;
+    h[j] = a;
+    m[j] = b;
+    l[j] = (__bf16)r2;
+  }
+}
+
+__device__ __forceinline__ int x6_slot(int R, int kg, int r, int h) {
+  return ((kg * (R >> 5) + (r >> 5)) * 2 + h) * 32 + (r & 31);
+}
+
+struct GemmX6Args {
+  GemmArgs g;
+  int64_t kslice;   // mode 2: reduction rows per split-K slice (multiple of 16)
+  int64_t cstride;  // mode 2: elements between slices' outputs
+  int slices;
+};
+
+// one operand's staging: R rows x (16 KG) k of the chunk at reduction index kc.  KC:
+// k-contiguous rows (row r at P + r ld): items (r, 8-k piece), two 16-byte loads each;
+// reduction-major (element (r, k) at P[k ld + r]): items (r, 8-k piece), eight scalar loads each
+// (64 lanes = 64 consecutive r: 256 contiguous bytes per load instruction).  (Items of four r
+// with 16-byte loads were measured 2-3x slower: a quarter of the threads carried the staging.)
+template <int R, int KG, int NT, bool KC, bool VEC>
+struct X6Stage {
+  static constexpr int ITEMS = R * 2 * KG;
+  static constexpr int IPT = (ITEMS + NT - 1) / NT;
+  float v[IPT][8];
+  __device__ __forceinline__ void item(int idx, int& r, int& piece) const {
+    if (KC) { r = idx / (2 * KG); piece = idx % (2 * KG); }
+    else { r = idx % R; piece = idx / R; }
+  }
+  // elements at or past kend read 0; rows past rmax read row rmax
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0, int64_t rmax, int64_t kc,
+                                       int64_t kend, bool tail, int tid) {
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int idx = tid + j * NT;
+      if (ITEMS % NT != 0 && idx >= ITEMS) break;
+      int r, piece;
+      item(idx, r, piece);
+      const int64_t rr = min<int64_t>(r0 + r, rmax);
+      const int64_t k0 = kc + 8 * piece;
+      if (KC) {
+        const float* p = P + rr * ld + k0;
+        if (!tail) {
+          if (VEC) {
+            const float4 x = *reinterpret_cast<const float4*>(p), y = *reinterpret_cast<const float4*>(p + 4);
+            v[j][0] = x.x; v[j][1] = x.y; v[j][2] = x.z; v[j][3] = x.w;
+            v[j][4] = y.x; v[j][5] = y.y; v[j][6] = y.z; v[j][7] = y.w;
+          } else {
+            const f32x4u x = *reinterpret_cast<const f32x4u*>(p), y = *reinterpret_cast<const f32x4u*>(p + 4);
+#pragma unroll
+            for (int q = 0; q < 4; q++) { v[j][q] = x[q]; v[j][4 + q] = y[q]; }
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; q++) v[j][q] = (k0 + q < kend) ? p[q] : 0.f;
+        }
+      } else {
+        const float* p = P + k0 * ld + rr;
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[j][q] = (!tail || k0 + q < kend) ? p[q * ld] : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(bf16x8* __restrict__ plane0, int tid) const {
+    constexpr int PS = R * 2 * KG;  // slots per plane
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int idx = tid + j * NT;
+      if (ITEMS % NT != 0 && idx >= ITEMS) break;
+      int r, piece;
+      item(idx, r, piece);
+      const int sl = x6_slot(R, piece >> 1, r, piece & 1);
+      bf16x8 x0, x1, x2;
+      split3x8(v[j], x0, x1, x2);
+      plane0[sl] = x0;
+      plane0[PS + sl] = x1;
+      plane0[2 * PS + sl] = x2;
+    }
+  }
+};
+
+// reduction-major operand (element (r, k) at P[k ld + r], r contiguous) staged through an f32 LDS
+// scratch: items (k row q, 4 consecutive r) read as 16-byte row segments (lanes along r, balanced
+// over all threads), written transposed into scratch [R][16 KG + 1] (odd pitch: the lanes' 4-byte
+// writes fall on distinct banks), then, after a barrier, every thread gathers one (r, 8-k piece)
+// from the scratch, splits it and writes the three planes.
+template <int R, int KG, int NT>
+struct X6StageT {
+  static constexpr int PITCH = 16 * KG + 1;
+  static constexpr int ITEMS = 16 * KG * (R / 4);
+  static constexpr int IPT = (ITEMS + NT - 1) / NT;
+  static constexpr int PITEMS = R * 2 * KG;
+  static constexpr int PIPT = (PITEMS + NT - 1) / NT;
+  static constexpr int SCRATCH = R * PITCH;  // floats
+  float v[IPT][4];
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0, int64_t rmax, int64_t kc,
+                                       int64_t kend, bool tail, int tid) {
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int idx = tid + j * NT;
+      if (ITEMS % NT != 0 && idx >= ITEMS) break;
+      const int g = idx % (R / 4), q = idx / (R / 4);
+      const int64_t k = kc + q;
+      const int64_t rr = r0 + 4 * g;
+      const float* p = P + k * ld;
+      const bool ok = !tail || k < kend;
+      if (rr + 3 <= rmax) {
+        f32x4u x = {0.f, 0.f, 0.f, 0.f};
+        if (ok) x = *reinterpret_cast<const f32x4u*>(p + rr);
+        v[j][0] = x[0]; v[j][1] = x[1]; v[j][2] = x[2]; v[j][3] = x[3];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++) v[j][c] = ok ? p[min<int64_t>(rr + c, rmax)] : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void to_scratch(float* __restrict__ sc, int tid) const {
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int idx = tid + j * NT;
+      if (ITEMS % NT != 0 && idx >= ITEMS) break;
+      const int g = idx % (R / 4), q = idx / (R / 4);
+#pragma unroll
+      for (int c = 0; c < 4; c++) sc[(4 * g + c) * PITCH + q] = v[j][c];
+    }
+  }
+  __device__ __forceinline__ void to_planes(bf16x8* __restrict__ plane0, const float* __restrict__ sc, int tid) const {
+    constexpr int PS = R * 2 * KG;
+#pragma unroll
+    for (int j = 0; j < PIPT; j++) {
+      const int idx = tid + j * NT;
+      if (PITEMS % NT != 0 && idx >= PITEMS) break;
+      const int r = idx % R, piece = idx / R;
+      float w[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) w[q] = sc[r * PITCH + 8 * piece + q];
+      const int sl = x6_slot(R, piece >> 1, r, piece & 1);
+      bf16x8 x0, x1, x2;
+      split3x8(w, x0, x1, x2);
+      plane0[sl] = x0;
+      plane0[PS + sl] = x1;
+      plane0[2 * PS + sl] = x2;
+    }
+  }
+};
+
+// the staging of one operand: k-contiguous (X6Stage, KC), reduction-major transposed through the
+// LDS scratch (X6StageT), selected at compile time
+template <int R, int KG, int NT, bool KC, bool VEC>
+struct X6Op {
+  X6Stage<R, KG, NT, true, VEC> kc;
+  X6StageT<R, KG, NT> rt;
+  static constexpr int SCRATCH = KC ? 0 : X6StageT<R, KG, NT>::SCRATCH;
+  __device__ __forceinline__ void load(const float* P, int64_t ld, int64_t r0, int64_t rmax, int64_t kc0, int64_t kend,
+                                       bool tail, int tid) {
+    if (KC) kc.load(P, ld, r0, rmax, kc0, kend, tail, tid);
+    else rt.load(P, ld, r0, rmax, kc0, kend, tail, tid);
+  }
+};
+
+template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
+  constexpr int PA = BM * 2 * KG, PB = BN * 2 * KG;  // 16-byte slots per plane
+  constexpr int STAGE = 3 * PA + 3 * PB;
+  constexpr int BK = 16 * KG;
+  static_assert(TM >= 1 && TN >= 1 && BM == 32 * TM * WGM && BN == 32 * TN * WGN, "wave tiling");
+  static_assert(2 * STAGE * 4 >= WGM * BN, "epilogue reduction buffer fits the staging LDS");
+  constexpr bool AKC = MODE != 2, BKC = MODE == 0 || MODE == 3 || MODE == 4;
+  constexpr int SCA = AKC ? 0 : X6StageT<BM, KG, 64 * WGM * WGN>::SCRATCH;
+  constexpr int SCB = BKC ? 0 : X6StageT<BN, KG, 64 * WGM * WGN>::SCRATCH;
+  constexpr int SCS = (SCA + SCB + 3) / 4;  // scratch in 16-byte slots, after the two stages
+  __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE + SCS];
+  const GemmArgs& g = xa.g;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const unsigned nb = gridDim.x;
+  unsigned L = blockIdx.x;
+  if ((nb & 7u) == 0) L = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+  if ((int64_t)L >= g.tiles * xa.slices) return;
+  const int slice = (int)((int64_t)L % xa.slices);
+  const int64_t tile = (int64_t)L / xa.slices;
+  const int64_t tm_idx = tile / g.tiles_n;
+  const int64_t m0 = tm_idx * BM;
+  const int n0 = (int)(tile % g.tiles_n) * BN;
+  const int wm0 = (wave % WGM) * (32 * TM), wn0 = (wave / WGM) * (32 * TN);
+  const int64_t mmax = g.M - 1;
+  const int nmax = g.N - 1;
+  constexpr bool SPLITK = MODE == 2 || MODE == 4;
+  const int64_t kbeg = SPLITK ? (int64_t)slice * xa.kslice : 0;
+  const int64_t kend = SPLITK ? min<int64_t>((int64_t)g.K, kbeg + xa.kslice) : g.K;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; m++)
+#pragma unroll
+    for (int n = 0; n < TN; n++) acc[m][n] = (f32x16)0.f;
+
+  X6Op<BM, KG, NT, AKC, VEC> sa;
+  X6Op<BN, KG, NT, BKC, VEC> sb;
+  float* scA = reinterpret_cast<float*>(lds + 2 * STAGE);
+  float* scB = scA + SCA;
+  const int64_t nk = kend - kbeg;
+  const int64_t kfull = kbeg + (nk & ~(int64_t)(BK - 1));
+  const int nchunks = (int)((nk + BK - 1) / BK);
+  auto load = [&](int64_t kc) {
+    const bool tail = kc + BK > kfull;
+    sa.load(g.A, g.lda, m0, mmax, kc, kend, tail, tid);
+    sb.load(g.B, g.ldb, n0, nmax, kc, kend, tail, tid);
+  };
+  auto store = [&](bf16x8* S) {
+    if (AKC) sa.kc.store(S, tid);
+    else sa.rt.to_scratch(scA, tid);
+    if (BKC) sb.kc.store(S + 3 * PA, tid);
+    else sb.rt.to_scratch(scB, tid);
+    if (!AKC || !BKC) {
+      __syncthreads();
+      if (!AKC) sa.rt.to_planes(S, scA, tid);
+      if (!BKC) sb.rt.to_planes(S + 3 * PA, scB, tid);
+    }
+  };
+  if (nchunks > 0) {
+    load(kbeg);
+    store(lds);
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; c++) {
+    const bf16x8* cur = lds + (c & 1) * STAGE;
+    bf16x8* nxt = lds + ((c + 1) & 1) * STAGE;
+    const bool more = c + 1 < nchunks;
+    if (more) load(kbeg + (int64_t)(c + 1) * BK);
+#pragma unroll
+    for (int kg = 0; kg < KG; kg++) {
+      bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+#pragma unroll
+        for (int m = 0; m < TM; m++) a[p][m] = cur[p * PA + x6_slot(BM, kg, wm0 + 32 * m + i, h)];
+#pragma unroll
+        for (int n = 0; n < TN; n++) b[p][n] = cur[3 * PA + p * PB + x6_slot(BN, kg, wn0 + 32 * n + i, h)];
+      }
+#pragma unroll
+      for (int m = 0; m < TM; m++)
+#pragma unroll
+        for (int n = 0; n < TN; n++) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b[0][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[1][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[2][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[0][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[1][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[0][n], acc[m][n], 0, 0, 0);
+        }
+    }
+    if (more) store(nxt);
+    __syncthreads();
+  }
+
+  // epilogue.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2) + 4h, column i.
+  if (MODE == 0 || SPLITK) {
+    float* Cs = g.C + (SPLITK ? (int64_t)slice * xa.cstride : 0);  // mode 3 takes the input-grad epilogue
+#pragma unroll
+    for (int n = 0; n < TN; n++) {
+      const int cidx = n0 + wn0 + 32 * n + i;
+      if (cidx > nmax) continue;
+      const float bc = (MODE == 0 && g.bias) ? g.bias[cidx] : 0.f;
+#pragma unroll
+      for (int m = 0; m < TM; m++) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
+          if (r <= mmax) {
+            float v = acc[m][n][q] + bc;
+            if (MODE == 0 && ELU) v = v > 0.f ? v : expm1f(v);
+            Cs[r * g.ldc + cidx] = v;
+          }
+        }
+      }
+    }
+  } else {
+    float* red = reinterpret_cast<float*>(lds);  // [WGM][BN] column partials of the waves along M
+#pragma unroll
+    for (int n = 0; n < TN; n++) {
+      const int cl = wn0 + 32 * n + i;
+      const int cidx = n0 + cl;
+      float cs = 0.f;
+#pragma unroll
+      for (int m = 0; m < TM; m++) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
+          float v = acc[m][n][q];
+          if (r <= mmax && cidx <= nmax) {
+            if (ELU) {
+              const float yv = g.Y[r * g.ldY + cidx];
+              v = yv > 0.f ? v : v * (yv + 1.f);
+            }
+            g.C[r * g.ldc + cidx] = v;
+          } else {
+            v = 0.f;
+          }
+          cs += v;
+        }
+      }
+      cs += __shfl_xor(cs, 32);
+      if (h == 0) red[(wave % WGM) * BN + cl] = cs;
+    }
+    if (g.colpart) {
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        if (n0 + c <= nmax) {
+          float sum = 0.f;
+#pragma unroll
+          for (int w = 0; w < WGM; w++) sum += red[w * BN + c];
+          g.colpart[tm_idx * g.N + n0 + c] = sum;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int KG>
+int launch_x6(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
+  GemmArgs& g = xa.g;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  const int64_t tiles_m = (g.M + BM - 1) / BM;
+  g.tiles = tiles_m * g.tiles_n;
+  if (mode != 2 && mode != 4) xa.slices = 1;
+  if (g.tiles * xa.slices > 0x7fffffff) return HG_ERR_ARG;
+  const dim3 grid((unsigned)(g.tiles * xa.slices)), block(64 * WGM * WGN);
+#define HG_X6(V, MD, E) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E>), grid, block, 0, s, xa)
+  if (mode == 0) {
+    if (vec && elu) HG_X6(true, 0, true);
+    else if (vec) HG_X6(true, 0, false);
+    else if (elu) HG_X6(false, 0, true);
+    else HG_X6(false, 0, false);
+  } else if (mode == 1) {
+    if (vec && elu) HG_X6(true, 1, true);
+    else if (vec) HG_X6(true, 1, false);
+    else if (elu) HG_X6(false, 1, true);
+    else HG_X6(false, 1, false);
+  } else if (mode == 3) {
+    if (vec && elu) HG_X6(true, 3, true);
+    else if (vec) HG_X6(true, 3, false);
+    else if (elu) HG_X6(false, 3, true);
+    else HG_X6(false, 3, false);
+  } else if (mode == 4) {
+    if (vec) HG_X6(true, 4, false);
+    else HG_X6(false, 4, false);
+  } else {
+    HG_X6(false, 2, false);
+  }
+#undef HG_X6
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+constexpr int NTILES = 26;
 // block rows of a tile id (the column-partial row count of mode 1)
 int tile_bm(int tile) {
-  return (tile <= 2 || (tile >= 8 && tile <= 10) || tile == 12 || tile == 13 || tile == 16 || tile == 17) ? 128 : 64;
+  if (tile == 25) return 256;
+  return (tile <= 2 || (tile >= 8 && tile <= 10) || tile == 12 || tile == 13 || tile == 16 || tile == 17 ||
+          (tile >= 20 && tile <= 22) || tile == 24 || tile == 26)
+             ? 128
+             : 64;
 }
 
 }  // namespace
@@ -373,11 +767,13 @@ extern "C" int64_t hg_gemm_colpart_rows(int64_t M, int tile) {
 extern "C" int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                            const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K,
                            int act, int tile, void* stream) {
-  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || (mode != 0 && mode != 1) || act < 0 ||
-      act > 1 || tile < 1 || tile > NTILES)
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || mode < 0 || mode > 3 || mode == 2 ||
+      act < 0 || act > 1 || tile < 1 || tile > NTILES)
     return HG_ERR_ARG;
-  if (mode == 0 && ldb < K) return HG_ERR_ARG;
-  if (mode == 1 && (ldb < N || (act == 1 && (!Y || ldY < N)))) return HG_ERR_ARG;
+  if (mode == 3 && tile < 19) return HG_ERR_ARG;  // the transposed-W input grad: bf16-split tiles only
+  if ((mode == 0 || mode == 3) && ldb < K) return HG_ERR_ARG;
+  if (mode == 1 && ldb < N) return HG_ERR_ARG;
+  if ((mode == 1 || mode == 3) && act == 1 && (!Y || ldY < N)) return HG_ERR_ARG;
   if ((uintptr_t)A % 4 || (uintptr_t)B % 4 || (uintptr_t)C % 4) return HG_ERR_ARG;
   const bool vec = lda % 4 == 0 && (uintptr_t)A % 16 == 0 &&
                    (mode == 1 || (ldb % 4 == 0 && (uintptr_t)B % 16 == 0));
@@ -402,6 +798,47 @@ extern "C" int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B
     case 15: return launch<64, 64, 2, 2, 32, 1, 1>(mode, g, vec, elu, s);
     case 16: return launch<128, 64, 4, 2, 32, 1, 1>(mode, g, vec, elu, s);
     case 17: return launch<128, 128, 2, 4, 32, 1, 1>(mode, g, vec, elu, s);
-    default: return launch<64, 64, 2, 2, 16, 1, 1>(mode, g, vec, elu, s);
+    case 18: return launch<64, 64, 2, 2, 16, 1, 1>(mode, g, vec, elu, s);
+    default: break;
+  }
+  // tiles 20..26: the bf16-split (6-term) kernels, <BM, BN, WGM, WGN, KG>
+  GemmX6Args xa{g, 0, 0, 1};
+  switch (tile) {
+    case 20: return launch_x6<128, 128, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 21: return launch_x6<128, 128, 2, 4, 1>(mode, xa, vec, elu, s);
+    case 22: return launch_x6<128, 64, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 23: return launch_x6<64, 64, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 24: return launch_x6<128, 128, 2, 2, 2>(mode, xa, vec, elu, s);
+    case 25: return launch_x6<256, 128, 4, 2, 1>(mode, xa, vec, elu, s);
+    case 26: return launch_x6<128, 128, 2, 4, 2>(mode, xa, vec, elu, s);
+    default: return launch_x6<64, 128, 2, 2, 1>(mode, xa, vec, elu, s);  // 19
+  }
+}
+
+extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                                 int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile,
+                                 void* stream) {
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || slices < 1 || tile < 19 || tile > NTILES ||
+      K > 0x7fffffff || (kmajor != 0 && kmajor != 1))
+    return HG_ERR_ARG;
+  if (kmajor == 0 && (lda < M || ldb < N)) return HG_ERR_ARG;
+  if (kmajor == 1 && (lda < K || ldb < K)) return HG_ERR_ARG;
+  if (slices > 1 && cstride < M * (int64_t)ldc) return HG_ERR_ARG;
+  if ((uintptr_t)A % 4 || (uintptr_t)B % 4 || (uintptr_t)C % 4) return HG_ERR_ARG;
+  GemmArgs g{A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, nullptr, M, N, (int)K, 0, 0};
+  const int64_t kslice = ((K + slices - 1) / slices + 15) & ~(int64_t)15;
+  GemmX6Args xa{g, kslice, cstride, slices};
+  hipStream_t s = (hipStream_t)stream;
+  const int md = kmajor ? 4 : 2;
+  const bool vec = kmajor && lda % 4 == 0 && ldb % 4 == 0 && (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
+  switch (tile) {
+    case 20: return launch_x6<128, 128, 2, 2, 1>(md, xa, vec, false, s);
+    case 21: return launch_x6<128, 128, 2, 4, 1>(md, xa, vec, false, s);
+    case 22: return launch_x6<128, 64, 2, 2, 1>(md, xa, vec, false, s);
+    case 23: return launch_x6<64, 64, 2, 2, 1>(md, xa, vec, false, s);
+    case 24: return launch_x6<128, 128, 2, 2, 2>(md, xa, vec, false, s);
+    case 25: return launch_x6<256, 128, 4, 2, 1>(md, xa, vec, false, s);
+    case 26: return launch_x6<128, 128, 2, 4, 2>(md, xa, vec, false, s);
+    default: return launch_x6<64, 128, 2, 2, 1>(md, xa, vec, false, s);
   }
 }

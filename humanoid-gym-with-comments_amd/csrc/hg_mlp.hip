@@ -307,10 +307,17 @@ __global__ void __launch_bounds__(256) k_skinny_fwd(const TX* __restrict__ x, in
 constexpr int SK_WAVES = 4;
 constexpr int SK_WROWS = SK_ROWS / SK_WAVES;
 
-template <int N, typename TD>
+// ACT: the layer below's ELU backward fused in — dx becomes that layer's pre-activation gradient
+// dx * elu'(h) (h = this layer's input = the layer below's ELU output; elu' = 1 for h > 0, h + 1
+// otherwise) and the block's column sums of it (that layer's bias-gradient partials, one row per
+// 64-row tile: each wave sums its 16 rows in order, then waves 0 + 1 + 2 + 3).
+template <int N, typename TD, bool ACT = false>
 __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
-                                                             TD* __restrict__ dx, int64_t rows) {
+                                                             TD* __restrict__ dx, int64_t rows,
+                                                             const float* __restrict__ h = nullptr, int64_t ldh = 0,
+                                                             float* __restrict__ colpart = nullptr) {
   __shared__ float g_s[SK_ROWS * N];
+  __shared__ float2 red[ACT ? SK_WAVES - 1 : 1][64];
   const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
   const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
   for (int i = threadIdx.x; i < nr * N; i += 64 * SK_WAVES) g_s[i] = gh[r0 * N + i];
@@ -325,6 +332,7 @@ __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __rest
   }
   __syncthreads();
   const int re = min(nr, SK_WROWS * (wv + 1));
+  float s0 = 0.f, s1 = 0.f;
   for (int r = SK_WROWS * wv; r < re; r++) {
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
@@ -333,7 +341,27 @@ __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __rest
       a0 = fmaf(g, w0[n], a0);
       a1 = fmaf(g, w1[n], a1);
     }
+    if (ACT) {
+      const float2 y = *reinterpret_cast<const float2*>(h + (r0 + r) * ldh + c);
+      a0 = y.x > 0.f ? a0 : a0 * (y.x + 1.f);
+      a1 = y.y > 0.f ? a1 : a1 * (y.y + 1.f);
+      s0 += a0;
+      s1 += a1;
+    }
     st2(dx + (r0 + r) * SK_K + c, make_float2(a0, a1));
+  }
+  if (ACT) {
+    if (wv > 0) red[wv - 1][threadIdx.x & 63] = make_float2(s0, s1);
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+      for (int q = 0; q < SK_WAVES - 1; q++) {
+        const float2 t = red[q][threadIdx.x];
+        s0 += t.x;
+        s1 += t.y;
+      }
+      *reinterpret_cast<float2*>(colpart + (int64_t)blockIdx.x * SK_K + c) = make_float2(s0, s1);
+    }
   }
 }
 
@@ -486,6 +514,26 @@ extern "C" int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k)
 extern "C" int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, const float* W, float* dx,
                                          float* grad_wb, int64_t rows, int n, int k, float* scratch, void* stream) {
   return skinny_backward<float>(gh, h, ldh, W, dx, grad_wb, rows, n, k, scratch, stream);
+}
+
+extern "C" int64_t hg_linear_skinny_colpart_rows(int64_t rows) { return (rows + SK_ROWS - 1) / SK_ROWS; }
+
+extern "C" int hg_linear_skinny_backward_act(const float* gh, const float* h, int64_t ldh, const float* W,
+                                             float* gh_prev, float* colpart, int64_t rows, int n, int k,
+                                             float* scratch, void* stream) {
+  // dW / db partials as hg_linear_skinny_backward (left in scratch), then the fused input gradient
+  if (!gh_prev || !colpart || ldh % 2 != 0 || (uintptr_t)h % 8 != 0 || (uintptr_t)gh_prev % 8 != 0 ||
+      (uintptr_t)colpart % 8 != 0)
+    return HG_ERR_ARG;
+  const int rc = skinny_backward<float>(gh, h, ldh, W, nullptr, nullptr, rows, n, k, scratch, stream);
+  if (rc != HG_OK) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((rows + SK_ROWS - 1) / SK_ROWS));
+#define HG_SK_DXA(NN) \
+  hipLaunchKernelGGL((k_skinny_dx<NN, float, true>), grid, dim3(64 * SK_WAVES), 0, s, gh, W, gh_prev, rows, h, ldh, colpart)
+  HG_SKINNY_SWITCH(n, HG_SK_DXA)
+#undef HG_SK_DXA
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
 extern "C" int hg_linear_skinny_backward_bf16(const float* gh, const uint16_t* h, int64_t ldh, const float* W,

@@ -105,7 +105,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch",
            "hg_mlp_act_backward_bf16", "hg_linear_skinny_forward_bf16", "hg_linear_skinny_backward_bf16",
            "hg_cast_bf16_jobs", "hg_linear_act_forward", "hg_linear_act_tile", "hg_gemm_f32", "hg_gemm_tile",
-           "hg_gemm_colpart_rows", "hg_version"]
+           "hg_gemm_colpart_rows", "hg_gemm_f32_wgrad", "hg_linear_skinny_backward_act", "hg_linear_skinny_colpart_rows", "hg_version"]
 
 _LIB = None
 
@@ -224,10 +224,19 @@ def load_library(path=LIB_PATH):
     L.hg_gemm_f32.restype = ctypes.c_int
     L.hg_gemm_f32.argtypes = [ctypes.c_int, vp, ctypes.c_int64, vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp,
                               ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
+    L.hg_gemm_f32_wgrad.restype = ctypes.c_int
+    L.hg_gemm_f32_wgrad.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    vp]
     L.hg_gemm_tile.restype = ctypes.c_int
     L.hg_gemm_tile.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
     L.hg_gemm_colpart_rows.restype = ctypes.c_int64
     L.hg_gemm_colpart_rows.argtypes = [ctypes.c_int64, ctypes.c_int]
+    L.hg_linear_skinny_backward_act.restype = ctypes.c_int
+    L.hg_linear_skinny_backward_act.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_int,
+                                                ctypes.c_int, vp, vp]
+    L.hg_linear_skinny_colpart_rows.restype = ctypes.c_int64
+    L.hg_linear_skinny_colpart_rows.argtypes = [ctypes.c_int64]
     L.hg_version.restype = ctypes.c_char_p
     L.hg_version.argtypes = []
     return L

@@ -118,6 +118,30 @@ def _skinny_backward(g, h, W, need_dx, red=None):
     return wb[: n * k].view(n, k), wb[n * k:], dx
 
 
+def _skinny_backward_act(g, h, W, red):
+    """The output layer's dW, db (partials into ``red``) and its input gradient through the ELU
+    backward of the layer below (h = that layer's ELU output): (gh_prev, gb_prev), gb_prev's
+    column sums deferred to ``red`` (hg_linear_skinny_backward_act)."""
+    rows, (n, k) = g.shape[0], W.shape
+    L = N.lib()
+    wb = torch.empty(n * k + n, dtype=torch.float32, device=g.device)
+    gh_prev = torch.empty(rows, k, dtype=torch.float32, device=g.device)
+    parts = int(L.hg_linear_skinny_colpart_rows(rows))
+    cp = torch.empty(parts, k, dtype=torch.float32, device=g.device)
+    gb_prev = torch.empty(k, dtype=torch.float32, device=g.device)
+    scratch = torch.empty(int(L.hg_linear_skinny_backward_scratch(rows, n, k)), dtype=torch.float32, device=g.device)
+    rc = L.hg_linear_skinny_backward_act(g.data_ptr(), h.data_ptr(), h.stride(0), W.data_ptr(), gh_prev.data_ptr(),
+                                         cp.data_ptr(), rows, n, k, scratch.data_ptr(), _stream(g.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_linear_skinny_backward_act failed ({rc})")
+    r = red if red is not None else _Reductions()
+    r.add(scratch, wb, n * k + n, scratch.numel() // (n * k + n))
+    r.add(cp, gb_prev, k, parts)
+    if red is None:
+        r.launch(g.device)
+    return wb[: n * k].view(n, k), wb[n * k:], gh_prev, gb_prev
+
+
 # Split-K factors for the weight gradients dW[n, k] = gh[R, n]^T x[R, k] at the 24576-row
 # minibatch: the reduction over R is cut into S row chunks computed as one batched GEMM; the chunk
 # sum runs in the batched end-of-backward column-sum launch.  Small outputs (128 x 256, 256 x 512,
@@ -129,9 +153,28 @@ _DW_SPLIT = {(128, 256): 32, (128, 128): 16, (256, 512): 4, (128, 705): 8, (512,
              (256, 768): 4}
 
 
+# Weight gradients on the bf16-split GEMM (hg_gemm_f32_wgrad, the row-major gh and x staged
+# through an LDS transpose): (n, k) -> [(max rows, tile, split-K slices)], first entry whose row
+# bound covers the call; the slices are summed in the batched end-of-backward column-sum launch.
+_GEMM_DW = {}
+
+
 def _weight_grad(gh, x, red=None):
     rows, n = gh.shape
     k = x.shape[1]
+    route = _route(_GEMM_DW, rows, n, k) if (red is not None and gh.is_contiguous() and x.dim() == 2
+                                             and x.stride(1) == 1) else 0
+    if route:
+        tile, S = route
+        L = N.lib()
+        part = torch.empty(S, n, k, dtype=torch.float32, device=gh.device)
+        rc = L.hg_gemm_f32_wgrad(gh.data_ptr(), gh.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), k, n * k,
+                                 n, k, rows, S, 0, tile, _stream(gh.device))
+        if rc != 0:
+            raise RuntimeError(f"hg_gemm_f32_wgrad failed ({rc})")
+        dw = torch.empty(n, k, dtype=torch.float32, device=gh.device)
+        red.add(part, dw, n * k, S)
+        return dw
     S = _DW_SPLIT.get((n, k), 1) if rows >= 8192 else 1
     if S == 1 or rows % S or not (gh.is_contiguous() and x.is_contiguous()):
         return torch.mm(gh.t(), x)
@@ -183,18 +226,28 @@ def linear_act(h, W, b, elu=True, out=None, tile=0):
 # previous path.  Tiles measured on MI355X per shape against torch (addmm + ELU, mm + the fused
 # ELU-backward pass) and the register-operand kernel above (scripts/gemm_probe.py,
 # profiles/r3_gemm/gemm_probe.jsonl).
-# profiles/r3_gemm/gemm_probe_variants.jsonl (us, torch -> this kernel): forward 24576 rows 705x512
-# 167 -> 160 (tile 17), 256x128 29.5 -> 22.4 (5), 128x128 fused 20.2 -> 15.0 (4); 4096 rows 512x256
-# fused 21 -> 17.5 (5), 705x128 25.3 -> 22.0 (5); the critic's 98304-row value pass 219x768 428 ->
-# 380 (9).  Input gradients (24576 rows, torch mm + ELU-backward pass -> fused): actor 256->512
-# 82.5 -> 71.6, 128->256 33.1 -> 25.0, critic 256->768 115 -> 103, 128->256 33.4 -> 25.1 (tile
-# 16), lin-vel 128->128 22.0 -> 17.7 (4).  512x256 and 705x128 at 24576 rows, 768x256 and 219x768
-# up to 32768 rows stay on torch (equal or faster there).
+# profiles/r3_gemm/gemm_probe_x6.jsonl (us per call, torch addmm + ELU -> this kernel): the
+# bf16-split tiles (>= 19) on the large products — 24576 rows 705x512 174 -> 126 (tile 20),
+# 219x768 102 -> 79 (21), 768x256 82 -> 81 (19), 512x256 60.2 -> 60.3 (22), 705x128 46.5 -> 47.6
+# (23); the critic's 98304-row value pass 219x768 424 -> 305, 768x256 311 -> 264, 256x128 72 ->
+# 56 (20); the f32-MFMA 64x64 tile on the small / rollout products — 24576 rows 256x128 30 -> 22.4,
+# 128x128 (fused register kernel 20.2) -> 15.2; 4096 rows 705x512 35.5 -> 34.3, 512x256 21 ->
+# 17.5, 705x128 26 -> 22.5.  Equal-time routes still pay: the separate ELU pass is gone.
 _BIG = 1 << 40
-_GEMM_FWD = {(705, 512): [(8192, 0), (_BIG, 17)], (512, 256): [(8192, 5)], (256, 128): [(8192, 0), (_BIG, 5)],
-             (705, 128): [(8192, 5)], (128, 128): [(8192, 0), (_BIG, 4)], (219, 768): [(32768, 0), (_BIG, 9)]}
-_GEMM_DX = {(256, 512): [(_BIG, 16)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 16)], (128, 128): [(_BIG, 4)]}
+X6_TILE0 = 19  # tiles >= 19: the bf16-split (6-term) kernels of hg_gemm_f32
+_GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG, 22)],
+             (256, 128): [(8192, 0), (32768, 5), (_BIG, 20)], (705, 128): [(8192, 5), (_BIG, 23)],
+             (128, 128): [(8192, 0), (_BIG, 5)], (219, 768): [(32768, 21), (_BIG, 20)],
+             (768, 256): [(32768, 19), (_BIG, 20)]}
+# input gradients (24576 rows, torch mm + ELU-backward pass -> fused; gemm_probe_x6.jsonl): 256->512
+# 84.7 -> 72.9 (bf16-split tile 22), 256->768 118 -> 103 (f32 tile 16), 128->256 33 -> 24.8 (16),
+# 128->128 22 -> 17.9 (f32 tile 5).  Weight gradients stay on hipBLASLt: the bf16-split kernel with
+# split-K slices (LDS-transposed staging of the row-major gh and x, or explicit transposes) was
+# 0.57-0.94x of its tuned TN kernels on every shape.
+_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 16)], (128, 128): [(_BIG, 5)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
+# the output layer's input gradient with the ELU backward of the layer below fused in
+SKINNY_ACT = os.environ.get("HG_SKINNY_ACT", "1") != "0"
 
 
 def _route(table, rows, k, n):
@@ -241,7 +294,11 @@ def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0):
     out = torch.empty(rows, n, dtype=torch.float32, device=gh.device)
     parts = int(L.hg_gemm_colpart_rows(rows, tile))
     cp = torch.empty(parts, n, dtype=torch.float32, device=gh.device)
-    rc = L.hg_gemm_f32(1, gh.data_ptr(), gh.stride(0), W.data_ptr(), W.stride(0), None, y_prev.data_ptr(),
+    # W read as is ([n_i, k_i], n-contiguous in the reduction index): the f32 tiles stage it with
+    # coalesced scalar loads, the bf16-split tiles through an LDS transpose (mode 3 with a W^T copy
+    # measured no faster, profiles/r3_gemm/gemm_probe_x6.jsonl)
+    mode, B = 1, W
+    rc = L.hg_gemm_f32(mode, gh.data_ptr(), gh.stride(0), B.data_ptr(), B.stride(0), None, y_prev.data_ptr(),
                        y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
                        _stream(gh.device))
     if rc != 0:
@@ -310,8 +367,14 @@ class _MLP(torch.autograd.Function):
             need_dx = i > 0 or ctx.needs_input_grad[0]
             gnext = None
             if i == n - 1 and _skinny_ok(ins[i], Ws[i]):
-                # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
-                grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx, red)
+                if i > 0 and SKINNY_ACT:
+                    # output layer: dW, db and the layer below's pre-activation gradient + bias
+                    # gradient partials (its ELU backward fused into the skinny dX pass)
+                    grads[2 * i], grads[2 * i + 1], gh_prev, gb_prev = _skinny_backward_act(g, ins[i], Ws[i], red)
+                    pre = (gh_prev, gb_prev)
+                else:
+                    # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
+                    grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx, red)
             else:
                 if pre is not None:
                     gh, gb = pre

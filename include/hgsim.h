@@ -388,6 +388,15 @@ int hg_linear_skinny_backward(const float* gh, const float* h, int64_t ldh, cons
                               float* grad_wb, int64_t rows, int n, int k,
                               float* scratch /* >= hg_linear_skinny_backward_scratch() floats */, void* stream);
 int64_t hg_linear_skinny_backward_scratch(int64_t rows, int n, int k);
+/* hg_linear_skinny_backward (dW / db partials left in scratch for hg_colsum_jobs) with the input
+ * gradient fused with the ELU backward of the layer below (h is that layer's ELU output):
+ * gh_prev[r][c] = (sum_j gh[r][j] W[j][c]) * (h[r][c] > 0 ? 1 : h[r][c] + 1), and colpart
+ * [hg_linear_skinny_colpart_rows(rows), k] = its column sums per 64-row tile (the layer below's
+ * bias-gradient partials, fixed order).  Replaces the skinny dX pass + hg_mlp_act_backward. */
+int hg_linear_skinny_backward_act(const float* gh, const float* h, int64_t ldh, const float* W, float* gh_prev,
+                                  float* colpart, int64_t rows, int n, int k,
+                                  float* scratch /* >= hg_linear_skinny_backward_scratch() floats */, void* stream);
+int64_t hg_linear_skinny_colpart_rows(int64_t rows);
 /* bf16 policy (config 5, policy_dtype "bf16"): the same three passes with the activations,
  * activation gradients and hidden-layer inputs in bf16 (uint16_t bit patterns, round-to-nearest-
  * even), all accumulation, bias/weight-gradient partials, W of the skinny layer and its output y /
@@ -427,16 +436,28 @@ int hg_linear_act_tile(int64_t rows, int n, int k);
  * backward, the input-gradient mm + the next lower layer's ELU backward + its bias-gradient sum):
  *   mode 0 (forward):    C[r][c] = act(sum_k A[r][k] B[c][k] + bias[c])      A [M, K] (lda), B [N, K] (ldb)
  *   mode 1 (input grad): C[r][c] = (sum_k A[r][k] B[k][c]) * elu'(Y[r][c])  A [M, K] (lda), B [K, N] (ldb)
+ *   mode 3 (input grad, B given transposed: B [N, K] (ldb), bf16-split tiles only), as mode 1
  *     with elu'(from the ELU output y) = 1 for y > 0, y + 1 otherwise (act 1; act 0: no factor,
  *     Y unused); colpart (may be NULL) receives the column sums of C per row tile,
  *     [hg_gemm_colpart_rows(M, tile), N], reduced later in fixed order (hg_colsum_jobs).
- * tile 1..4 = block tiles 128x128, 128x64, 64x128, 64x64 (hg_gemm_tile picks one); rows of A,
- * B, C 4-byte aligned (16-byte rows take the vector-load staging).  One launch, no host
- * synchronisation, exact f32 products with f32 accumulation (v_mfma_f32_32x32x2_f32). */
+ * tile 1..18 = f32-MFMA block tiles (exact f32 products, f32 accumulation, v_mfma_f32_32x32x2_f32);
+ * tile 19..26 = the same product on the bf16 matrix cores with every f32 operand split exactly
+ * into three bf16 terms and the six products of total order <= 2 accumulated in f32
+ * (v_mfma_f32_32x32x16_bf16; error per element below torch's f32 GEMM's, csrc/hg_gemm.hip);
+ * hg_gemm_tile picks one.  Rows of A, B, C 4-byte aligned (16-byte rows take the vector-load
+ * staging).  One launch, no host synchronisation. */
 int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, const float* Y,
                 int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K, int act, int tile,
                 void* stream);
 int hg_gemm_tile(int mode, int64_t M, int N, int K);
+/* Weight gradient (replaces the dW = gh^T x matmuls of each Linear's backward): split-K slices
+ * s < slices of the reduction over K rows, C + s * cstride [M, N] (ldc) =
+ * sum_{k in slice s} A(m, k) B(n, k), with kmajor 0: A [K, M] (lda), B [K, N] (ldb) (the row-major
+ * activations / gradients themselves), kmajor 1: A [M, K], B [N, K] (their transposes) — the
+ * slices summed later in fixed order (hg_colsum_jobs).  tile 19..26 (the bf16-split kernels of
+ * hg_gemm_f32). */
+int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                      int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile, void* stream);
 int64_t hg_gemm_colpart_rows(int64_t M, int tile);
 
 /* library build info */

@@ -23,7 +23,7 @@ L = N.lib()
 print(json.dumps({"tunableop_table_loaded": use_tuned_gemms()}))
 torch.manual_seed(0)
 ITERS = int(os.environ.get("ITERS", 30))
-TILES = [int(t) for t in os.environ.get("TILES", "4,5,8,9,11,12,13,14,15,16,17,18").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "5,16,17,19,20,21,22,23,24,25,26").split(",")]
 
 FWD = [("actor0_mb", 24576, 705, 512), ("actor1_mb", 24576, 512, 256), ("actor2_mb", 24576, 256, 128),
        ("linvel0_mb", 24576, 705, 128), ("linvel1_mb", 24576, 128, 128),
@@ -67,12 +67,14 @@ for tag, rows, k, n in FWD:
     W = torch.randn(n, k, device=dev) * (1.0 / k ** 0.5)
     b = torch.randn(n, device=dev) * 0.1
     ref = F.elu(torch.addmm(b.double(), x.double(), W.double().t()))
+    scale = x.double().abs() @ W.double().abs().t() + b.double().abs()
     err_t = (F.elu(torch.addmm(b, x, W.t())).double() - ref).abs().max().item()
     t_torch = timeit(lambda: F.elu(torch.addmm(b, x, W.t())))
     t_gemm = timeit(lambda: torch.addmm(b, x, W.t()))
+    rec_torch_relerr = ((F.elu(torch.addmm(b, x, W.t())).double() - ref).abs() / scale).max().item()
     flop = 2.0 * rows * k * n
     rec = {"shape": tag, "mode": 0, "rows": rows, "k": k, "n": n, "torch_us": round(t_torch, 2),
-           "torch_gemm_only_us": round(t_gemm, 2), "torch_err": err_t,
+           "torch_gemm_only_us": round(t_gemm, 2), "torch_err": err_t, "torch_relerr": rec_torch_relerr,
            "auto_tile": int(L.hg_gemm_tile(0, rows, n, k))}
     best = None
     for tile in TILES:
@@ -80,6 +82,7 @@ for tag, rows, k, n in FWD:
         gemm(0, x, W, b, None, y, None, rows, n, k, 1, tile)
         torch.cuda.synchronize()
         rec[f"tile{tile}_err"] = (y.double() - ref).abs().max().item()
+        rec[f"tile{tile}_relerr"] = ((y.double() - ref).abs() / scale).max().item()
         t = timeit(lambda: gemm(0, x, W, b, None, y, None, rows, n, k, 1, tile))
         rec[f"tile{tile}_us"] = round(t, 2)
         rec[f"tile{tile}_tflops"] = round(flop / t * 1e-6, 1)
@@ -115,15 +118,23 @@ for tag, rows, kr, n in DX:
     rec = {"shape": tag, "mode": 1, "rows": rows, "k": kr, "n": n, "torch_us": round(t_torch, 2), "torch_err": err_t,
            "torch_bias_err": (gb.double() - ref_cs).abs().max().item(), "auto_tile": int(L.hg_gemm_tile(1, rows, n, kr))}
     best = None
+    Wt = W.t().contiguous()
+    rec["wt_transpose_us"] = round(timeit(lambda: W.t().contiguous()), 2)
     for tile in TILES:
         parts = int(L.hg_gemm_colpart_rows(rows, tile))
         cp = torch.empty(parts, n, device=dev)
         out = torch.empty(rows, n, device=dev)
-        gemm(1, g, W, None, y, out, cp, rows, n, kr, 1, tile)
+        md, BB = (3, Wt) if tile >= 19 else (1, W)
+        if tile >= 19:  # the transposing staging of W as is (mode 1) beside the W^T form
+            gemm(1, g, W, None, y, out, cp, rows, n, kr, 1, tile)
+            torch.cuda.synchronize()
+            rec[f"tile{tile}_m1_us"] = round(timeit(lambda: gemm(1, g, W, None, y, out, cp, rows, n, kr, 1, tile)), 2)
+            rec[f"tile{tile}_m1_err"] = (out.double() - ref).abs().max().item()
+        gemm(md, g, BB, None, y, out, cp, rows, n, kr, 1, tile)
         torch.cuda.synchronize()
         rec[f"tile{tile}_err"] = (out.double() - ref).abs().max().item()
         rec[f"tile{tile}_bias_err"] = (cp.double().sum(0) - ref_cs).abs().max().item()
-        t = timeit(lambda: gemm(1, g, W, None, y, out, cp, rows, n, kr, 1, tile))
+        t = timeit(lambda: gemm(md, g, BB, None, y, out, cp, rows, n, kr, 1, tile))
         rec[f"tile{tile}_us"] = round(t, 2)
         rec[f"tile{tile}_tflops"] = round(flop / t * 1e-6, 1)
         if best is None or t < best[1]:
@@ -132,4 +143,62 @@ for tag, rows, kr, n in DX:
     rec["speedup_vs_torch"] = round(t_torch / best[1], 3)
     print(json.dumps(rec), flush=True)
     summary[tag] = (rec["torch_us"], rec["best_us"], rec["best_tile"], rec.get(f"tile{rec['auto_tile']}_us"))
+# weight gradients dW [n, k] = gh[R, n]^T x[R, k] (R = 24576 minibatch rows): torch's split-K bmm
+# path of hg_mlp._weight_grad + the chunk sum, against hg_gemm_f32_wgrad slices + the slice sum
+DW = [("actor_dw0", 24576, 512, 705), ("actor_dw1", 24576, 256, 512), ("actor_dw2", 24576, 128, 256),
+      ("critic_dw0", 24576, 768, 219), ("critic_dw1", 24576, 256, 768), ("critic_dw2", 24576, 128, 256),
+      ("linvel_dw0", 24576, 128, 705), ("linvel_dw1", 24576, 128, 128)]
+from humanoid.algo.ppo import hg_mlp  # noqa: E402
+DW_TILES = [int(t) for t in os.environ.get("DW_TILES", "20,22,26").split(",")]
+for tag, rows, n, k in DW:
+    gh = torch.randn(rows, n, device=dev)
+    x = torch.randn(rows, k, device=dev)
+    ref = gh.double().t() @ x.double()
+    scale = gh.double().abs().t() @ x.double().abs()
+    red = hg_mlp._Reductions()
+
+    def torch_path():
+        dw = hg_mlp._weight_grad(gh, x, red)
+        red.launch(dev)
+        return dw
+
+    dw_t = torch_path()
+    torch.cuda.synchronize()
+    t_torch = timeit(torch_path)
+    rec = {"shape": tag, "mode": 2, "rows": rows, "n": n, "k": k, "torch_us": round(t_torch, 2),
+           "torch_err": (dw_t.double() - ref).abs().max().item(),
+           "torch_relerr": ((dw_t.double() - ref).abs() / scale).max().item()}
+    best = None
+    for kmajor in (0, 1):
+        for tile in DW_TILES:
+            for S in (16, 32, 64):
+                part = torch.empty(S, n, k, device=dev)
+                dw = torch.empty(n, k, device=dev)
+
+                def ours():
+                    if kmajor:
+                        A, B = gh.t().contiguous(), x.t().contiguous()  # the transposes, timed with the product
+                    else:
+                        A, B = gh, x
+                    rc = L.hg_gemm_f32_wgrad(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), part.data_ptr(), k,
+                                             n * k, n, k, rows, S, kmajor, tile, stream())
+                    if rc != 0:
+                        raise RuntimeError(f"hg_gemm_f32_wgrad rc={rc}")
+                    red.add(part, dw, n * k, S)
+                    red.launch(dev)
+                    return dw
+
+                out = ours()
+                torch.cuda.synchronize()
+                t = timeit(ours)
+                key = f"km{kmajor}_tile{tile}_S{S}"
+                rec[key + "_us"] = round(t, 2)
+                rec[key + "_relerr"] = ((out.double() - ref).abs() / scale).max().item()
+                if best is None or t < best[1]:
+                    best = (key, t)
+    rec["transpose_us"] = round(timeit(lambda: (gh.t().contiguous(), x.t().contiguous())), 2)
+    rec["best"], rec["best_us"] = best[0], round(best[1], 2)
+    rec["best_tile"] = best[0]
+    rec["speedup_vs_torch"] = round(t_torch / best[1], 3)
+    print(json.dumps(rec), flush=True)
 print(json.dumps({"summary_torch_best_tile_auto": summary}))

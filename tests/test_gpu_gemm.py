@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 pytestmark = pytest.mark.gpu
 
 REL = 1e-6
-TILES = list(range(1, 19))
+TILES = list(range(1, 27))  # 1..18 f32 MFMA, 19..26 bf16-split (6-term)
 
 
 def _need_gpu():
@@ -85,12 +85,14 @@ def test_gemm_input_grad_matches_fp64(rows, kr, n):
     bound = REL * (g.double().abs() @ W.double().abs())
     cs_ref = ref.sum(0)
     cs_bound = (bound.sum(0) + REL * ref.abs().sum(0)) * 2
+    Wt = W.t().contiguous()
     for tile in TILES:
         parts = int(L.hg_gemm_colpart_rows(rows, tile))
         cp = torch.full((parts, n), float("nan"), device=dev)
         out = torch.empty(rows, n, device=dev)
-        rc = L.hg_gemm_f32(1, g.data_ptr(), g.stride(0), W.data_ptr(), W.stride(0), None, y.data_ptr(), y.stride(0),
-                           out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile, _stream())
+        md, BB = (1, W) if tile < 19 or tile % 2 else (3, Wt)  # the bf16-split tiles take both B layouts
+        rc = L.hg_gemm_f32(md, g.data_ptr(), g.stride(0), BB.data_ptr(), BB.stride(0), None, y.data_ptr(),
+                           y.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile, _stream())
         assert rc == 0
         err = (out.double() - ref).abs()
         assert (err <= bound).all(), f"tile {tile}: worst ratio {(err / bound).max().item():.3f}"
@@ -98,10 +100,38 @@ def test_gemm_input_grad_matches_fp64(rows, kr, n):
         assert (cs_err <= cs_bound).all(), f"tile {tile}: bias worst ratio {(cs_err / cs_bound).max().item():.3f}"
         # act 0: the plain product, no colpart
         out0 = torch.empty(rows, n, device=dev)
-        rc = L.hg_gemm_f32(1, g.data_ptr(), g.stride(0), W.data_ptr(), W.stride(0), None, None, 0,
+        rc = L.hg_gemm_f32(md, g.data_ptr(), g.stride(0), BB.data_ptr(), BB.stride(0), None, None, 0,
                            out0.data_ptr(), out0.stride(0), None, rows, n, kr, 0, tile, _stream())
         assert rc == 0
         assert ((out0.double() - d).abs() <= bound).all()
+
+
+# (rows = reduction, n, k, slices): weight gradients dW [n, k] = gh^T x, split-K slices summed here
+WG_CASES = [(24576, 512, 705, 4), (777, 128, 219, 3), (33, 5, 7, 1), (100, 130, 66, 2), (4096, 256, 512, 16)]
+
+
+@pytest.mark.parametrize("rows,n,k,S", WG_CASES)
+def test_gemm_wgrad_matches_fp64(rows, n, k, S):
+    _need_gpu()
+    from humanoid import _native as N
+    L = N.lib()
+    torch.manual_seed(rows + n + k + S)
+    dev = "cuda:0"
+    gh = torch.randn(rows, n, device=dev)
+    x = torch.randn(rows, k, device=dev)
+    ref = gh.double().t() @ x.double()
+    bound = REL * (gh.double().abs().t() @ x.double().abs()) * 1.5  # + the slice sum's roundings
+    ght, xt = gh.t().contiguous(), x.t().contiguous()
+    for kmajor, (A, B) in ((0, (gh, x)), (1, (ght, xt))):
+        for tile in range(19, 27):
+            part = torch.full((S, n, k + 2), 5.0, device=dev)  # strided output: the pad columns untouched
+            rc = L.hg_gemm_f32_wgrad(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), part.data_ptr(), k + 2,
+                                     n * (k + 2), n, k, rows, S, kmajor, tile, _stream())
+            assert rc == 0
+            dw = part[:, :, :k].double().sum(0)
+            err = (dw - ref).abs()
+            assert (err <= bound).all(), f"kmajor {kmajor} tile {tile}: worst ratio {(err / bound).max().item():.3f}"
+            assert (part[:, :, k:] == 5.0).all()
 
 
 def test_gemm_rejects_bad_arguments():
