@@ -409,7 +409,12 @@ def main():
                                 "XBot-L heightfield terrain 2100x2100, 4096 envs/GPU, PPO 24-step rollout (config 3)"),
                    "envs_per_gpu": args.envs, "num_steps_per_env": args.T, "parallelism": f"dp{world}",
                    "ppo": "2 epochs x 4 minibatches, actor 705-512-256-128-12, critic 219-768-256-128-1",
-                   "gemm_table": "tuning/tunableop_mi355x_f32.csv" if tuned else None},
+                   "gemm_table": "tuning/tunableop_mi355x_f32.csv" if tuned else None,
+                   "gemm": ("f32 operands and accumulation; the large hidden-layer forwards run on the bf16 matrix "
+                            "cores as exact three-way bf16 splits of each f32 operand (six partial products, f32 "
+                            "accumulation; error per element below torch's f32 GEMM's, tests/test_gpu_gemm.py), "
+                            "the other products on f32 MFMA (own kernels) or hipBLASLt f32"
+                            if not c5 else "bf16 policy (config 5)")},
         "roofline": roofline,
         "collection_time_s": round(runner.last_iteration_stats.get("collection_time", float("nan")), 4),
         "learn_time_s": round(runner.last_iteration_stats.get("learn_time", float("nan")), 4),

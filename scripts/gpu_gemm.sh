@@ -10,6 +10,7 @@ python -c "
 import json
 for l in open('gpurun_out/gemm_probe.jsonl'):
     d=json.loads(l)
+    if 'shape' in d and d['mode'] == 5: print(d['shape'], ' '.join('%s:%.1f'%(kk[:-3],vv) for kk,vv in d.items() if kk.endswith('_us'))); continue
     if 'shape' in d and d['mode'] == 2: print(d['shape'], 'torch', d['torch_us'], 'best', d['best_us'], d['best'], 'x', d['speedup_vs_torch'], 'rel', d['torch_relerr'], d[d['best']+'_relerr'], 'transp', d['transpose_us'], ' '.join('%s:%.1f'%(kk[:-3],vv) for kk,vv in d.items() if kk.endswith('_us') and kk.startswith('km'))); continue
     if 'shape' in d: print(d['shape'], 'torch', d['torch_us'], 'best', d['best_us'], 'tile', d['best_tile'], 'x', d['speedup_vs_torch'], 'err', '%.2e'%d['tile%d_err'%d['best_tile']], 'terr', '%.2e'%d['torch_err'], 'rel', d.get('tile%d_relerr'%d['best_tile']), d.get('torch_relerr'), ' '.join('%d:%.1f'%(t,d['tile%d_us'%t]) for t in range(1,27) if 'tile%d_us'%t in d), 'm1', ' '.join('%d:%.1f'%(t,d['tile%d_m1_us'%t]) for t in range(19,27) if 'tile%d_m1_us'%t in d))
 "
