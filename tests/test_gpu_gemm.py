@@ -195,3 +195,39 @@ def test_mlp_backward_with_fused_gemm_matches_autograd():
         assert any(c[0] == "g" for c in calls), calls
     if hg_mlp.GEMM and hg_mlp._GEMM_FWD:
         assert any(c[0] == "f" for c in calls), calls
+
+
+@pytest.mark.parametrize("rows,n", [(24576, 12), (777, 3), (64, 1), (65, 12)])
+def test_skinny_backward_act_matches_fp64(rows, n):
+    """hg_linear_skinny_backward_act: the output layer's dW / db partials and its input gradient
+    through the ELU backward of the layer below (h = that layer's ELU output), with that layer's
+    bias-gradient partials, against fp64."""
+    _need_gpu()
+    from humanoid import _native as N
+    L = N.lib()
+    torch.manual_seed(rows + n)
+    dev, k = "cuda:0", 128
+    g = torch.randn(rows, n, device=dev)
+    h = F.elu(torch.randn(rows, k, device=dev))
+    W = torch.randn(n, k, device=dev) / k ** 0.5
+    gh = torch.empty(rows, k, device=dev)
+    parts = int(L.hg_linear_skinny_colpart_rows(rows))
+    cp = torch.empty(parts, k, device=dev)
+    scratch = torch.empty(int(L.hg_linear_skinny_backward_scratch(rows, n, k)), device=dev)
+    rc = L.hg_linear_skinny_backward_act(g.data_ptr(), h.data_ptr(), h.stride(0), W.data_ptr(), gh.data_ptr(),
+                                         cp.data_ptr(), rows, n, k, scratch.data_ptr(), _stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    d = g.double() @ W.double()
+    ref = torch.where(h.double() > 0, d, d * (h.double() + 1))
+    bound = REL * (g.double().abs() @ W.double().abs()) + 1e-12
+    assert ((gh.double() - ref).abs() <= bound).all()
+    cs_bound = 2 * (bound.sum(0) + REL * ref.abs().sum(0))
+    assert ((cp.double().sum(0) - ref.sum(0)).abs() <= cs_bound).all()
+    tiles = scratch.numel() // (n * k + n)
+    wb = scratch.view(tiles, n * k + n)[:tiles].double().sum(0)
+    dw_ref = (g.double().t() @ h.double()).reshape(-1)
+    db_ref = g.double().sum(0)
+    dw_bound = REL * (g.double().abs().t() @ h.double().abs()).reshape(-1) * 2 + 1e-9
+    assert ((wb[: n * k] - dw_ref).abs() <= dw_bound).all()
+    assert ((wb[n * k:] - db_ref).abs() <= REL * g.double().abs().sum(0) * 2 + 1e-9).all()
