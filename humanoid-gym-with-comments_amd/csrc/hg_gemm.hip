@@ -539,7 +539,10 @@ struct X6Op {
   }
 };
 
-template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU>
+// BIMG: B comes as a pre-split image (hg_gemm_x6_image): per (column tile, 16 KG-deep chunk) the
+// three planes in exactly the LDS order, copied by LDS-DMA (global_load_lds, 1 KB per wave
+// instruction, lane-linear) with no register staging, split or LDS write pass for B.
+template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, bool BIMG = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
@@ -550,7 +553,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   static_assert(2 * STAGE * 4 >= WGM * BN, "epilogue reduction buffer fits the staging LDS");
   constexpr bool AKC = MODE != 2, BKC = MODE == 0 || MODE == 3 || MODE == 4;
   constexpr int SCA = AKC ? 0 : X6StageT<BM, KG, 64 * WGM * WGN>::SCRATCH;
-  constexpr int SCB = BKC ? 0 : X6StageT<BN, KG, 64 * WGM * WGN>::SCRATCH;
+  static_assert(!BIMG || MODE == 0 || MODE == 1, "B image: forward and input-grad epilogues");
+  constexpr int SCB = (BKC || BIMG) ? 0 : X6StageT<BN, KG, 64 * WGM * WGN>::SCRATCH;
   constexpr int SCS = (SCA + SCB + 3) / 4;  // scratch in 16-byte slots, after the two stages
   __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE + SCS];
   const GemmArgs& g = xa.g;
@@ -587,23 +591,35 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   const int64_t nk = kend - kbeg;
   const int64_t kfull = kbeg + (nk & ~(int64_t)(BK - 1));
   const int nchunks = (int)((nk + BK - 1) / BK);
+  // B image chunk c of this column tile: 3 PB slots = BIMG_KB instructions of 64 lanes x 16 B
+  constexpr int BIMG_KB = 3 * PB / 64;
+  const bf16x8* bimg = reinterpret_cast<const bf16x8*>(g.B) + (tile % g.tiles_n) * (int64_t)nchunks * (3 * PB);
+  auto dma_b = [&](int c, bf16x8* S) {
+    const bf16x8* src = bimg + (int64_t)c * (3 * PB) + lane;
+    for (int q = wave; q < BIMG_KB; q += WGM * WGN)
+      __builtin_amdgcn_global_load_lds(src + q * 64, (__attribute__((address_space(3))) void*)(S + 3 * PA + q * 64), 16,
+                                       0, 0);
+  };
   auto load = [&](int64_t kc) {
     const bool tail = kc + BK > kfull;
     sa.load(g.A, g.lda, m0, mmax, kc, kend, tail, tid);
-    sb.load(g.B, g.ldb, n0, nmax, kc, kend, tail, tid);
+    if (!BIMG) sb.load(g.B, g.ldb, n0, nmax, kc, kend, tail, tid);
   };
   auto store = [&](bf16x8* S) {
     if (AKC) sa.kc.store(S, tid);
     else sa.rt.to_scratch(scA, tid);
-    if (BKC) sb.kc.store(S + 3 * PA, tid);
-    else sb.rt.to_scratch(scB, tid);
-    if (!AKC || !BKC) {
+    if (!BIMG) {
+      if (BKC) sb.kc.store(S + 3 * PA, tid);
+      else sb.rt.to_scratch(scB, tid);
+    }
+    if (!AKC || (!BKC && !BIMG)) {
       __syncthreads();
       if (!AKC) sa.rt.to_planes(S, scA, tid);
-      if (!BKC) sb.rt.to_planes(S + 3 * PA, scB, tid);
+      if (!BKC && !BIMG) sb.rt.to_planes(S + 3 * PA, scB, tid);
     }
   };
   if (nchunks > 0) {
+    if (BIMG) dma_b(0, lds);
     load(kbeg);
     store(lds);
   }
@@ -612,7 +628,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
     const bf16x8* cur = lds + (c & 1) * STAGE;
     bf16x8* nxt = lds + ((c + 1) & 1) * STAGE;
     const bool more = c + 1 < nchunks;
-    if (more) load(kbeg + (int64_t)(c + 1) * BK);
+    if (more) {
+      if (BIMG) dma_b(c + 1, nxt);
+      load(kbeg + (int64_t)(c + 1) * BK);
+    }
 #pragma unroll
     for (int kg = 0; kg < KG; kg++) {
       bf16x8 a[3][TM], b[3][TN];
@@ -702,6 +721,77 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   }
 }
 
+// the pre-split B images of a list of weights, one launch: block (job, column tile tn, chunk c),
+// the (column r, 8-k piece) items of that chunk over its 256 threads; element (n, k) of B is
+// W[n ldw + k] (trans 0: W rows are B rows, the forward / transposed input-grad operand) or
+// W[k ldw + n] (trans 1: the input-grad operand W[K][N]); past N or K the image holds 0
+constexpr int IMG_MAX = 16;
+struct ImageJobs {
+  const float* W[IMG_MAX];
+  bf16x8* img[IMG_MAX];
+  int64_t ldw[IMG_MAX];
+  int trans[IMG_MAX], N[IMG_MAX], K[IMG_MAX], bn[IMG_MAX], kg[IMG_MAX], chunks[IMG_MAX];
+  int block0[IMG_MAX + 1];
+  int njobs;
+};
+
+__global__ void __launch_bounds__(256) k_x6_image_jobs(ImageJobs J) {
+  const int bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < J.njobs && bid >= J.block0[j + 1]) j++;
+  const int lb = bid - J.block0[j];
+  const int chunks = J.chunks[j], BN = J.bn[j], KG = J.kg[j];
+  const int tn = lb / chunks, c = lb % chunks;
+  const int PB = BN * 2 * KG;
+  const float* __restrict__ W = J.W[j];
+  const int64_t ldw = J.ldw[j];
+  const int N = J.N[j], K = J.K[j];
+  const bool trans = J.trans[j] != 0;
+  bf16x8* base = J.img[j] + (int64_t)lb * (3 * PB);
+  for (int idx = threadIdx.x; idx < PB; idx += 256) {
+    const int r = idx % BN, piece = idx / BN;
+    const int n = tn * BN + r;
+    const int k0 = c * 16 * KG + 8 * piece;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int k = k0 + q;
+      v[q] = (n < N && k < K) ? (trans ? W[(int64_t)k * ldw + n] : W[(int64_t)n * ldw + k]) : 0.f;
+    }
+    bf16x8 x0, x1, x2;
+    split3x8(v, x0, x1, x2);
+    const int sl = x6_slot(BN, piece >> 1, r, piece & 1);
+    base[sl] = x0;
+    base[PB + sl] = x1;
+    base[2 * PB + sl] = x2;
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int KG>
+int launch_x6_img(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
+  GemmArgs& g = xa.g;
+  g.tiles_n = (g.N + BN - 1) / BN;
+  const int64_t tiles_m = (g.M + BM - 1) / BM;
+  g.tiles = tiles_m * g.tiles_n;
+  xa.slices = 1;
+  if (g.tiles > 0x7fffffff) return HG_ERR_ARG;
+  const dim3 grid((unsigned)g.tiles), block(64 * WGM * WGN);
+#define HG_X6I(V, MD, E) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, true>), grid, block, 0, s, xa)
+  if (mode == 0) {
+    if (vec && elu) HG_X6I(true, 0, true);
+    else if (vec) HG_X6I(true, 0, false);
+    else if (elu) HG_X6I(false, 0, true);
+    else HG_X6I(false, 0, false);
+  } else {
+    if (vec && elu) HG_X6I(true, 1, true);
+    else if (vec) HG_X6I(true, 1, false);
+    else if (elu) HG_X6I(false, 1, true);
+    else HG_X6I(false, 1, false);
+  }
+#undef HG_X6I
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
 template <int BM, int BN, int WGM, int WGN, int KG>
 int launch_x6(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
   GemmArgs& g = xa.g;
@@ -747,7 +837,85 @@ int tile_bm(int tile) {
              : 64;
 }
 
+// (BN, KG) of an x6 tile id
+void x6_bn_kg(int tile, int& bn, int& kg) {
+  bn = (tile == 22 || tile == 23) ? 64 : 128;
+  kg = (tile == 24 || tile == 26) ? 2 : 1;
+}
+
 }  // namespace
+
+extern "C" int64_t hg_gemm_x6_image_bytes(int N, int K, int tile) {
+  if (N <= 0 || K <= 0 || tile < 19 || tile > NTILES) return -1;
+  int bn, kg;
+  x6_bn_kg(tile, bn, kg);
+  const int64_t tiles_n = (N + bn - 1) / bn, chunks = (K + 16 * kg - 1) / (16 * kg);
+  return tiles_n * chunks * 3 * (bn * 2 * kg) * 16;
+}
+
+extern "C" int hg_gemm_x6_image_jobs(const float* const* W, const int64_t* ldw, const int* trans, const int* N,
+                                     const int* K, const int* tile, void* const* img, int njobs, void* stream) {
+  if (njobs <= 0) return HG_OK;
+  if (njobs > IMG_MAX || !W || !ldw || !trans || !N || !K || !tile || !img) return HG_ERR_ARG;
+  ImageJobs J;
+  J.njobs = njobs;
+  int64_t blocks = 0;
+  for (int j = 0; j < njobs; j++) {
+    if (!W[j] || !img[j] || N[j] <= 0 || K[j] <= 0 || tile[j] < 19 || tile[j] > NTILES ||
+        (trans[j] != 0 && trans[j] != 1))
+      return HG_ERR_ARG;
+    if ((trans[j] == 0 && ldw[j] < K[j]) || (trans[j] == 1 && ldw[j] < N[j])) return HG_ERR_ARG;
+    if ((uintptr_t)W[j] % 4 || (uintptr_t)img[j] % 16) return HG_ERR_ARG;
+    int bn, kg;
+    x6_bn_kg(tile[j], bn, kg);
+    J.W[j] = W[j];
+    J.img[j] = reinterpret_cast<bf16x8*>(img[j]);
+    J.ldw[j] = ldw[j];
+    J.trans[j] = trans[j];
+    J.N[j] = N[j];
+    J.K[j] = K[j];
+    J.bn[j] = bn;
+    J.kg[j] = kg;
+    J.chunks[j] = (K[j] + 16 * kg - 1) / (16 * kg);
+    J.block0[j] = (int)blocks;
+    blocks += (int64_t)J.chunks[j] * ((N[j] + bn - 1) / bn);
+    if (blocks > (int64_t)1 << 30) return HG_ERR_ARG;
+  }
+  J.block0[njobs] = (int)blocks;
+  hipLaunchKernelGGL(k_x6_image_jobs, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+extern "C" int hg_gemm_x6_image(const float* W, int64_t ldw, int trans, int N, int K, int tile, void* img,
+                                void* stream) {
+  if (!W || !img) return HG_ERR_ARG;
+  return hg_gemm_x6_image_jobs(&W, &ldw, &trans, &N, &K, &tile, &img, 1, stream);
+}
+
+extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* img, const float* bias,
+                               const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N,
+                               int K, int act, int tile, void* stream) {
+  if (!A || !img || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || (mode != 0 && mode != 1) || act < 0 ||
+      act > 1 || tile < 19 || tile > NTILES)
+    return HG_ERR_ARG;
+  if (mode == 1 && act == 1 && (!Y || ldY < N)) return HG_ERR_ARG;
+  if ((uintptr_t)A % 4 || (uintptr_t)img % 16 || (uintptr_t)C % 4) return HG_ERR_ARG;
+  const bool vec = lda % 4 == 0 && (uintptr_t)A % 16 == 0;
+  GemmArgs g{A, lda, reinterpret_cast<const float*>(img), 0, bias, Y, ldY, C, ldc, colpart, M, N, K, 0, 0};
+  GemmX6Args xa{g, 0, 0, 1};
+  hipStream_t s = (hipStream_t)stream;
+  const bool elu = act == 1;
+  switch (tile) {
+    case 20: return launch_x6_img<128, 128, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 21: return launch_x6_img<128, 128, 2, 4, 1>(mode, xa, vec, elu, s);
+    case 22: return launch_x6_img<128, 64, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 23: return launch_x6_img<64, 64, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 24: return launch_x6_img<128, 128, 2, 2, 2>(mode, xa, vec, elu, s);
+    case 25: return launch_x6_img<256, 128, 4, 2, 1>(mode, xa, vec, elu, s);
+    case 26: return launch_x6_img<128, 128, 2, 4, 2>(mode, xa, vec, elu, s);
+    default: return launch_x6_img<64, 128, 2, 2, 1>(mode, xa, vec, elu, s);  // 19
+  }
+}
 
 extern "C" int hg_gemm_tile(int mode, int64_t M, int N, int K) {
   (void)mode;

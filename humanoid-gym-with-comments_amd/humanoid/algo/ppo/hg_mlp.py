@@ -238,14 +238,21 @@ X6_TILE0 = 19  # tiles >= 19: the bf16-split (6-term) kernels of hg_gemm_f32
 _GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG, 22)],
              (256, 128): [(8192, 0), (32768, 5), (_BIG, 20)], (705, 128): [(8192, 5), (_BIG, 23)],
              (128, 128): [(8192, 0), (_BIG, 5)], (219, 768): [(32768, 21), (_BIG, 20)],
-             (768, 256): [(32768, 19), (_BIG, 20)]}
+             (768, 256): [(32768, 22), (_BIG, 20)]}
 # input gradients (24576 rows, torch mm + ELU-backward pass -> fused; gemm_probe_x6.jsonl): 256->512
 # 84.7 -> 72.9 (bf16-split tile 22), 256->768 118 -> 103 (f32 tile 16), 128->256 33 -> 24.8 (16),
-# 128->128 22 -> 17.9 (f32 tile 5).  Weight gradients stay on hipBLASLt: the bf16-split kernel with
+# 128->128 22 -> 17.9 (f32 tile 5); with the B image (below) 256->512 72.4 -> 68.6 (22), 256->768
+# 103 -> 93.2 (22), 768x256 forward 84.9 (19) -> 71.2 (22) (profiles/r3_gemm/x6_image_probe.jsonl).
+# Weight gradients stay on hipBLASLt: the bf16-split kernel with
 # split-K slices (LDS-transposed staging of the row-major gh and x, or explicit transposes) was
 # 0.57-0.94x of its tuned TN kernels on every shape.
-_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 16)], (128, 128): [(_BIG, 5)]}
+_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 22)], (128, 128): [(_BIG, 5)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
+# The bf16-split tiles read B (the weight) from an image split once per MLP call
+# (hg_gemm_x6_image_jobs: every routed layer's forward and input-grad image in ONE launch) and
+# copied to LDS by LDS-DMA, instead of loading + splitting + writing it per row tile: same result
+# bit for bit, 5-15 % less time per GEMM (profiles/r3_gemm/x6_image_probe.jsonl).
+X6_IMAGE = os.environ.get("HG_X6_IMAGE", "1") != "0"
 # the output layer's input gradient with the ELU backward of the layer below fused in
 SKINNY_ACT = os.environ.get("HG_SKINNY_ACT", "1") != "0"
 
@@ -266,8 +273,66 @@ def _gemm_fwd_tile(h, W, b):
     return _route(_GEMM_FWD, h.shape[0], W.shape[1], W.shape[0])
 
 
-def gemm_forward(h, W, b, elu=True, tile=0, out=None):
-    """y = elu(h W^T + b) (``elu`` False: h W^T + b) on hg_gemm_f32 (mode 0)."""
+def x6_images(jobs, dev):
+    """B images for the bf16-split tiles in one launch: jobs [(W, trans, N, K, tile)] (trans 0: B =
+    W [N, K], the forward; trans 1: B = W^T of W [K, N], the input grad) -> one image tensor each,
+    slices of a single allocation."""
+    if not jobs:
+        return []
+    L = N.lib()
+    sizes = [int(L.hg_gemm_x6_image_bytes(n, k, t)) for _, _, n, k, t in jobs]
+    buf = torch.empty(sum(sizes) // 4, dtype=torch.float32, device=dev)
+    imgs, off = [], 0
+    for sz in sizes:
+        imgs.append(buf[off // 4:(off + sz) // 4])
+        off += sz
+    m = len(jobs)
+    vp = ctypes.c_void_p
+    rc = L.hg_gemm_x6_image_jobs((vp * m)(*[j[0].data_ptr() for j in jobs]),
+                                 (ctypes.c_int64 * m)(*[j[0].stride(0) for j in jobs]),
+                                 (ctypes.c_int * m)(*[j[1] for j in jobs]), (ctypes.c_int * m)(*[j[2] for j in jobs]),
+                                 (ctypes.c_int * m)(*[j[3] for j in jobs]), (ctypes.c_int * m)(*[j[4] for j in jobs]),
+                                 (vp * m)(*[im.data_ptr() for im in imgs]), m, _stream(dev))
+    if rc != 0:
+        raise RuntimeError(f"hg_gemm_x6_image_jobs failed ({rc})")
+    return imgs
+
+
+def _forward_images(params, n, rows, dev, dx):
+    """{layer: (tile, image)} of the routed bf16-split forward GEMMs of an n-layer MLP call on
+    ``rows`` rows and, when ``dx``, of its routed bf16-split input-grad GEMMs — built in one launch."""
+    fwd, dxi = {}, {}
+    if not (X6_IMAGE and GEMM):
+        return fwd, dxi
+    jobs, keys = [], []
+    for i in range(n):
+        W = params[2 * i]
+        if not W.is_contiguous():
+            continue
+        nn_, kk = W.shape
+        if i < n - 1:
+            t = _route(_GEMM_FWD, rows, kk, nn_)
+            if t >= X6_TILE0:
+                jobs.append((W, 0, nn_, kk, t))
+                keys.append((fwd, i, t))
+        if dx and i > 0:
+            t = _route(_GEMM_DX, rows, nn_, kk)
+            if t >= X6_TILE0:
+                jobs.append((W, 1, kk, nn_, t))
+                keys.append((dxi, i, t))
+    for (d, i, t), im in zip(keys, x6_images(jobs, dev)):
+        d[i] = (t, im)
+    return fwd, dxi
+
+
+def _img_for(images, i, tile):
+    ti = images.get(i)
+    return ti[1] if ti is not None and ti[0] == tile else None
+
+
+def gemm_forward(h, W, b, elu=True, tile=0, out=None, img=None):
+    """y = elu(h W^T + b) (``elu`` False: h W^T + b) on hg_gemm_f32 (mode 0); ``img`` = W's B image
+    for ``tile`` (x6_images) when given."""
     rows, n, k = h.shape[0], W.shape[0], W.shape[1]
     L = N.lib()
     if tile == 0:
@@ -275,14 +340,18 @@ def gemm_forward(h, W, b, elu=True, tile=0, out=None):
     y = torch.empty(rows, n, dtype=torch.float32, device=h.device) if out is None else out
     if y.shape != (rows, n) or y.stride(1) != 1 or y.dtype != torch.float32:
         raise RuntimeError("gemm_forward: out must be a float32 [rows, n] tensor with unit column stride")
-    rc = L.hg_gemm_f32(0, h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0, y.data_ptr(),
-                       y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
+    if img is not None:
+        rc = L.hg_gemm_f32_img(0, h.data_ptr(), h.stride(0), img.data_ptr(), b.data_ptr(), None, 0, y.data_ptr(),
+                               y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
+    else:
+        rc = L.hg_gemm_f32(0, h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0,
+                           y.data_ptr(), y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
     if rc != 0:
         raise RuntimeError(f"hg_gemm_f32 (forward) failed ({rc})")
     return y
 
 
-def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0):
+def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0, img=None):
     """(gh W) * elu'(y_prev) — layer i's input gradient through layer i-1's ELU backward (its
     pre-activation gradient) — with layer i-1's bias gradient gb = column sums, on hg_gemm_f32
     (mode 1).  gh [rows, n_i] contiguous, W [n_i, k_i] (nn.Linear.weight), y_prev [rows, k_i]."""
@@ -297,10 +366,15 @@ def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0):
     # W read as is ([n_i, k_i], n-contiguous in the reduction index): the f32 tiles stage it with
     # coalesced scalar loads, the bf16-split tiles through an LDS transpose (mode 3 with a W^T copy
     # measured no faster, profiles/r3_gemm/gemm_probe_x6.jsonl)
-    mode, B = 1, W
-    rc = L.hg_gemm_f32(mode, gh.data_ptr(), gh.stride(0), B.data_ptr(), B.stride(0), None, y_prev.data_ptr(),
-                       y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
-                       _stream(gh.device))
+    # (``img``: W^T's B image for ``tile``, x6_images trans 1)
+    if img is not None:
+        rc = L.hg_gemm_f32_img(1, gh.data_ptr(), gh.stride(0), img.data_ptr(), None, y_prev.data_ptr(),
+                               y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
+                               _stream(gh.device))
+    else:
+        rc = L.hg_gemm_f32(1, gh.data_ptr(), gh.stride(0), W.data_ptr(), W.stride(0), None, y_prev.data_ptr(),
+                           y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
+                           _stream(gh.device))
     if rc != 0:
         raise RuntimeError(f"hg_gemm_f32 (input grad) failed ({rc})")
     if red is None:
@@ -323,11 +397,12 @@ def _gemm_dx_tile(gh, W, y_prev):
 DEFER_REDUCTIONS = os.environ.get("HG_DEFER_REDUCTIONS", "1") != "0"
 
 
-def _hidden_forward(h, W, b):
-    """One hidden layer: the LDS-staged GEMM, the register-operand fused kernel, or addmm + ELU."""
+def _hidden_forward(h, W, b, images=None, i=0):
+    """One hidden layer: the LDS-staged GEMM (with layer i's B image from ``images`` when built for
+    the routed tile), the register-operand fused kernel, or addmm + ELU."""
     tile = _gemm_fwd_tile(h, W, b)
     if tile:
-        return gemm_forward(h, W, b, True, tile)
+        return gemm_forward(h, W, b, True, tile, img=_img_for(images, i, tile) if images else None)
     if _fused_ok(h, W, b):
         return linear_act(h, W, b)
     return F.elu(torch.addmm(b, h, W.t()))
@@ -339,12 +414,13 @@ class _MLP(torch.autograd.Function):
         n = len(params) // 2
         acts = [x]
         h = x
+        fimg, ctx.dximg = _forward_images(params, n, x.shape[0], x.device, any(ctx.needs_input_grad))
         for i in range(n):
             W, b = params[2 * i], params[2 * i + 1]
             if i == n - 1 and _skinny_ok(h, W):
                 h = _skinny_forward(h, W, b)
             elif i < n - 1:
-                h = _hidden_forward(h, W, b)
+                h = _hidden_forward(h, W, b, fimg, i)
             else:
                 h = torch.addmm(b, h, W.t())
             acts.append(h)
@@ -391,7 +467,8 @@ class _MLP(torch.autograd.Function):
                     if tile:
                         # layer i-1's pre-activation gradient and bias gradient straight from this GEMM
                         gb_prev = torch.empty(Ws[i].shape[1], dtype=torch.float32, device=gh.device)
-                        pre = (gemm_input_grad(gh, Ws[i], ins[i], gb_prev, red, tile), gb_prev)
+                        pre = (gemm_input_grad(gh, Ws[i], ins[i], gb_prev, red, tile, _img_for(ctx.dximg, i, tile)),
+                               gb_prev)
                     else:
                         gnext = torch.mm(gh, Ws[i])
             if i > 0:
@@ -401,6 +478,7 @@ class _MLP(torch.autograd.Function):
                 gx = gnext
         if red is not None:
             red.launch(ins[0].device)
+        ctx.dximg = None
         return (gx, *grads)
 
 
@@ -424,10 +502,14 @@ def mlp_infer(net, x, out=None):
     given)."""
     mods = list(net)
     h = x
+    fimg = None
+    if fusable(net):
+        params = _params(net)
+        fimg = _forward_images(params, len(params) // 2, x.shape[0], x.device, False)[0]
     for j in range(0, len(mods) - 1, 2):
         lin = mods[j]
         if isinstance(mods[j + 1], nn.ELU) and mods[j + 1].alpha == 1.0 and not mods[j + 1].inplace:
-            h = _hidden_forward(h, lin.weight, lin.bias)
+            h = _hidden_forward(h, lin.weight, lin.bias, fimg, j // 2)
         else:
             h = mods[j + 1](lin(h))
     last = mods[-1]

@@ -459,6 +459,22 @@ int hg_gemm_tile(int mode, int64_t M, int N, int K);
 int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                       int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile, void* stream);
 int64_t hg_gemm_colpart_rows(int64_t M, int tile);
+/* The B operand of the bf16-split tiles (19..26) split once into a global image: per (column
+ * tile, 16-deep k chunk) the three bf16 planes in the kernel's LDS order, zero past N / K.
+ * Element (n, k) of B is W[n ldw + k] (trans 0: the forward's W [N, K], mode 3's transposed W)
+ * or W[k ldw + n] (trans 1: mode 1's W [K, N]).  hg_gemm_f32_img then runs mode 0 / mode 1 of
+ * hg_gemm_f32 (same epilogues, same result bit for bit) with B copied image -> LDS by LDS-DMA
+ * instead of staged and split per block: the split of B happens once per weight instead of once
+ * per row tile.  The image is tile-specific (its BN and chunk depth): build it with the tile
+ * that consumes it.  img 16-byte aligned, hg_gemm_x6_image_bytes(N, K, tile) bytes. */
+int64_t hg_gemm_x6_image_bytes(int N, int K, int tile);
+int hg_gemm_x6_image(const float* W, int64_t ldw, int trans, int N, int K, int tile, void* img, void* stream);
+/* hg_gemm_x6_image for njobs <= 16 weights in ONE launch (arrays of njobs entries, host memory). */
+int hg_gemm_x6_image_jobs(const float* const* W, const int64_t* ldw, const int* trans, const int* N, const int* K,
+                          const int* tile, void* const* img, int njobs, void* stream);
+int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* img, const float* bias, const float* Y,
+                    int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K, int act, int tile,
+                    void* stream);
 
 /* library build info */
 const char* hg_version(void);

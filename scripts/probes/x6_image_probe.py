@@ -1,0 +1,117 @@
+"""B-operand image probe for the bf16-split GEMM (csrc/hg_gemm.hip): per policy-MLP shape and x6
+tile, hg_gemm_f32 (B staged + split per block) against hg_gemm_x6_image + hg_gemm_f32_img (B split
+once into a global image, copied to LDS by LDS-DMA).  Reports the time of both GEMM forms, the
+image build, and whether the outputs (and, for the input grad, the column partials) are bitwise
+equal.  One JSON line per (shape, tile)."""
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "humanoid-gym-with-comments_amd"))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from humanoid import _native as N  # noqa: E402
+
+dev = "cuda:0"
+L = N.lib()
+torch.manual_seed(0)
+ITERS = int(os.environ.get("ITERS", 30))
+TILES = [int(t) for t in os.environ.get("TILES", "19,20,21,22,23,24,25,26").split(",")]
+FWD = [("actor0_mb", 24576, 705, 512), ("actor1_mb", 24576, 512, 256), ("linvel0_mb", 24576, 705, 128),
+       ("critic0_mb", 24576, 219, 768), ("critic1_mb", 24576, 768, 256), ("actor2_mb", 24576, 256, 128),
+       ("actor0_roll", 4096, 705, 512), ("critic0_vals", 98304, 219, 768), ("critic1_vals", 98304, 768, 256)]
+DX = [("actor_dx1", 24576, 256, 512), ("actor_dx2", 24576, 128, 256), ("critic_dx1", 24576, 256, 768),
+      ("critic_dx2", 24576, 128, 256), ("linvel_dx1", 24576, 128, 128)]
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def timeit(fn):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(ITERS):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / ITERS
+
+
+def ck(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} rc={rc}")
+
+
+def image(W, trans, n, k, tile):
+    img = torch.empty(int(L.hg_gemm_x6_image_bytes(n, k, tile)) // 4, device=dev)
+    ck(L.hg_gemm_x6_image(W.data_ptr(), W.stride(0), trans, n, k, tile, img.data_ptr(), stream()), "image")
+    return img
+
+
+for tag, rows, k, n in FWD:
+    x = torch.randn(rows, k, device=dev)
+    W = torch.randn(n, k, device=dev) * (1.0 / k ** 0.5)
+    b = torch.randn(n, device=dev) * 0.1
+    for tile in TILES:
+        y0 = torch.empty(rows, n, device=dev)
+        y1 = torch.empty(rows, n, device=dev)
+
+        def plain():
+            ck(L.hg_gemm_f32(0, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0,
+                             y0.data_ptr(), y0.stride(0), None, rows, n, k, 1, tile, stream()), "plain")
+
+        img = image(W, 0, n, k, tile)
+
+        def imaged():
+            ck(L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), img.data_ptr(), b.data_ptr(), None, 0, y1.data_ptr(),
+                                 y1.stride(0), None, rows, n, k, 1, tile, stream()), "img")
+
+        plain()
+        imaged()
+        torch.cuda.synchronize()
+        rec = {"shape": tag, "mode": 0, "rows": rows, "k": k, "n": n, "tile": tile,
+               "bitwise_equal": bool(torch.equal(y0, y1)), "plain_us": round(timeit(plain), 2),
+               "img_us": round(timeit(imaged), 2), "image_build_us": round(timeit(lambda: image(W, 0, n, k, tile)), 2)}
+        print(json.dumps(rec), flush=True)
+
+for tag, rows, kr, n in DX:
+    g = torch.randn(rows, kr, device=dev)
+    W = torch.randn(kr, n, device=dev) * (1.0 / kr ** 0.5)
+    y = F.elu(torch.randn(rows, n, device=dev))
+    for tile in TILES:
+        parts = int(L.hg_gemm_colpart_rows(rows, tile))
+        o0, o1 = torch.empty(rows, n, device=dev), torch.empty(rows, n, device=dev)
+        c0, c1 = torch.empty(parts, n, device=dev), torch.empty(parts, n, device=dev)
+
+        def plain():
+            ck(L.hg_gemm_f32(1, g.data_ptr(), g.stride(0), W.data_ptr(), W.stride(0), None, y.data_ptr(), y.stride(0),
+                             o0.data_ptr(), o0.stride(0), c0.data_ptr(), rows, n, kr, 1, tile, stream()), "plain")
+
+        img = image(W, 1, n, kr, tile)
+
+        def imaged():
+            ck(L.hg_gemm_f32_img(1, g.data_ptr(), g.stride(0), img.data_ptr(), None, y.data_ptr(), y.stride(0),
+                                 o1.data_ptr(), o1.stride(0), c1.data_ptr(), rows, n, kr, 1, tile, stream()), "img")
+
+        plain()
+        imaged()
+        torch.cuda.synchronize()
+        rec = {"shape": tag, "mode": 1, "rows": rows, "k": kr, "n": n, "tile": tile,
+               "bitwise_equal": bool(torch.equal(o0, o1) and torch.equal(c0, c1)),
+               "plain_us": round(timeit(plain), 2), "img_us": round(timeit(imaged), 2),
+               "image_build_us": round(timeit(lambda: image(W, 1, n, kr, tile)), 2)}
+        # the f32 tile 16 (the routed input-grad tile) for reference
+        if tile == TILES[0]:
+            p16 = int(L.hg_gemm_colpart_rows(rows, 16))
+            c16 = torch.empty(p16, n, device=dev)
+            rec["tile16_us"] = round(timeit(lambda: ck(L.hg_gemm_f32(
+                1, g.data_ptr(), g.stride(0), W.data_ptr(), W.stride(0), None, y.data_ptr(), y.stride(0),
+                o0.data_ptr(), o0.stride(0), c16.data_ptr(), rows, n, kr, 1, 16, stream()), "t16")), 2)
+        print(json.dumps(rec), flush=True)

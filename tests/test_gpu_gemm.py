@@ -134,6 +134,59 @@ def test_gemm_wgrad_matches_fp64(rows, n, k, S):
             assert (part[:, :, k:] == 5.0).all()
 
 
+# (rows, k, n): the B-image form (hg_gemm_x6_image + hg_gemm_f32_img) of modes 0 and 1 against
+# hg_gemm_f32 with the per-block staging, bit for bit (same split, same MFMA order), ragged shapes
+IMG_CASES = [(3001, 705, 512), (777, 219, 768), (4096, 256, 128), (33, 7, 5), (65, 40, 129), (1, 705, 128)]
+
+
+@pytest.mark.parametrize("rows,k,n", IMG_CASES)
+def test_gemm_b_image_bitwise_equal(rows, k, n):
+    _need_gpu()
+    from humanoid import _native as N
+    L = N.lib()
+    torch.manual_seed(rows + 3 * k + n)
+    dev = "cuda:0"
+    x = torch.randn(rows, k, device=dev)
+    W = torch.randn(n, k, device=dev) / k ** 0.5
+    b = torch.randn(n, device=dev) * 0.1
+    Wd = torch.randn(k, n, device=dev) / k ** 0.5  # mode 1: g [rows, k] x Wd [k, n]
+    y = F.elu(torch.randn(rows, n, device=dev))
+    for tile in range(19, 27):
+        for mode, B, trans in ((0, W, 0), (1, Wd, 1)):
+            img = torch.empty(int(L.hg_gemm_x6_image_bytes(n, k, tile)) // 4, device=dev)
+            assert L.hg_gemm_x6_image(B.data_ptr(), B.stride(0), trans, n, k, tile, img.data_ptr(), _stream()) == 0
+            parts = int(L.hg_gemm_colpart_rows(rows, tile))
+            outs = []
+            for use_img in (False, True):
+                out = torch.full((rows, n + 2), 3.0, device=dev)
+                cp = torch.full((parts, n), float("nan"), device=dev) if mode == 1 else None
+                bias = b.data_ptr() if mode == 0 else None
+                Y, ldY = (y.data_ptr(), y.stride(0)) if mode == 1 else (None, 0)
+                cpp = cp.data_ptr() if cp is not None else None
+                if use_img:
+                    rc = L.hg_gemm_f32_img(mode, x.data_ptr(), x.stride(0), img.data_ptr(), bias, Y, ldY,
+                                           out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _stream())
+                else:
+                    rc = L.hg_gemm_f32(mode, x.data_ptr(), x.stride(0), B.data_ptr(), B.stride(0), bias, Y, ldY,
+                                       out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _stream())
+                assert rc == 0
+                outs.append((out, cp))
+            (o0, c0), (o1, c1) = outs
+            assert torch.equal(o0, o1), f"tile {tile} mode {mode}"
+            assert (o1[:, n:] == 3.0).all()
+            if mode == 1:
+                assert torch.equal(c0, c1), f"tile {tile} colpart"
+    # arguments: an f32 tile or a misaligned image is refused
+    img = torch.empty(int(L.hg_gemm_x6_image_bytes(n, k, 20)) // 4 + 4, device=dev)
+    out = torch.empty(rows, n, device=dev)
+    assert L.hg_gemm_x6_image(W.data_ptr(), W.stride(0), 0, n, k, 5, img.data_ptr(), _stream()) != 0
+    assert L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), img.data_ptr() + 4, None, None, 0, out.data_ptr(),
+                             out.stride(0), None, rows, n, k, 0, 20, _stream()) != 0
+    assert L.hg_gemm_f32_img(2, x.data_ptr(), x.stride(0), img.data_ptr(), None, None, 0, out.data_ptr(),
+                             out.stride(0), None, rows, n, k, 0, 20, _stream()) != 0
+    torch.cuda.synchronize()
+
+
 def test_gemm_rejects_bad_arguments():
     _need_gpu()
     from humanoid import _native as N
