@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "hg_common.h"
 
 namespace {
@@ -539,10 +541,12 @@ struct X6Op {
   }
 };
 
-// BIMG: B comes as a pre-split image (hg_gemm_x6_image): per (column tile, 16 KG-deep chunk) the
-// three planes in exactly the LDS order, copied by LDS-DMA (global_load_lds, 1 KB per wave
-// instruction, lane-linear) with no register staging, split or LDS write pass for B.
-template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, bool BIMG = false>
+// IMG bit 0 (B) / bit 1 (A): the operand comes as a pre-split image (hg_gemm_x6_image_jobs; layout
+// at k_x6_image_jobs): per 16-deep k chunk and plane, 32 rows form one contiguous 1 KB unit in
+// exactly the LDS fragment order, so a block's BM (BN) rows of a chunk are copied by LDS-DMA
+// (global_load_lds, 1 KB per wave instruction, lane-linear) with no register staging, split or LDS
+// write pass.  The image's plane pitch (16-byte slots) rides in lda / ldb.
+template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, int IMG = 0>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
@@ -552,8 +556,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   static_assert(TM >= 1 && TN >= 1 && BM == 32 * TM * WGM && BN == 32 * TN * WGN, "wave tiling");
   static_assert(2 * STAGE * 4 >= WGM * BN, "epilogue reduction buffer fits the staging LDS");
   constexpr bool AKC = MODE != 2, BKC = MODE == 0 || MODE == 3 || MODE == 4;
-  constexpr int SCA = AKC ? 0 : X6StageT<BM, KG, 64 * WGM * WGN>::SCRATCH;
-  static_assert(!BIMG || MODE == 0 || MODE == 1, "B image: forward and input-grad epilogues");
+  constexpr int SCA = (AKC || (IMG & 2)) ? 0 : X6StageT<BM, KG, 64 * WGM * WGN>::SCRATCH;
+  constexpr bool AIMG = (IMG & 2) != 0, BIMG = (IMG & 1) != 0;
+  static_assert(IMG == 0 || MODE == 0 || MODE == 1 || MODE == 2, "images: forward, input-grad, split-K epilogues");
+  static_assert(MODE != 2 || IMG == 0 || IMG == 3, "split-K: both operands as images");
   constexpr int SCB = (BKC || BIMG) ? 0 : X6StageT<BN, KG, 64 * WGM * WGN>::SCRATCH;
   constexpr int SCS = (SCA + SCB + 3) / 4;  // scratch in 16-byte slots, after the two stages
   __shared__ __attribute__((aligned(16))) bf16x8 lds[2 * STAGE + SCS];
@@ -591,37 +597,49 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   const int64_t nk = kend - kbeg;
   const int64_t kfull = kbeg + (nk & ~(int64_t)(BK - 1));
   const int nchunks = (int)((nk + BK - 1) / BK);
-  // B image chunk c of this column tile: 3 PB slots = BIMG_KB instructions of 64 lanes x 16 B
-  constexpr int BIMG_KB = 3 * PB / 64;
-  const bf16x8* bimg = reinterpret_cast<const bf16x8*>(g.B) + (tile % g.tiles_n) * (int64_t)nchunks * (3 * PB);
-  auto dma_b = [&](int c, bf16x8* S) {
-    const bf16x8* src = bimg + (int64_t)c * (3 * PB) + lane;
-    for (int q = wave; q < BIMG_KB; q += WGM * WGN)
-      __builtin_amdgcn_global_load_lds(src + q * 64, (__attribute__((address_space(3))) void*)(S + 3 * PA + q * 64), 16,
-                                       0, 0);
+  // image chunk c (relative to kbeg) of an operand with R block rows from row r0: 3 planes x KG
+  // chunk slices x R/32 units of 1 KB, one LDS-DMA instruction each, spread over the waves
+  const int64_t cabs0 = kbeg / 16;
+  auto dma = [&](auto RC, const float* img, int64_t pitch, int64_t r0, int c, bf16x8* dst) {
+    constexpr int R = decltype(RC)::value, U = R / 32, PR = R * 2 * KG;
+    const bf16x8* base = reinterpret_cast<const bf16x8*>(img) + r0 * 2 + lane;
+    for (int q = wave; q < 3 * KG * U; q += WGM * WGN) {
+      const int u = q % U, kg = (q / U) % KG, p = q / (U * KG);
+      const bf16x8* src = base + ((cabs0 + (int64_t)c * KG + kg) * 3 + p) * pitch + u * 64;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + p * PR + kg * R * 2 + u * 64),
+                                       16, 0, 0);
+    }
+  };
+  auto dma_all = [&](int c, bf16x8* S) {
+    if (AIMG) dma(std::integral_constant<int, BM>(), g.A, g.lda, m0, c, S);
+    if (BIMG) dma(std::integral_constant<int, BN>(), g.B, g.ldb, n0, c, S + 3 * PA);
   };
   auto load = [&](int64_t kc) {
     const bool tail = kc + BK > kfull;
-    sa.load(g.A, g.lda, m0, mmax, kc, kend, tail, tid);
+    if (!AIMG) sa.load(g.A, g.lda, m0, mmax, kc, kend, tail, tid);
     if (!BIMG) sb.load(g.B, g.ldb, n0, nmax, kc, kend, tail, tid);
   };
   auto store = [&](bf16x8* S) {
-    if (AKC) sa.kc.store(S, tid);
-    else sa.rt.to_scratch(scA, tid);
+    if (!AIMG) {
+      if (AKC) sa.kc.store(S, tid);
+      else sa.rt.to_scratch(scA, tid);
+    }
     if (!BIMG) {
       if (BKC) sb.kc.store(S + 3 * PA, tid);
       else sb.rt.to_scratch(scB, tid);
     }
-    if (!AKC || (!BKC && !BIMG)) {
+    if ((!AKC && !AIMG) || (!BKC && !BIMG)) {
       __syncthreads();
-      if (!AKC) sa.rt.to_planes(S, scA, tid);
+      if (!AKC && !AIMG) sa.rt.to_planes(S, scA, tid);
       if (!BKC && !BIMG) sb.rt.to_planes(S + 3 * PA, scB, tid);
     }
   };
   if (nchunks > 0) {
-    if (BIMG) dma_b(0, lds);
-    load(kbeg);
-    store(lds);
+    if (IMG) dma_all(0, lds);
+    if (IMG != 3) {
+      load(kbeg);
+      store(lds);
+    }
   }
   __syncthreads();
   for (int c = 0; c < nchunks; c++) {
@@ -629,8 +647,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
     bf16x8* nxt = lds + ((c + 1) & 1) * STAGE;
     const bool more = c + 1 < nchunks;
     if (more) {
-      if (BIMG) dma_b(c + 1, nxt);
-      load(kbeg + (int64_t)(c + 1) * BK);
+      if (IMG) dma_all(c + 1, nxt);
+      if (IMG != 3) load(kbeg + (int64_t)(c + 1) * BK);
     }
 #pragma unroll
     for (int kg = 0; kg < KG; kg++) {
@@ -654,7 +672,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
           acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[0][n], acc[m][n], 0, 0, 0);
         }
     }
-    if (more) store(nxt);
+    if (more && IMG != 3) store(nxt);
     __syncthreads();
   }
 
@@ -721,75 +739,106 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   }
 }
 
-// the pre-split B images of a list of weights, one launch: block (job, column tile tn, chunk c),
-// the (column r, 8-k piece) items of that chunk over its 256 threads; element (n, k) of B is
-// W[n ldw + k] (trans 0: W rows are B rows, the forward / transposed input-grad operand) or
-// W[k ldw + n] (trans 1: the input-grad operand W[K][N]); past N or K the image holds 0
+// Operand images of the bf16-split kernels, a list of operands in one launch.  An operand X with
+// R rows (the product's M or N side) and reduction length K: element (r, k) = P[r ld + k]
+// (trans 0: k-contiguous rows — W of the forward, activations, gradients as the A side) or
+// P[k ld + r] (trans 1: reduction-major — W [K, N] of the input grad, the weight gradient's
+// row-major gh / x).  Layout: chunks of 16 k (count rounded up to even, so 32-deep tiles read whole
+// pairs), per chunk three planes (x0, x1, x2 of the exact split), per plane the rows padded to a
+// multiple of 256, row r's 8-k half h at 16-byte slot (r / 32 * 2 + h) * 32 + r % 32 — the LDS
+// fragment order of every tile (32-row units of 1 KB).  Zero past R and K.  Block (job, chunk,
+// 128-row group), thread (row r, half h).
 constexpr int IMG_MAX = 16;
 struct ImageJobs {
-  const float* W[IMG_MAX];
+  const float* P[IMG_MAX];
   bf16x8* img[IMG_MAX];
-  int64_t ldw[IMG_MAX];
-  int trans[IMG_MAX], N[IMG_MAX], K[IMG_MAX], bn[IMG_MAX], kg[IMG_MAX], chunks[IMG_MAX];
+  int64_t ld[IMG_MAX], pitch[IMG_MAX];
+  int trans[IMG_MAX], R[IMG_MAX], K[IMG_MAX], groups[IMG_MAX];
   int block0[IMG_MAX + 1];
   int njobs;
 };
+
+__host__ __device__ inline int64_t img_rows(int64_t R) { return (R + 255) / 256 * 256; }
+__host__ __device__ inline int64_t img_chunks(int64_t K) { return (K + 31) / 32 * 2; }
 
 __global__ void __launch_bounds__(256) k_x6_image_jobs(ImageJobs J) {
   const int bid = blockIdx.x;
   int j = 0;
   while (j + 1 < J.njobs && bid >= J.block0[j + 1]) j++;
   const int lb = bid - J.block0[j];
-  const int chunks = J.chunks[j], BN = J.bn[j], KG = J.kg[j];
-  const int tn = lb / chunks, c = lb % chunks;
-  const int PB = BN * 2 * KG;
-  const float* __restrict__ W = J.W[j];
-  const int64_t ldw = J.ldw[j];
-  const int N = J.N[j], K = J.K[j];
-  const bool trans = J.trans[j] != 0;
-  bf16x8* base = J.img[j] + (int64_t)lb * (3 * PB);
-  for (int idx = threadIdx.x; idx < PB; idx += 256) {
-    const int r = idx % BN, piece = idx / BN;
-    const int n = tn * BN + r;
-    const int k0 = c * 16 * KG + 8 * piece;
-    float v[8];
+  const int grp = lb % J.groups[j], c = lb / J.groups[j];
+  const int r = grp * 128 + (threadIdx.x & 127), h = threadIdx.x >> 7;
+  const float* __restrict__ P = J.P[j];
+  const int64_t ld = J.ld[j];
+  const int R = J.R[j], K = J.K[j];
+  const int k0 = c * 16 + 8 * h;
+  float v[8];
+  if (J.trans[j]) {
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int k = k0 + q;
-      v[q] = (n < N && k < K) ? (trans ? W[(int64_t)k * ldw + n] : W[(int64_t)n * ldw + k]) : 0.f;
-    }
-    bf16x8 x0, x1, x2;
-    split3x8(v, x0, x1, x2);
-    const int sl = x6_slot(BN, piece >> 1, r, piece & 1);
-    base[sl] = x0;
-    base[PB + sl] = x1;
-    base[2 * PB + sl] = x2;
+    for (int q = 0; q < 8; q++) v[q] = (r < R && k0 + q < K) ? P[(int64_t)(k0 + q) * ld + r] : 0.f;
+  } else if (r < R && k0 + 8 <= K && ld % 4 == 0 && ((uintptr_t)P & 15) == 0) {
+    const float4 a = *reinterpret_cast<const float4*>(P + (int64_t)r * ld + k0);
+    const float4 b = *reinterpret_cast<const float4*>(P + (int64_t)r * ld + k0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = (r < R && k0 + q < K) ? P[(int64_t)r * ld + k0 + q] : 0.f;
   }
+  bf16x8 x0, x1, x2;
+  split3x8(v, x0, x1, x2);
+  const int64_t pitch = J.pitch[j];
+  bf16x8* base = J.img[j] + (int64_t)c * 3 * pitch + (r / 32 * 2 + h) * 32 + r % 32;
+  base[0] = x0;
+  base[pitch] = x1;
+  base[2 * pitch] = x2;
 }
 
 template <int BM, int BN, int WGM, int WGN, int KG>
-int launch_x6_img(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
+int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
   GemmArgs& g = xa.g;
   g.tiles_n = (g.N + BN - 1) / BN;
   const int64_t tiles_m = (g.M + BM - 1) / BM;
   g.tiles = tiles_m * g.tiles_n;
-  xa.slices = 1;
-  if (g.tiles > 0x7fffffff) return HG_ERR_ARG;
-  const dim3 grid((unsigned)g.tiles), block(64 * WGM * WGN);
-#define HG_X6I(V, MD, E) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, true>), grid, block, 0, s, xa)
-  if (mode == 0) {
-    if (vec && elu) HG_X6I(true, 0, true);
-    else if (vec) HG_X6I(true, 0, false);
-    else if (elu) HG_X6I(false, 0, true);
-    else HG_X6I(false, 0, false);
+  if (mode != 2) xa.slices = 1;
+  if (g.tiles * xa.slices > 0x7fffffff) return HG_ERR_ARG;
+  const dim3 grid((unsigned)(g.tiles * xa.slices)), block(64 * WGM * WGN);
+#define HG_X6I(V, MD, E, I) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, I>), grid, block, 0, s, xa)
+  if (mode == 2) {
+    HG_X6I(false, 2, false, 3);
+  } else if (img == 3) {
+    if (mode == 0) {
+      if (elu) HG_X6I(false, 0, true, 3);
+      else HG_X6I(false, 0, false, 3);
+    } else {
+      if (elu) HG_X6I(false, 1, true, 3);
+      else HG_X6I(false, 1, false, 3);
+    }
+  } else if (mode == 0) {
+    if (vec && elu) HG_X6I(true, 0, true, 1);
+    else if (vec) HG_X6I(true, 0, false, 1);
+    else if (elu) HG_X6I(false, 0, true, 1);
+    else HG_X6I(false, 0, false, 1);
   } else {
-    if (vec && elu) HG_X6I(true, 1, true);
-    else if (vec) HG_X6I(true, 1, false);
-    else if (elu) HG_X6I(false, 1, true);
-    else HG_X6I(false, 1, false);
+    if (vec && elu) HG_X6I(true, 1, true, 1);
+    else if (vec) HG_X6I(true, 1, false, 1);
+    else if (elu) HG_X6I(false, 1, true, 1);
+    else HG_X6I(false, 1, false, 1);
   }
 #undef HG_X6I
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+int x6_img_dispatch(int tile, int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
+  switch (tile) {
+    case 20: return launch_x6_img<128, 128, 2, 2, 1>(mode, img, xa, vec, elu, s);
+    case 21: return launch_x6_img<128, 128, 2, 4, 1>(mode, img, xa, vec, elu, s);
+    case 22: return launch_x6_img<128, 64, 2, 2, 1>(mode, img, xa, vec, elu, s);
+    case 23: return launch_x6_img<64, 64, 2, 2, 1>(mode, img, xa, vec, elu, s);
+    case 24: return launch_x6_img<128, 128, 2, 2, 2>(mode, img, xa, vec, elu, s);
+    case 25: return launch_x6_img<256, 128, 4, 2, 1>(mode, img, xa, vec, elu, s);
+    case 26: return launch_x6_img<128, 128, 2, 4, 2>(mode, img, xa, vec, elu, s);
+    default: return launch_x6_img<64, 128, 2, 2, 1>(mode, img, xa, vec, elu, s);  // 19
+  }
 }
 
 template <int BM, int BN, int WGM, int WGN, int KG>
@@ -837,48 +886,36 @@ int tile_bm(int tile) {
              : 64;
 }
 
-// (BN, KG) of an x6 tile id
-void x6_bn_kg(int tile, int& bn, int& kg) {
-  bn = (tile == 22 || tile == 23) ? 64 : 128;
-  kg = (tile == 24 || tile == 26) ? 2 : 1;
-}
-
 }  // namespace
 
-extern "C" int64_t hg_gemm_x6_image_bytes(int N, int K, int tile) {
-  if (N <= 0 || K <= 0 || tile < 19 || tile > NTILES) return -1;
-  int bn, kg;
-  x6_bn_kg(tile, bn, kg);
-  const int64_t tiles_n = (N + bn - 1) / bn, chunks = (K + 16 * kg - 1) / (16 * kg);
-  return tiles_n * chunks * 3 * (bn * 2 * kg) * 16;
+extern "C" int64_t hg_gemm_x6_image_bytes(int64_t rows, int64_t K) {
+  if (rows <= 0 || K <= 0 || rows > 0x7fffffff || K > 0x7fffffff) return -1;
+  return img_chunks(K) * 3 * img_rows(rows) * 2 * 16;
 }
 
-extern "C" int hg_gemm_x6_image_jobs(const float* const* W, const int64_t* ldw, const int* trans, const int* N,
-                                     const int* K, const int* tile, void* const* img, int njobs, void* stream) {
+extern "C" int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* trans, const int64_t* rows,
+                                     const int64_t* K, void* const* img, int njobs, void* stream) {
   if (njobs <= 0) return HG_OK;
-  if (njobs > IMG_MAX || !W || !ldw || !trans || !N || !K || !tile || !img) return HG_ERR_ARG;
+  if (njobs > IMG_MAX || !P || !ld || !trans || !rows || !K || !img) return HG_ERR_ARG;
   ImageJobs J;
   J.njobs = njobs;
   int64_t blocks = 0;
   for (int j = 0; j < njobs; j++) {
-    if (!W[j] || !img[j] || N[j] <= 0 || K[j] <= 0 || tile[j] < 19 || tile[j] > NTILES ||
+    if (!P[j] || !img[j] || rows[j] <= 0 || K[j] <= 0 || rows[j] > 0x7fffffff || K[j] > 0x7fffffff ||
         (trans[j] != 0 && trans[j] != 1))
       return HG_ERR_ARG;
-    if ((trans[j] == 0 && ldw[j] < K[j]) || (trans[j] == 1 && ldw[j] < N[j])) return HG_ERR_ARG;
-    if ((uintptr_t)W[j] % 4 || (uintptr_t)img[j] % 16) return HG_ERR_ARG;
-    int bn, kg;
-    x6_bn_kg(tile[j], bn, kg);
-    J.W[j] = W[j];
+    if ((trans[j] == 0 && ld[j] < K[j]) || (trans[j] == 1 && ld[j] < rows[j])) return HG_ERR_ARG;
+    if ((uintptr_t)P[j] % 4 || (uintptr_t)img[j] % 16) return HG_ERR_ARG;
+    J.P[j] = P[j];
     J.img[j] = reinterpret_cast<bf16x8*>(img[j]);
-    J.ldw[j] = ldw[j];
+    J.ld[j] = ld[j];
+    J.pitch[j] = img_rows(rows[j]) * 2;
     J.trans[j] = trans[j];
-    J.N[j] = N[j];
-    J.K[j] = K[j];
-    J.bn[j] = bn;
-    J.kg[j] = kg;
-    J.chunks[j] = (K[j] + 16 * kg - 1) / (16 * kg);
+    J.R[j] = (int)rows[j];
+    J.K[j] = (int)K[j];
+    J.groups[j] = (int)(img_rows(rows[j]) / 128);
     J.block0[j] = (int)blocks;
-    blocks += (int64_t)J.chunks[j] * ((N[j] + bn - 1) / bn);
+    blocks += img_chunks(K[j]) * J.groups[j];
     if (blocks > (int64_t)1 << 30) return HG_ERR_ARG;
   }
   J.block0[njobs] = (int)blocks;
@@ -886,35 +923,37 @@ extern "C" int hg_gemm_x6_image_jobs(const float* const* W, const int64_t* ldw, 
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-extern "C" int hg_gemm_x6_image(const float* W, int64_t ldw, int trans, int N, int K, int tile, void* img,
-                                void* stream) {
-  if (!W || !img) return HG_ERR_ARG;
-  return hg_gemm_x6_image_jobs(&W, &ldw, &trans, &N, &K, &tile, &img, 1, stream);
-}
-
-extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* img, const float* bias,
-                               const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N,
-                               int K, int act, int tile, void* stream) {
-  if (!A || !img || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || (mode != 0 && mode != 1) || act < 0 ||
+extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, const void* Bimg,
+                               const float* bias, const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart,
+                               int64_t M, int N, int K, int act, int tile, void* stream) {
+  if ((!A && !Aimg) || !Bimg || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || (mode != 0 && mode != 1) || act < 0 ||
       act > 1 || tile < 19 || tile > NTILES)
     return HG_ERR_ARG;
+  if (!Aimg && lda < K) return HG_ERR_ARG;
   if (mode == 1 && act == 1 && (!Y || ldY < N)) return HG_ERR_ARG;
-  if ((uintptr_t)A % 4 || (uintptr_t)img % 16 || (uintptr_t)C % 4) return HG_ERR_ARG;
-  const bool vec = lda % 4 == 0 && (uintptr_t)A % 16 == 0;
-  GemmArgs g{A, lda, reinterpret_cast<const float*>(img), 0, bias, Y, ldY, C, ldc, colpart, M, N, K, 0, 0};
+  if ((!Aimg && (uintptr_t)A % 4) || (uintptr_t)Aimg % 16 || (uintptr_t)Bimg % 16 || (uintptr_t)C % 4)
+    return HG_ERR_ARG;
+  const bool vec = !Aimg && lda % 4 == 0 && (uintptr_t)A % 16 == 0;
+  const float* a = Aimg ? reinterpret_cast<const float*>(Aimg) : A;
+  const int64_t la = Aimg ? img_rows(M) * 2 : lda;
+  GemmArgs g{a, la, reinterpret_cast<const float*>(Bimg), img_rows(N) * 2, bias, Y, ldY, C, ldc, colpart, M, N, K, 0, 0};
   GemmX6Args xa{g, 0, 0, 1};
-  hipStream_t s = (hipStream_t)stream;
-  const bool elu = act == 1;
-  switch (tile) {
-    case 20: return launch_x6_img<128, 128, 2, 2, 1>(mode, xa, vec, elu, s);
-    case 21: return launch_x6_img<128, 128, 2, 4, 1>(mode, xa, vec, elu, s);
-    case 22: return launch_x6_img<128, 64, 2, 2, 1>(mode, xa, vec, elu, s);
-    case 23: return launch_x6_img<64, 64, 2, 2, 1>(mode, xa, vec, elu, s);
-    case 24: return launch_x6_img<128, 128, 2, 2, 2>(mode, xa, vec, elu, s);
-    case 25: return launch_x6_img<256, 128, 4, 2, 1>(mode, xa, vec, elu, s);
-    case 26: return launch_x6_img<128, 128, 2, 4, 2>(mode, xa, vec, elu, s);
-    default: return launch_x6_img<64, 128, 2, 2, 1>(mode, xa, vec, elu, s);  // 19
-  }
+  return x6_img_dispatch(tile, mode, Aimg ? 3 : 1, xa, vec, act == 1, (hipStream_t)stream);
+}
+
+extern "C" int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M,
+                                 int N, int64_t K, int slices, int tile, void* stream) {
+  if (!Aimg || !Bimg || !C || M <= 0 || N <= 0 || K <= 0 || K > 0x7fffffff || ldc < N || slices < 1 || tile < 19 ||
+      tile > NTILES)
+    return HG_ERR_ARG;
+  if (slices > 1 && cstride < M * (int64_t)ldc) return HG_ERR_ARG;
+  if ((uintptr_t)Aimg % 16 || (uintptr_t)Bimg % 16 || (uintptr_t)C % 4) return HG_ERR_ARG;
+  GemmArgs g{reinterpret_cast<const float*>(Aimg), img_rows(M) * 2, reinterpret_cast<const float*>(Bimg),
+             img_rows(N) * 2, nullptr, nullptr, 0, C, ldc, nullptr, M, N, (int)K, 0, 0};
+  // slices start on whole 32-deep chunk pairs of the images
+  const int64_t kslice = ((K + slices - 1) / slices + 31) & ~(int64_t)31;
+  GemmX6Args xa{g, kslice, cstride, slices};
+  return x6_img_dispatch(tile, 2, 3, xa, false, false, (hipStream_t)stream);
 }
 
 extern "C" int hg_gemm_tile(int mode, int64_t M, int N, int K) {

@@ -251,7 +251,11 @@ GEMM = os.environ.get("HG_GEMM", "1") != "0"
 # The bf16-split tiles read B (the weight) from an image split once per MLP call
 # (hg_gemm_x6_image_jobs: every routed layer's forward and input-grad image in ONE launch) and
 # copied to LDS by LDS-DMA, instead of loading + splitting + writing it per row tile: same result
-# bit for bit, 5-15 % less time per GEMM (profiles/r3_gemm/x6_image_probe.jsonl).
+# bit for bit, 5-15 % less time per GEMM (profiles/r3_gemm/x6_image_probe.jsonl).  Activation
+# images (A) and the weight gradients from two images were measured there too and are not routed:
+# a separate split pass over an activation (24576 x 705: 41 us) costs more than the GEMM saves
+# (actor 705->512 117 -> 103 us), and the image-fed split-K weight gradient (123 us + 58 us of
+# images for 512x705) loses to hipBLASLt's 181 us once the images are counted.
 X6_IMAGE = os.environ.get("HG_X6_IMAGE", "1") != "0"
 # the output layer's input gradient with the ELU backward of the layer below fused in
 SKINNY_ACT = os.environ.get("HG_SKINNY_ACT", "1") != "0"
@@ -274,13 +278,13 @@ def _gemm_fwd_tile(h, W, b):
 
 
 def x6_images(jobs, dev):
-    """B images for the bf16-split tiles in one launch: jobs [(W, trans, N, K, tile)] (trans 0: B =
-    W [N, K], the forward; trans 1: B = W^T of W [K, N], the input grad) -> one image tensor each,
-    slices of a single allocation."""
+    """Operand images of the bf16-split tiles in one launch (hg_gemm_x6_image_jobs): jobs
+    [(P, trans, rows, K)] (trans 0: element (r, k) = P[r][k]; trans 1: P[k][r]) -> one image tensor
+    each, slices of a single allocation."""
     if not jobs:
         return []
     L = N.lib()
-    sizes = [int(L.hg_gemm_x6_image_bytes(n, k, t)) for _, _, n, k, t in jobs]
+    sizes = [int(L.hg_gemm_x6_image_bytes(r, k)) for _, _, r, k in jobs]
     buf = torch.empty(sum(sizes) // 4, dtype=torch.float32, device=dev)
     imgs, off = [], 0
     for sz in sizes:
@@ -290,17 +294,17 @@ def x6_images(jobs, dev):
     vp = ctypes.c_void_p
     rc = L.hg_gemm_x6_image_jobs((vp * m)(*[j[0].data_ptr() for j in jobs]),
                                  (ctypes.c_int64 * m)(*[j[0].stride(0) for j in jobs]),
-                                 (ctypes.c_int * m)(*[j[1] for j in jobs]), (ctypes.c_int * m)(*[j[2] for j in jobs]),
-                                 (ctypes.c_int * m)(*[j[3] for j in jobs]), (ctypes.c_int * m)(*[j[4] for j in jobs]),
-                                 (vp * m)(*[im.data_ptr() for im in imgs]), m, _stream(dev))
+                                 (ctypes.c_int * m)(*[j[1] for j in jobs]), (ctypes.c_int64 * m)(*[j[2] for j in jobs]),
+                                 (ctypes.c_int64 * m)(*[j[3] for j in jobs]), (vp * m)(*[im.data_ptr() for im in imgs]),
+                                 m, _stream(dev))
     if rc != 0:
         raise RuntimeError(f"hg_gemm_x6_image_jobs failed ({rc})")
     return imgs
 
 
 def _forward_images(params, n, rows, dev, dx):
-    """{layer: (tile, image)} of the routed bf16-split forward GEMMs of an n-layer MLP call on
-    ``rows`` rows and, when ``dx``, of its routed bf16-split input-grad GEMMs — built in one launch."""
+    """{layer: image} of W for the routed bf16-split forward GEMMs of an n-layer MLP call on ``rows``
+    rows and, when ``dx``, of W^T for its routed bf16-split input-grad GEMMs — built in one launch."""
     fwd, dxi = {}, {}
     if not (X6_IMAGE and GEMM):
         return fwd, dxi
@@ -310,24 +314,19 @@ def _forward_images(params, n, rows, dev, dx):
         if not W.is_contiguous():
             continue
         nn_, kk = W.shape
-        if i < n - 1:
-            t = _route(_GEMM_FWD, rows, kk, nn_)
-            if t >= X6_TILE0:
-                jobs.append((W, 0, nn_, kk, t))
-                keys.append((fwd, i, t))
-        if dx and i > 0:
-            t = _route(_GEMM_DX, rows, nn_, kk)
-            if t >= X6_TILE0:
-                jobs.append((W, 1, kk, nn_, t))
-                keys.append((dxi, i, t))
-    for (d, i, t), im in zip(keys, x6_images(jobs, dev)):
-        d[i] = (t, im)
+        if i < n - 1 and _route(_GEMM_FWD, rows, kk, nn_) >= X6_TILE0:
+            jobs.append((W, 0, nn_, kk))
+            keys.append((fwd, i))
+        if dx and i > 0 and _route(_GEMM_DX, rows, nn_, kk) >= X6_TILE0:
+            jobs.append((W, 1, kk, nn_))
+            keys.append((dxi, i))
+    for (d, i), im in zip(keys, x6_images(jobs, dev)):
+        d[i] = im
     return fwd, dxi
 
 
 def _img_for(images, i, tile):
-    ti = images.get(i)
-    return ti[1] if ti is not None and ti[0] == tile else None
+    return images.get(i) if images and tile >= X6_TILE0 else None
 
 
 def gemm_forward(h, W, b, elu=True, tile=0, out=None, img=None):
@@ -341,8 +340,8 @@ def gemm_forward(h, W, b, elu=True, tile=0, out=None, img=None):
     if y.shape != (rows, n) or y.stride(1) != 1 or y.dtype != torch.float32:
         raise RuntimeError("gemm_forward: out must be a float32 [rows, n] tensor with unit column stride")
     if img is not None:
-        rc = L.hg_gemm_f32_img(0, h.data_ptr(), h.stride(0), img.data_ptr(), b.data_ptr(), None, 0, y.data_ptr(),
-                               y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
+        rc = L.hg_gemm_f32_img(0, h.data_ptr(), h.stride(0), None, img.data_ptr(), b.data_ptr(), None, 0,
+                               y.data_ptr(), y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
     else:
         rc = L.hg_gemm_f32(0, h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0,
                            y.data_ptr(), y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
@@ -368,7 +367,7 @@ def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0, img=None):
     # measured no faster, profiles/r3_gemm/gemm_probe_x6.jsonl)
     # (``img``: W^T's B image for ``tile``, x6_images trans 1)
     if img is not None:
-        rc = L.hg_gemm_f32_img(1, gh.data_ptr(), gh.stride(0), img.data_ptr(), None, y_prev.data_ptr(),
+        rc = L.hg_gemm_f32_img(1, gh.data_ptr(), gh.stride(0), None, img.data_ptr(), None, y_prev.data_ptr(),
                                y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
                                _stream(gh.device))
     else:
@@ -402,7 +401,7 @@ def _hidden_forward(h, W, b, images=None, i=0):
     the routed tile), the register-operand fused kernel, or addmm + ELU."""
     tile = _gemm_fwd_tile(h, W, b)
     if tile:
-        return gemm_forward(h, W, b, True, tile, img=_img_for(images, i, tile) if images else None)
+        return gemm_forward(h, W, b, True, tile, img=_img_for(images, i, tile))
     if _fused_ok(h, W, b):
         return linear_act(h, W, b)
     return F.elu(torch.addmm(b, h, W.t()))

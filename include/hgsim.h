@@ -459,22 +459,32 @@ int hg_gemm_tile(int mode, int64_t M, int N, int K);
 int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                       int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile, void* stream);
 int64_t hg_gemm_colpart_rows(int64_t M, int tile);
-/* The B operand of the bf16-split tiles (19..26) split once into a global image: per (column
- * tile, 16-deep k chunk) the three bf16 planes in the kernel's LDS order, zero past N / K.
- * Element (n, k) of B is W[n ldw + k] (trans 0: the forward's W [N, K], mode 3's transposed W)
- * or W[k ldw + n] (trans 1: mode 1's W [K, N]).  hg_gemm_f32_img then runs mode 0 / mode 1 of
- * hg_gemm_f32 (same epilogues, same result bit for bit) with B copied image -> LDS by LDS-DMA
- * instead of staged and split per block: the split of B happens once per weight instead of once
- * per row tile.  The image is tile-specific (its BN and chunk depth): build it with the tile
- * that consumes it.  img 16-byte aligned, hg_gemm_x6_image_bytes(N, K, tile) bytes. */
-int64_t hg_gemm_x6_image_bytes(int N, int K, int tile);
-int hg_gemm_x6_image(const float* W, int64_t ldw, int trans, int N, int K, int tile, void* img, void* stream);
-/* hg_gemm_x6_image for njobs <= 16 weights in ONE launch (arrays of njobs entries, host memory). */
-int hg_gemm_x6_image_jobs(const float* const* W, const int64_t* ldw, const int* trans, const int* N, const int* K,
-                          const int* tile, void* const* img, int njobs, void* stream);
-int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* img, const float* bias, const float* Y,
-                    int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K, int act, int tile,
-                    void* stream);
+/* Operand images of the bf16-split tiles (19..26): an f32 operand X with `rows` rows (the
+ * product's M or N side) and reduction length K, split once into the three exact bf16 terms and
+ * stored in the kernels' LDS fragment order (16-deep k chunks, count rounded up to even; three
+ * planes; rows padded to a multiple of 256; zero past rows / K; csrc/hg_gemm.hip), so a GEMM block
+ * copies its slice by LDS-DMA instead of loading, splitting and writing it per block tile.
+ * Element (r, k) of X is P[r ld + k] (trans 0: k-contiguous rows — nn.Linear.weight as the
+ * forward's B, activations / gradients as the A side) or P[k ld + r] (trans 1: reduction-major —
+ * the weight [K, N] of the input grad, the row-major gh / x of the weight gradient).  One launch
+ * for njobs <= 16 operands (arrays of njobs entries, host memory); img 16-byte aligned,
+ * hg_gemm_x6_image_bytes(rows, K) bytes.  The image is tile-independent.  Routed: the weights
+ * (B) only — split once per MLP call, 5-15 % off each GEMM; activation (A) and weight-gradient
+ * images built by this separate pass cost more than they save (profiles/r3_gemm/x6_image_probe.jsonl). */
+int64_t hg_gemm_x6_image_bytes(int64_t rows, int64_t K);
+int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* trans, const int64_t* rows,
+                          const int64_t* K, void* const* img, int njobs, void* stream);
+/* hg_gemm_f32 modes 0 / 1 on a bf16-split tile with B from its image (Bimg: rows N, reduction K)
+ * and A from its image (Aimg: rows M) or, Aimg NULL, staged from A (lda) as in hg_gemm_f32 — the
+ * same epilogues and, bit for bit, the same result. */
+int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, const void* Bimg, const float* bias,
+                    const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K,
+                    int act, int tile, void* stream);
+/* hg_gemm_f32_wgrad's split-K weight gradient from two images (Aimg: rows M, Bimg: rows N, both
+ * with reduction K — build them with trans 1 from the row-major gh [K, M] and x [K, N]); the
+ * slices start on 32-deep chunk pairs, ceil(K / slices) rounded up to a multiple of 32 rows each. */
+int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M, int N,
+                      int64_t K, int slices, int tile, void* stream);
 
 /* library build info */
 const char* hg_version(void);

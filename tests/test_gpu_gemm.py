@@ -134,13 +134,24 @@ def test_gemm_wgrad_matches_fp64(rows, n, k, S):
             assert (part[:, :, k:] == 5.0).all()
 
 
-# (rows, k, n): the B-image form (hg_gemm_x6_image + hg_gemm_f32_img) of modes 0 and 1 against
-# hg_gemm_f32 with the per-block staging, bit for bit (same split, same MFMA order), ragged shapes
+def _image(L, P, trans, rows, k):
+    img = torch.empty(int(L.hg_gemm_x6_image_bytes(rows, k)) // 4, device="cuda:0")
+    vp = ctypes.c_void_p
+    rc = L.hg_gemm_x6_image_jobs((vp * 1)(P.data_ptr()), (ctypes.c_int64 * 1)(P.stride(0)), (ctypes.c_int * 1)(trans),
+                                 (ctypes.c_int64 * 1)(rows), (ctypes.c_int64 * 1)(k), (vp * 1)(img.data_ptr()), 1,
+                                 _stream())
+    assert rc == 0
+    return img
+
+
+# (rows, k, n): the image forms (hg_gemm_x6_image_jobs + hg_gemm_f32_img, B from its image, A staged
+# or from its image) of modes 0 and 1 against hg_gemm_f32 with the per-block staging, bit for bit
+# (same split, same MFMA order), ragged shapes
 IMG_CASES = [(3001, 705, 512), (777, 219, 768), (4096, 256, 128), (33, 7, 5), (65, 40, 129), (1, 705, 128)]
 
 
 @pytest.mark.parametrize("rows,k,n", IMG_CASES)
-def test_gemm_b_image_bitwise_equal(rows, k, n):
+def test_gemm_images_bitwise_equal(rows, k, n):
     _need_gpu()
     from humanoid import _native as N
     L = N.lib()
@@ -151,40 +162,69 @@ def test_gemm_b_image_bitwise_equal(rows, k, n):
     b = torch.randn(n, device=dev) * 0.1
     Wd = torch.randn(k, n, device=dev) / k ** 0.5  # mode 1: g [rows, k] x Wd [k, n]
     y = F.elu(torch.randn(rows, n, device=dev))
-    for tile in range(19, 27):
-        for mode, B, trans in ((0, W, 0), (1, Wd, 1)):
-            img = torch.empty(int(L.hg_gemm_x6_image_bytes(n, k, tile)) // 4, device=dev)
-            assert L.hg_gemm_x6_image(B.data_ptr(), B.stride(0), trans, n, k, tile, img.data_ptr(), _stream()) == 0
+    aimg = _image(L, x, 0, rows, k)
+    for mode, B, trans in ((0, W, 0), (1, Wd, 1)):
+        bimg = _image(L, B, trans, n, k)
+        for tile in range(19, 27):
             parts = int(L.hg_gemm_colpart_rows(rows, tile))
             outs = []
-            for use_img in (False, True):
+            for form in ("staged", "b_image", "ab_image"):
                 out = torch.full((rows, n + 2), 3.0, device=dev)
                 cp = torch.full((parts, n), float("nan"), device=dev) if mode == 1 else None
                 bias = b.data_ptr() if mode == 0 else None
                 Y, ldY = (y.data_ptr(), y.stride(0)) if mode == 1 else (None, 0)
                 cpp = cp.data_ptr() if cp is not None else None
-                if use_img:
-                    rc = L.hg_gemm_f32_img(mode, x.data_ptr(), x.stride(0), img.data_ptr(), bias, Y, ldY,
-                                           out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _stream())
-                else:
+                if form == "staged":
                     rc = L.hg_gemm_f32(mode, x.data_ptr(), x.stride(0), B.data_ptr(), B.stride(0), bias, Y, ldY,
                                        out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _stream())
+                else:
+                    ab = form == "ab_image"
+                    rc = L.hg_gemm_f32_img(mode, None if ab else x.data_ptr(), 0 if ab else x.stride(0),
+                                           aimg.data_ptr() if ab else None, bimg.data_ptr(), bias, Y, ldY,
+                                           out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _stream())
                 assert rc == 0
-                outs.append((out, cp))
-            (o0, c0), (o1, c1) = outs
-            assert torch.equal(o0, o1), f"tile {tile} mode {mode}"
-            assert (o1[:, n:] == 3.0).all()
-            if mode == 1:
-                assert torch.equal(c0, c1), f"tile {tile} colpart"
-    # arguments: an f32 tile or a misaligned image is refused
-    img = torch.empty(int(L.hg_gemm_x6_image_bytes(n, k, 20)) // 4 + 4, device=dev)
+                outs.append((form, out, cp))
+            _, o0, c0 = outs[0]
+            for form, o1, c1 in outs[1:]:
+                assert torch.equal(o0, o1), f"tile {tile} mode {mode} {form}"
+                assert (o1[:, n:] == 3.0).all()
+                if mode == 1:
+                    assert torch.equal(c0, c1), f"tile {tile} {form} colpart"
+    # arguments: a misaligned image, a mode without an image form, no A at all
     out = torch.empty(rows, n, device=dev)
-    assert L.hg_gemm_x6_image(W.data_ptr(), W.stride(0), 0, n, k, 5, img.data_ptr(), _stream()) != 0
-    assert L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), img.data_ptr() + 4, None, None, 0, out.data_ptr(),
+    bimg = _image(L, W, 0, n, k)
+    assert L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), None, bimg.data_ptr() + 4, None, None, 0, out.data_ptr(),
                              out.stride(0), None, rows, n, k, 0, 20, _stream()) != 0
-    assert L.hg_gemm_f32_img(2, x.data_ptr(), x.stride(0), img.data_ptr(), None, None, 0, out.data_ptr(),
+    assert L.hg_gemm_f32_img(2, x.data_ptr(), x.stride(0), None, bimg.data_ptr(), None, None, 0, out.data_ptr(),
+                             out.stride(0), None, rows, n, k, 0, 20, _stream()) != 0
+    assert L.hg_gemm_f32_img(0, None, 0, None, bimg.data_ptr(), None, None, 0, out.data_ptr(),
                              out.stride(0), None, rows, n, k, 0, 20, _stream()) != 0
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("rows,n,k,S", WG_CASES)
+def test_gemm_wgrad_images_match_fp64(rows, n, k, S):
+    """hg_gemm_wgrad_img from the two reduction-major images of gh [rows, n] and x [rows, k]: the
+    split-K slices summed here against fp64, under the bound of hg_gemm_f32_wgrad."""
+    _need_gpu()
+    from humanoid import _native as N
+    L = N.lib()
+    torch.manual_seed(rows + n + k + S + 1)
+    dev = "cuda:0"
+    gh = torch.randn(rows, n, device=dev)
+    x = torch.randn(rows, k, device=dev)
+    ref = gh.double().t() @ x.double()
+    bound = REL * (gh.double().abs().t() @ x.double().abs()) * 1.5
+    ai, bi = _image(L, gh, 1, n, rows), _image(L, x, 1, k, rows)
+    for tile in range(19, 27):
+        part = torch.full((S, n, k + 2), 5.0, device=dev)
+        rc = L.hg_gemm_wgrad_img(ai.data_ptr(), bi.data_ptr(), part.data_ptr(), k + 2, n * (k + 2), n, k, rows, S,
+                                 tile, _stream())
+        assert rc == 0
+        dw = part[:, :, :k].double().sum(0)
+        err = (dw - ref).abs()
+        assert (err <= bound).all(), f"tile {tile}: worst ratio {(err / bound).max().item():.3f}"
+        assert (part[:, :, k:] == 5.0).all()
 
 
 def test_gemm_rejects_bad_arguments():
