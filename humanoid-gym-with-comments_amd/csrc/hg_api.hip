@@ -11,9 +11,8 @@
 
 extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
                                hipStream_t stream);
-extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask, float* frame_obs,
-                              float* frame_priv, const float* obs_src, float* obs_dst, const float* priv_src,
-                              float* priv_dst, int frame_stack, int c_frame_stack, float inv_len_s,
+extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
+                              float* frame_obs, float* frame_priv, HgWindow obs, HgWindow priv, float inv_len_s,
                               int ep_slot, hipStream_t stream);
 
 namespace {
@@ -35,7 +34,7 @@ struct Layout {
   size_t off[HG_T_COUNT + 8];
   size_t bytes;
   // extra regions
-  size_t obs_buf[2], priv_buf[2], frame_obs, frame_priv, cfg, model, obs_noise, noise_counter;
+  size_t obs_buf, priv_buf, frame_obs, frame_priv, cfg, model, obs_noise, noise_counter;
 };
 
 enum { X_OBS0 = HG_T_COUNT, X_OBS1, X_PRIV0, X_PRIV1, X_FOBS, X_FPRIV, X_CFG, X_MODEL };
@@ -69,6 +68,14 @@ int dtype_of(int id) {
   }
 }
 
+// Observation histories as sliding windows: env row e holds F - 1 + HW frame slots; the current
+// stack (the policy input) is slots [head, head + F), head advancing by one per post launch, so a
+// step writes one frame per env instead of re-copying the whole stack.  When head reaches HW the
+// newest F - 1 frames move to slots 0 .. F - 2 in the same launch (once every HW steps).  HW is
+// shared by both tables, >= 26 and >= F - 1 of each.
+int win_advance(const hg_cfg* c) { return std::max(26, std::max(c->frame_stack, c->c_frame_stack) - 1); }
+int win_frames(int F, const hg_cfg* c) { return F - 1 + win_advance(c); }
+
 Layout make_layout(const hg_cfg* c) {
   Layout L;
   const int n = c->num_envs;
@@ -82,19 +89,19 @@ Layout make_layout(const hg_cfg* c) {
     if (id == HG_T_EP_STATS_RING) { L.off[id] = L.off[HG_T_EP_STATS] + 48 * sizeof(float); continue; }
     o += align256((size_t)soa_rows(id) * np * esize(dtype_of(id)));
   }
-  const size_t ob = (size_t)n * c->frame_stack * HG_OBS1 * 4, pb = (size_t)n * c->c_frame_stack * HG_PRIV1 * 4;
-  L.obs_buf[0] = o; o += align256(ob);
-  L.obs_buf[1] = o; o += align256(ob);
-  L.priv_buf[0] = o; o += align256(pb);
-  L.priv_buf[1] = o; o += align256(pb);
+  // the observation histories: one sliding window per env row (hg_obs_window_frames)
+  const size_t ob = (size_t)n * win_frames(c->frame_stack, c) * HG_OBS1 * 4;
+  const size_t pb = (size_t)n * win_frames(c->c_frame_stack, c) * HG_PRIV1 * 4;
+  L.obs_buf = o; o += align256(ob);
+  L.priv_buf = o; o += align256(pb);
   L.frame_obs = o; o += align256((size_t)n * HG_OBS1 * 4);
   L.frame_priv = o; o += align256((size_t)n * HG_PRIV1 * 4);
   L.cfg = o; o += align256(sizeof(hg_cfg));
   L.model = o; o += align256(sizeof(hg_model));
   L.obs_noise = o; o += align256((size_t)48 * np * 4);
   L.noise_counter = o; o += align256(sizeof(uint64_t));
-  L.off[HG_T_OBS_BUF] = L.obs_buf[0];
-  L.off[HG_T_PRIV_BUF] = L.priv_buf[0];
+  L.off[HG_T_OBS_BUF] = L.obs_buf;
+  L.off[HG_T_PRIV_BUF] = L.priv_buf;
   L.bytes = o;
   return L;
 }
@@ -106,7 +113,7 @@ struct Sim {
   size_t bytes;
   Layout L;
   HgState S;
-  int parity;  // which obs/priv buffer holds the latest stack
+  int head;    // first window slot of the current observation stack
   uint64_t post_seq = 0;  // post/reset launches so far: EP_STATS ring row of the next one
   int ep_slot = 0;        // ring row written by the latest one
   std::string err;
@@ -189,7 +196,7 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   }
   s->arena = (char*)arena;
   s->bytes = arena_bytes;
-  s->parity = 0;
+  s->head = 0;
   const int n = cfg->num_envs;
   HgState& S = s->S;
   S.n = n;
@@ -207,8 +214,8 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   S.last_dof_vel = (float*)P(HG_T_LAST_DOF_VEL);
   S.last_root_vel = (float*)P(HG_T_LAST_ROOT_VEL);
   S.commands = (float*)P(HG_T_COMMANDS);
-  S.obs = (float*)(s->arena + s->L.obs_buf[0]);
-  S.priv = (float*)(s->arena + s->L.priv_buf[0]);
+  S.obs = (float*)(s->arena + s->L.obs_buf);
+  S.priv = (float*)(s->arena + s->L.priv_buf);
   S.rew = (float*)P(HG_T_REW_BUF);
   S.reset_buf = (uint8_t*)P(HG_T_RESET_BUF);
   S.time_out = (uint8_t*)P(HG_T_TIME_OUT_BUF);
@@ -270,13 +277,13 @@ int hg_tensor(void* sim, int id, hg_desc* d) {
   d->offset_bytes = s->L.off[id];
   d->dtype = dtype_of(id);
   switch (id) {
-    case HG_T_OBS_BUF:  // both halves of the double buffer: [2, N, F*47]
-    case HG_T_PRIV_BUF: {
-      const int64_t w = id == HG_T_OBS_BUF ? (int64_t)s->cfg.frame_stack * HG_OBS1 : (int64_t)s->cfg.c_frame_stack * HG_PRIV1;
-      const size_t b1 = id == HG_T_OBS_BUF ? s->L.obs_buf[1] : s->L.priv_buf[1];
-      d->ndim = 3;
-      d->shape[0] = 2; d->shape[1] = n; d->shape[2] = w;
-      d->strides[0] = (int64_t)(b1 - d->offset_bytes) / 4; d->strides[1] = w; d->strides[2] = 1;
+    case HG_T_OBS_BUF:  // the history windows: [N, (F - 1 + HW) * width]; the stack = columns
+    case HG_T_PRIV_BUF: {  // [head * width, (head + F) * width) (hg_obs_head)
+      const int64_t w = id == HG_T_OBS_BUF ? (int64_t)win_frames(s->cfg.frame_stack, &s->cfg) * HG_OBS1
+                                           : (int64_t)win_frames(s->cfg.c_frame_stack, &s->cfg) * HG_PRIV1;
+      d->ndim = 2;
+      d->shape[0] = n; d->shape[1] = w;
+      d->strides[0] = w; d->strides[1] = 1;
       return HG_OK;
     }
     case HG_T_EP_STATS:
@@ -314,21 +321,34 @@ int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream
 }
 
 static int do_post(Sim* s, uint64_t counter, int mode, const uint8_t* mask, void* stream) {
-  const int p = s->parity;
-  float* ob0 = (float*)(s->arena + s->L.obs_buf[p]);
-  float* ob1 = (float*)(s->arena + s->L.obs_buf[1 - p]);
-  float* pb0 = (float*)(s->arena + s->L.priv_buf[p]);
-  float* pb1 = (float*)(s->arena + s->L.priv_buf[1 - p]);
+  const int hw = win_advance(&s->cfg);
+  const int old = s->head;
+  const int shift = old + 1 >= hw;  // slots old + 1 .. old + F - 1 move to 0 .. F - 2
+  const int head = shift ? 0 : old + 1;
   const float inv_len_s = 1.0f / ((float)s->cfg.max_episode_length * s->cfg.dt);
   const int slot = (int)(s->post_seq % HG_EP_RING);
+  const HgWindow wo = {(float*)(s->arena + s->L.obs_buf), (int64_t)win_frames(s->cfg.frame_stack, &s->cfg) * HG_OBS1,
+                       HG_OBS1, s->cfg.frame_stack, head, shift ? old + 1 : -1};
+  const HgWindow wp = {(float*)(s->arena + s->L.priv_buf),
+                       (int64_t)win_frames(s->cfg.c_frame_stack, &s->cfg) * HG_PRIV1, HG_PRIV1, s->cfg.c_frame_stack,
+                       head, shift ? old + 1 : -1};
   int rc = hg_launch_post(&s->S, &s->cfg, counter, mode, mask, (float*)(s->arena + s->L.frame_obs),
-                          (float*)(s->arena + s->L.frame_priv), ob0, ob1, pb0, pb1, s->cfg.frame_stack,
-                          s->cfg.c_frame_stack, inv_len_s, slot, (hipStream_t)stream);
+                          (float*)(s->arena + s->L.frame_priv), wo, wp, inv_len_s, slot, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_post launch failed");
   s->ep_slot = slot;
   s->post_seq++;
-  s->parity = 1 - p;
+  s->head = head;
   return HG_OK;
+}
+
+int hg_obs_head(void* sim) {
+  Sim* s = (Sim*)sim;
+  return s ? s->head : -1;
+}
+
+int hg_obs_window_advance(void* sim) {
+  Sim* s = (Sim*)sim;
+  return s ? win_advance(&s->cfg) : -1;
 }
 
 int hg_ep_stats_slot(void* sim) {

@@ -28,8 +28,8 @@ struct HgState {
   float* last_dof_vel;    // [12][np]
   float* last_root_vel;   // [6][np]
   float* commands;        // [4][np]
-  float* obs;             // [n][frame_stack*47] row-major
-  float* priv;            // [n][c_frame_stack*73] row-major
+  float* obs;             // [n][(frame_stack - 1 + HW) * 47] history windows (hg_api.hip)
+  float* priv;            // [n][(c_frame_stack - 1 + HW) * 73]
   float* rew;             // [np]
   uint8_t* reset_buf;     // [np]
   uint8_t* time_out;      // [np]
@@ -60,6 +60,16 @@ struct HgState {
   uint64_t* noise_counter;// [1] the post counter obs_noise was drawn for (~0: none)
   const hg_cfg* cfg;      // device copy
   const hg_model* model;  // device copy
+};
+
+// one observation history window table for the post launch: row e = win + e * rowlen, frame slots of
+// `width` floats; this launch writes the new frame into slot head + frames - 1, zeroes slots
+// head .. head + frames - 2 of reset envs and, when shift_src >= 0, first moves slots
+// shift_src .. shift_src + frames - 2 to 0 .. frames - 2
+struct HgWindow {
+  float* win;
+  int64_t rowlen;
+  int width, frames, head, shift_src;
 };
 
 // contact forces / rigid states are SoA too (field-major, [b*3+i][np] and [b*13+f][np]); the torch

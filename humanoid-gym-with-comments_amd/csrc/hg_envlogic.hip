@@ -8,8 +8,8 @@
 //   _get_phase/_get_gait_phase/compute_ref_state :683-744, _get_noise_scale_vec :748-768,
 //   and the obs/priv clip in step() :654-657.
 // Reset is mask-based (the reference's reset_buf.nonzero() host sync :796 is gone).
-// Frame stacking (deque append + stack, :880-887) is k_stack_stats below: a coalesced double-buffered
-// shift of the [N, frames*width] row-major history.
+// Frame stacking (deque append + stack, :880-887) is k_window_stats below: one frame written per env
+// into a sliding history window (no copy of the whole stack).
 #include "hg_common.h"
 
 namespace {
@@ -1120,19 +1120,15 @@ __global__ void __launch_bounds__(64 * PWAVES) k_post_step(HgState S, const hg_c
 #undef X
 }
 
-// history stacking: dst[e] = [src[e][W:], frame[e]] (src zeroed for reset envs), for the
-// observation and the privileged tables in one launch; one block per (env, table) row, threads
-// along the row so both the reads and the writes are contiguous.  The last block also folds the episode statistics
-// (ep_stats[k] = acc[k] / n_reset / episode_length_s when any env reset) and clears the
-// accumulators.
-struct StackT {
-  const float* src;
-  float* dst;
-  const float* frame;
-  int width, frames;
-};
-__global__ void __launch_bounds__(256) k_stack_stats(StackT A, StackT B, const uint8_t* __restrict__ reset, int n,
-                                                     float* ep_stats, float inv_len_s, int ring_slot) {
+// history windows (HgWindow, hg_api.hip): the reference's deque append + stack
+// (humanoid_env.py:880-887, history zeroed on reset) as one frame write per (env, table) into the
+// row's sliding window instead of a copy of the whole stack; one block per (env, table) row.  The
+// last block also folds the episode statistics (ep_stats[k] = acc[k] / n_reset / episode_length_s
+// when any env reset) and clears the accumulators.
+__global__ void __launch_bounds__(256) k_window_stats(HgWindow A, HgWindow B, const float* __restrict__ frame_a,
+                                                      const float* __restrict__ frame_b,
+                                                      const uint8_t* __restrict__ reset, int n, float* ep_stats,
+                                                      float inv_len_s, int ring_slot) {
   if (blockIdx.x == gridDim.x - 1) {
     const int k = threadIdx.x;
     float* acc = ep_stats + 24;
@@ -1150,25 +1146,27 @@ __global__ void __launch_bounds__(256) k_stack_stats(StackT A, StackT B, const u
     if (k < 24) acc[k] = 0.f;
     return;
   }
-  // one block per (env, table) row: no per-element index division (the former flat one-thread-
-  // per-element form spent its time in 64-bit divides), contiguous reads and writes along the row
   const int b = blockIdx.x;
   const bool a = b < n;
-  const StackT& T = a ? A : B;
+  const HgWindow& T = a ? A : B;
   const int e = a ? b : b - n;
-  const int row = T.frames * T.width;
-  const int cut = row - T.width;
+  const float* __restrict__ fr = (a ? frame_a : frame_b) + (size_t)e * T.width;
+  float* __restrict__ row = T.win + (size_t)e * T.rowlen;
+  const int hist = (T.frames - 1) * T.width;  // the older frames of the new stack
   const bool rs = reset[e] != 0;
-  const float* __restrict__ src = T.src + (size_t)e * row + T.width;
-  const float* __restrict__ fr = T.frame + (size_t)e * T.width - cut;
-  float* __restrict__ dst = T.dst + (size_t)e * row;
-  for (int k = threadIdx.x; k < row; k += blockDim.x) dst[k] = k >= cut ? fr[k] : (rs ? 0.f : src[k]);
+  float* __restrict__ h0 = row + (size_t)T.head * T.width;
+  if (T.shift_src >= 0) {  // h0 == row; source and destination slots do not overlap (HW >= frames - 1)
+    const float* __restrict__ src = row + (size_t)T.shift_src * T.width;
+    for (int k = threadIdx.x; k < hist; k += blockDim.x) h0[k] = rs ? 0.f : src[k];
+  } else if (rs) {
+    for (int k = threadIdx.x; k < hist; k += blockDim.x) h0[k] = 0.f;
+  }
+  for (int k = threadIdx.x; k < T.width; k += blockDim.x) h0[hist + k] = fr[k];
 }
 
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
-                              float* frame_obs, float* frame_priv, const float* obs_src, float* obs_dst,
-                              const float* priv_src, float* priv_dst, int frame_stack, int c_frame_stack,
-                              float inv_len_s, int ep_slot, hipStream_t stream) {
+                              float* frame_obs, float* frame_priv, HgWindow obs, HgWindow priv, float inv_len_s,
+                              int ep_slot, hipStream_t stream) {
   const int n = S->n;
   if (mode == 0)
     hipLaunchKernelGGL(k_post_step, dim3((n + PEB - 1) / PEB), dim3(64 * PWAVES), 0, stream, *S, *hcfg, counter,
@@ -1177,9 +1175,7 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
     hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
                        frame_priv);
   const int g = 2 * n + 1;  // one block per (env, table) row + the statistics block
-  const StackT A = {obs_src, obs_dst, frame_obs, HG_OBS1, frame_stack};
-  const StackT B = {priv_src, priv_dst, frame_priv, HG_PRIV1, c_frame_stack};
-  hipLaunchKernelGGL(k_stack_stats, dim3(g), dim3(256), 0, stream, A, B, S->reset_buf, n, S->ep_stats, inv_len_s,
-                     ep_slot);
+  hipLaunchKernelGGL(k_window_stats, dim3(g), dim3(64), 0, stream, obs, priv, frame_obs, frame_priv, S->reset_buf, n,
+                     S->ep_stats, inv_len_s, ep_slot);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

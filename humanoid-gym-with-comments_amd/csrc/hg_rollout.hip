@@ -6,7 +6,8 @@
 //     log p(a) = sum_j [ -(a_j - mu_j)^2 / (2 sigma_j^2) - log sigma_j - log sqrt(2 pi) ]
 //     (torch.distributions.Normal.log_prob summed over actions); writes actions, log-prob, mu,
 //     sigma, value into slot t of the storage, and copies the observation / critic observation
-//     rows into slot t (fp32 or fp16 storage) in the same launch.
+//     rows into slot t (fp32 or fp16 storage) in the same launch — for the actor observation
+//     optionally only a column range (the newest frame of the stack: frame-only storage).
 //   hg_rollout_env (after env.step): rewards[t] = r + gamma * V * time_out (the time-out
 //     bootstrap of ppo.py:132-133), dones[t] = reset; with values == NULL the bootstrap is
 //     deferred: rewards[t] = r and time_outs[t] is kept for the batched value pass.
@@ -14,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "hg_common.h"
 
@@ -36,25 +39,15 @@ template <>
 __device__ inline void store_obs<__half>(__half* dst, float v) { *dst = __float2half(v); }
 
 template <typename OT>
-__device__ inline void store_obs4(OT* dst, float4 v);
-template <>
-__device__ inline void store_obs4<float>(float* dst, float4 v) { *reinterpret_cast<float4*>(dst) = v; }
-template <>
-__device__ inline void store_obs4<__half>(__half* dst, float4 v) {
-  const __half2 a = __floats2half2_rn(v.x, v.y), b = __floats2half2_rn(v.z, v.w);
-  reinterpret_cast<__half2*>(dst)[0] = a;
-  reinterpret_cast<__half2*>(dst)[1] = b;
-}
-
-template <typename OT>
 __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, const float* __restrict__ std,
                                             const float* __restrict__ value, const float* __restrict__ obs,
                                             const float* __restrict__ cobs, int n, int A, int64_t obs_w,
-                                            int64_t cobs_w, float* __restrict__ act_out, float* __restrict__ logp_out,
+                                            int64_t cobs_w, int64_t obs_ld, int64_t obs_c0, int64_t cobs_ld,
+                                            float* __restrict__ act_out, float* __restrict__ logp_out,
                                             float* __restrict__ mu_out, float* __restrict__ sigma_out,
                                             float* __restrict__ value_out, OT* __restrict__ obs_out,
                                             OT* __restrict__ cobs_out, int row_offset, uint64_t seed,
-                                            uint64_t counter, int env_blocks, int vec) {
+                                            uint64_t counter, int env_blocks) {
   if ((int)blockIdx.x < env_blocks) {
     const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
     if (A <= ACT_LANES) {
@@ -103,23 +96,26 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
     if (value) value_out[e] = value[e];
     return;
   }
-  // observation rows -> storage slot: both [n, width] tables are contiguous, so they are copied
-  // as flat arrays, 4 elements per thread (float4 loads) with a scalar tail
-  const int64_t tot_o = (int64_t)n * obs_w, tot_c = (int64_t)n * cobs_w;
-  const int64_t q_o = vec ? tot_o >> 2 : 0, q_c = vec ? tot_c >> 2 : 0;
-  const int64_t r_o = tot_o - 4 * q_o, r_c = tot_c - 4 * q_c;
-  const int64_t stride = (int64_t)(gridDim.x - env_blocks) * TPB;
-  const int64_t i0 = (int64_t)(blockIdx.x - env_blocks) * TPB + threadIdx.x;
-  for (int64_t i = i0; i < q_o + q_c; i += stride) {
-    const bool o = i < q_o;
-    const int64_t k = o ? i : i - q_o;
-    const float4 v = reinterpret_cast<const float4*>(o ? obs : cobs)[k];
-    store_obs4<OT>((o ? obs_out : cobs_out) + 4 * k, v);
-  }
-  for (int64_t i = i0; i < r_o + r_c; i += stride) {
-    const bool o = i < r_o;
-    const int64_t k = o ? 4 * q_o + i : 4 * q_c + (i - r_o);
-    store_obs<OT>((o ? obs_out : cobs_out) + k, (o ? obs : cobs)[k]);
+  // observation rows -> storage slot: one wave per (table, row), lanes along the row; source rows
+  // strided (the env's stacks are column slices of its history windows), storage rows packed
+  const int64_t rows = cobs_w > 0 ? 2 * (int64_t)n : n;
+  const int64_t wstride = (int64_t)(gridDim.x - env_blocks) * (TPB / 64);
+  const int lane = threadIdx.x & 63;
+  for (int64_t q = (int64_t)(blockIdx.x - env_blocks) * (TPB / 64) + (threadIdx.x >> 6); q < rows; q += wstride) {
+    const bool o = q < n;
+    const int64_t r = o ? q : q - n;
+    const int64_t w = o ? obs_w : cobs_w;
+    const float* __restrict__ src = o ? obs + r * obs_ld + obs_c0 : cobs + r * cobs_ld;
+    OT* __restrict__ dst = (o ? obs_out : cobs_out) + r * w;
+    int64_t c = lane;
+    for (; c + 192 < w; c += 256) {
+      const float a = src[c], b = src[c + 64], d = src[c + 128], e = src[c + 192];
+      store_obs<OT>(dst + c, a);
+      store_obs<OT>(dst + c + 64, b);
+      store_obs<OT>(dst + c + 128, d);
+      store_obs<OT>(dst + c + 192, e);
+    }
+    for (; c < w; c += 64) store_obs<OT>(dst + c, src[c]);
   }
 }
 
@@ -140,31 +136,31 @@ __global__ void __launch_bounds__(TPB) k_env(const float* __restrict__ rew, cons
 
 extern "C" int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
                               const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
-                              int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
-                              float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out,
-                              int obs_fp16, int row_offset, uint64_t seed, uint64_t counter, void* stream) {
+                              int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
+                              float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
+                              void* obs_out, void* critic_obs_out, int obs_fp16, int row_offset, uint64_t seed,
+                              uint64_t counter, void* stream) {
   if (!mean || !std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out ||
-      !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 ||
-      (critic_obs_width > 0 && (!critic_obs || !critic_obs_out)))
+      !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 || obs_col0 < 0 ||
+      obs_ld < obs_col0 + obs_width || (critic_obs_width > 0 && (!critic_obs || !critic_obs_out ||
+                                                                 critic_obs_ld < critic_obs_width)))
     return HG_ERR_ARG;
-  // 16-byte loads / 16-byte (fp32) or 8-byte (fp16) stores when every table is aligned for them
-  const uintptr_t in_al = (uintptr_t)obs | (critic_obs_width > 0 ? (uintptr_t)critic_obs : 0);
-  const uintptr_t out_al = (uintptr_t)obs_out | (critic_obs_width > 0 ? (uintptr_t)critic_obs_out : 0);
-  const int vec = in_al % 16 == 0 && out_al % (obs_fp16 ? 8 : 16) == 0;
   const int64_t env_threads = (int64_t)num_envs * (num_actions <= ACT_LANES ? ACT_LANES : 1);
   const int env_blocks = (int)((env_threads + TPB - 1) / TPB);
-  const int copy_blocks = 512;
+  const int64_t copy_rows = critic_obs_width > 0 ? 2 * (int64_t)num_envs : num_envs;
+  const int copy_blocks = (int)std::min<int64_t>((copy_rows + TPB / 64 - 1) / (TPB / 64), 2048);
+  const int64_t cw = critic_obs_width > 0 ? critic_obs_width : 0;
   hipStream_t s = (hipStream_t)stream;
   if (obs_fp16)
     hipLaunchKernelGGL(k_act<__half>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
-                       critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
+                       critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, critic_obs_ld,
                        actions_out, logp_out, mu_out, sigma_out, value_out, (__half*)obs_out,
-                       (__half*)critic_obs_out, row_offset, seed, counter, env_blocks, vec);
+                       (__half*)critic_obs_out, row_offset, seed, counter, env_blocks);
   else
     hipLaunchKernelGGL(k_act<float>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
-                       critic_obs, num_envs, num_actions, obs_width, critic_obs_width > 0 ? critic_obs_width : 0,
+                       critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, critic_obs_ld,
                        actions_out, logp_out, mu_out, sigma_out, value_out, (float*)obs_out, (float*)critic_obs_out,
-                       row_offset, seed, counter, env_blocks, vec);
+                       row_offset, seed, counter, env_blocks);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
@@ -320,5 +316,79 @@ extern "C" int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_r
   for (int t = 0; t < A.ntab; t++) A.short_rows &= (A.t[t].cvt == 0 && A.t[t].es == 4 && A.t[t].width <= 64 * GK);
   const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
   hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(TPB), 0, (hipStream_t)stream, idx, rows, src_rows, A);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Minibatch rows of a frame-only observation storage (RolloutStorage with obs_frames): slot t of
+// the rollout keeps only the newest W-element frame of the stacked observation the policy saw,
+// slot 0 also the whole stack (init).  The stack of storage row s = t N + e is rebuilt as the
+// reference's deque would have held it (humanoid_env.py:880-887): position j < F holds the
+// newest frame of slot tau = t - (F - 1 - j) (tau < 0: position j + t of init), zero when the env
+// was reset by a post step r with tau <= r <= t - 1 (dones[r][e]; the reset zeroes the history
+// before its new frame).  One wave per output row; lane l < F - 1 tests dones[t - 1 - l][e] and
+// one ballot gives the latest reset.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+template <typename S, typename D>
+__global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restrict__ idx, int64_t rows,
+                                                        const S* __restrict__ frames, const S* __restrict__ init,
+                                                        const uint8_t* __restrict__ dones, int T, int N, int F, int W,
+                                                        D* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= rows) return;
+  const int64_t total = (int64_t)T * N;
+  int64_t s = idx[i];
+  s = s < 0 ? 0 : (s >= total ? total - 1 : s);  // never read out of bounds
+  const int t = (int)(s / N), e = (int)(s - (int64_t)t * N);
+  const int back = t - 1 - lane;
+  const bool rs = lane < F - 1 && back >= 0 && dones[(int64_t)back * N + e] != 0;
+  const uint64_t m = __ballot(rs);
+  const int jz = m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0;  // positions j < jz are zero
+  const int64_t row = (int64_t)F * W;
+  D* __restrict__ out = dst + i * row;
+  constexpr int G = 8;  // frames per batch of loads in flight
+  for (int j0 = 0; j0 < F; j0 += G) {
+    for (int c = lane; c < W; c += 64) {
+      float v[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const int j = j0 + g;
+        v[g] = 0.f;
+        if (j < F && j >= jz) {
+          const int tau = t - (F - 1 - j);
+          v[g] = tau >= 0 ? (float)frames[((int64_t)tau * N + e) * W + c] : (float)init[(int64_t)e * row + (int64_t)(j + t) * W + c];
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; g++)
+        if (j0 + g < F) out[(int64_t)(j0 + g) * W + c] = (D)v[g];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* frames, const void* init,
+                                 const uint8_t* dones, int T, int N, int F, int W, int src_dtype, void* dst,
+                                 int dst_dtype, void* stream) {
+  if (!idx || rows <= 0 || !frames || !init || !dones || !dst || T <= 0 || N <= 0 || F <= 0 || F > 64 || W <= 0)
+    return HG_ERR_ARG;
+  const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
+  if (blocks > 0x7fffffff) return HG_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g((unsigned)blocks), b(TPB);
+#define HG_GS(ST, DT) \
+  hipLaunchKernelGGL((k_gather_stacked<ST, DT>), g, b, 0, s, idx, rows, (const ST*)frames, (const ST*)init, dones, T, N, F, \
+                     W, (DT*)dst)
+  if (src_dtype == HG_DTYPE_F32 && dst_dtype == HG_DTYPE_F32) HG_GS(float, float);
+  else if (src_dtype == HG_DTYPE_F32 && dst_dtype == HG_DTYPE_BF16) HG_GS(float, __bf16);
+  else if (src_dtype == HG_DTYPE_F16 && dst_dtype == HG_DTYPE_F16) HG_GS(_Float16, _Float16);
+  else if (src_dtype == HG_DTYPE_F16 && dst_dtype == HG_DTYPE_BF16) HG_GS(_Float16, __bf16);
+  else if (src_dtype == HG_DTYPE_F16 && dst_dtype == HG_DTYPE_F32) HG_GS(_Float16, float);
+  else return HG_ERR_ARG;
+#undef HG_GS
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

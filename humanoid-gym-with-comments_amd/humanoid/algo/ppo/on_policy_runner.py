@@ -65,8 +65,13 @@ class OnPolicyRunner:
         self.num_steps_per_env = self.cfg["num_steps_per_env"]
         self.save_interval = self.cfg["save_interval"]
         obs_dtype = {"fp32": torch.float32, "fp16": torch.float16}[self.cfg.get("storage_obs_dtype", "fp32")]
+        # frame-only actor observation storage when the env stacks frames (one frame per env-step
+        # written instead of the whole stack; rollout_storage.py)
+        ecfg = getattr(getattr(env, "cfg", None), "env", None)
+        fs, w1 = getattr(ecfg, "frame_stack", None), getattr(ecfg, "num_single_obs", None)
+        obs_frames = (int(fs), int(w1)) if fs and w1 and int(fs) * int(w1) == env.num_obs else None
         self.alg.init_storage(env.num_envs, self.num_steps_per_env, [env.num_obs], [env.num_privileged_obs],
-                              [env.num_actions], obs_dtype=obs_dtype)
+                              [env.num_actions], obs_dtype=obs_dtype, obs_frames=obs_frames)
         # the action noise is keyed by the global env id of each storage row
         env_cfg = getattr(getattr(env, "cfg", None), "env", None)
         self.alg.row_offset = int(getattr(env_cfg, "env_offset", 0) or 0)

@@ -62,7 +62,8 @@ def _slot_views(st, t):
               "mu": st.mu[t], "sigma": st.sigma[t], "rewards": st.rewards[t], "dones": st.dones[t]}
         sl.update(p_actions=vp(sl["actions"].data_ptr()), p_logp=vp(st.actions_log_prob[t].data_ptr()),
                   p_mu=vp(sl["mu"].data_ptr()), p_sigma=vp(sl["sigma"].data_ptr()), p_values=vp(sl["values"].data_ptr()),
-                  p_obs=vp(st.observations[t].data_ptr()), p_priv=vp(priv[t].data_ptr()) if priv is not None else None,
+                  p_obs=vp((st.obs_frames if st.obs_frames is not None else st.observations)[t].data_ptr()),
+                  p_priv=vp(priv[t].data_ptr()) if priv is not None else None,
                   p_rewards=vp(sl["rewards"].data_ptr()), p_dones=vp(sl["dones"].data_ptr()))
         cache[t] = sl
     return sl
@@ -180,9 +181,13 @@ class PPO:
                 g["lr"] = self._lr
 
     def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape,
-                     obs_dtype=torch.float32):
+                     obs_dtype=torch.float32, obs_frames=None):
+        """obs_frames = (frame_stack, frame width) of a frame-stacking env: frame-only actor
+        observation storage (rollout_storage.py module docstring) on the device path."""
+        if not self._on_device or critic_obs_shape[0] is None:
+            obs_frames = None
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
-                                      action_shape, self.device, obs_dtype=obs_dtype)
+                                      action_shape, self.device, obs_dtype=obs_dtype, obs_frames=obs_frames)
 
     def test_mode(self):
         self.actor_critic.eval()
@@ -193,8 +198,8 @@ class PPO:
     def _fused_rollout_ok(self, obs, critic_obs):
         st = self.storage
         return (self._on_device and self.use_fused_rollout and st is not None and hasattr(self.actor_critic, "_mlp")
-                and obs.is_cuda and obs.dtype == torch.float32 and obs.is_contiguous()
-                and critic_obs.dtype == torch.float32 and critic_obs.is_contiguous()
+                and obs.is_cuda and obs.dtype == torch.float32 and obs.dim() == 2 and obs.stride(1) == 1
+                and critic_obs.dtype == torch.float32 and critic_obs.dim() == 2 and critic_obs.stride(1) == 1
                 and st.step < st.num_transitions_per_env)
 
     def _act_fused(self, obs, critic_obs):
@@ -212,12 +217,20 @@ class PPO:
         priv = st.privileged_observations
         sl = _slot_views(st, t)
         s = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
+        if st.obs_frames is not None:
+            # frame-only storage: the newest frame of the stack per slot, slot 0's whole stack
+            if t == 0:
+                st.obs_init.copy_(obs)
+            w, c0 = st.frame_width, obs.shape[1] - st.frame_width
+        else:
+            w, c0 = obs.shape[1], 0
         N.check(N.lib().hg_rollout_act(
             p(mean), p(std), p(value) if value is not None else None, p(obs),
             p(critic_obs) if priv is not None else None, obs.shape[0],
-            mean.shape[1], ctypes.c_int64(obs.shape[1]), ctypes.c_int64(critic_obs.shape[1] if priv is not None else 0),
+            mean.shape[1], ctypes.c_int64(w), ctypes.c_int64(critic_obs.shape[1] if priv is not None else 0),
+            ctypes.c_int64(obs.stride(0)), ctypes.c_int64(c0), ctypes.c_int64(critic_obs.stride(0)),
             sl["p_actions"], sl["p_logp"], sl["p_mu"], sl["p_sigma"], sl["p_values"] if value is not None else None,
-            sl["p_obs"], sl["p_priv"], int(st.observations.dtype == torch.float16), int(self.row_offset),
+            sl["p_obs"], sl["p_priv"], int(st.obs_dtype == torch.float16), int(self.row_offset),
             ctypes.c_uint64(self._rollout_seed), ctypes.c_uint64(self._rollout_counter), s))
         self._rollout_counter += 1
         tr.actions = sl["actions"]
@@ -504,14 +517,15 @@ class PPO:
     # ------------------------------------------------------------------------------------------
     def _storage_key(self):
         st = self.storage
-        return (st.observations.data_ptr(), st.num_envs, st.num_transitions_per_env,
+        return (st.obs_key(), st.num_envs, st.num_transitions_per_env,
                 getattr(self.optimizer, "version", 0))
 
     def _capture(self, mb):
         st = self.storage
-        dev = st.observations.device
-        obs = st.observations.flatten(0, 1)
-        critic = st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else obs
+        dev = st.rewards.device
+        frames = st.obs_frames is not None  # frame-only storage: the obs rows come from hg_gather_stacked
+        obs = None if frames else st.observations.flatten(0, 1)
+        critic = (st.privileged_observations.flatten(0, 1) if st.privileged_observations is not None else obs)
         # the per-sample scalars/12-vectors are packed once per update into one [T*N, 40] table so a
         # minibatch needs three gathers (obs, critic obs, table) instead of ten
         A = st.actions.shape[-1]
@@ -526,7 +540,8 @@ class PPO:
         if self._lin_vel_packed:
             self._pack_src.append(critic.view(st.num_transitions_per_env, st.num_envs, -1)[..., 53:56])
         widths = [t.shape[-1] for t in self._pack_src]
-        self._packed = torch.empty(obs.shape[0], sum(widths), dtype=torch.float32, device=dev)
+        self._packed = torch.empty(st.num_transitions_per_env * st.num_envs, sum(widths), dtype=torch.float32,
+                                   device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
         # [value, surrogate, lin-vel loss sums, KL mean of the current minibatch]: the fused loss
         # accumulates into it directly
@@ -538,13 +553,15 @@ class PPO:
         if self._flat_grad is None:
             self.optimizer.zero_grad(set_to_none=True)  # backward allocates the grads in the graph pool
         # minibatch rows land in static buffers: the three row gathers are one HIP launch
-        self._mb_obs = torch.empty(mb, obs.shape[1], dtype=mb_dtype or obs.dtype, device=dev)
+        self._mb_obs = torch.empty(mb, st.obs_shape[0], dtype=mb_dtype or st.obs_dtype, device=dev)
         self._mb_critic = (torch.empty(mb, critic.shape[1], dtype=mb_dtype or critic.dtype, device=dev)
                            if critic is not obs else self._mb_obs)
         self._mb_packed = torch.empty(mb, self._packed.shape[1], dtype=torch.float32, device=dev)
-        tables = [(obs, self._mb_obs), (self._packed, self._mb_packed)]
+        tables = [(self._packed, self._mb_packed)]
+        if not frames:
+            tables.insert(0, (obs, self._mb_obs))
         if critic is not obs:
-            tables.insert(1, (critic, self._mb_critic))
+            tables.insert(1 if not frames else 0, (critic, self._mb_critic))
         self._mb_tables, self._mb_widths = tables, widths
         # world size 1: the whole update (epochs x minibatches, each with its LR rule and Adam step)
         # is ONE graph reading its row indices from a static permutation buffer; with ranks to
@@ -573,6 +590,8 @@ class PPO:
         if self._flat_grad is not None:
             self._flat_grad.zero_()
         gather_rows(idx, self._mb_tables)
+        if self.storage.obs_frames is not None:
+            self.storage.gather_stacked(idx, self._mb_obs)
         crit_b = self._mb_critic
         b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
         pk = self._mb_packed
@@ -624,7 +643,7 @@ class PPO:
         if self._graphs is None or self._graphs[2] != mb or self._graphs[3] != self._storage_key():
             self._capture(mb)
         ga, gb = self._graphs[0], self._graphs[1]
-        dev = st.observations.device
+        dev = st.rewards.device
         torch.cat([t.flatten(0, 1) for t in self._pack_src], dim=1, out=self._packed)
         self._sums.zero_()
         if gb is None:  # the whole update as one graph

@@ -8,6 +8,13 @@ with global statistics (collective (3)).
 
 There is no CPU path: GAE needs the HIP kernel (tensors on a ROCm device).  Test code may set
 ``storage.gae_fn`` to an oracle explicitly.
+
+Frame-only observations (``obs_frames=(F, W)``, device rollouts of a frame-stacking env): the
+actor observation of slot t is the env's F-frame stack (humanoid_env.py:880-887), so the storage
+keeps only its newest W-element frame per slot plus slot 0's whole stack, and a minibatch's rows
+are rebuilt from them by ``hg_gather_stacked`` (the dones mark where a reset zeroed the history):
+W instead of F*W observation elements written per env-step.  ``observations`` materialises the
+[T, N, F*W] view on demand.
 """
 import ctypes
 import os
@@ -35,10 +42,11 @@ class RolloutStorage:
             self.__init__()
 
     def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, actions_shape,
-                 device="cpu", obs_dtype=torch.float32):
+                 device="cpu", obs_dtype=torch.float32, obs_frames=None):
         """obs_dtype float16 (config 5) halves the observation buffers, the largest part of the
         storage (705 + 219 floats per env-step); minibatches are handed out in that dtype and the
-        policy consumes them under autocast."""
+        policy consumes them under autocast.  obs_frames = (F, W) with F * W = obs_shape[0]: the
+        frame-only actor observation storage (module docstring)."""
         self.device = device
         self.obs_shape = obs_shape
         self.privileged_obs_shape = privileged_obs_shape
@@ -49,7 +57,17 @@ class RolloutStorage:
             return torch.zeros(T, N, *shape, device=device, dtype=dtype)
 
         self.obs_dtype = obs_dtype
-        self.observations = z(*obs_shape, dtype=obs_dtype)
+        self.obs_frames = self.obs_init = None
+        if obs_frames is not None:
+            F, W = int(obs_frames[0]), int(obs_frames[1])
+            if F * W != int(obs_shape[0]) or len(obs_shape) != 1:
+                raise ValueError(f"obs_frames {obs_frames} do not tile the observation shape {obs_shape}")
+            self.frame_stack, self.frame_width = F, W
+            self.obs_frames = z(W, dtype=obs_dtype)  # [T, N, W]: the newest frame of each slot's stack
+            self.obs_init = torch.zeros(N, F * W, device=device, dtype=obs_dtype)  # slot 0's stack
+            self._observations = None
+        else:
+            self._observations = z(*obs_shape, dtype=obs_dtype)
         self.privileged_observations = (z(*privileged_obs_shape, dtype=obs_dtype)
                                         if privileged_obs_shape[0] is not None else None)
         self.rewards = z(1)
@@ -72,11 +90,48 @@ class RolloutStorage:
         self._stats_buf = None  # [hg_gae_stats_len(N)] f64: (sum A, sum A^2) + the kernel's block partials
         self._stats = torch.zeros(2, dtype=torch.float64, device=device)
 
+    @property
+    def observations(self):
+        """[T, N, obs] actor observations (frame-only storage: rebuilt on each access)."""
+        if self.obs_frames is None:
+            return self._observations
+        T, N = self.num_transitions_per_env, self.num_envs
+        idx = torch.arange(T * N, device=self.device, dtype=torch.int64)
+        out = torch.empty(T * N, self.obs_shape[0], dtype=self.obs_dtype, device=self.device)
+        self.gather_stacked(idx, out)
+        return out.view(T, N, -1)
+
+    def obs_key(self):
+        """Address identifying the actor observation buffers (captured-graph keys)."""
+        return (self.obs_frames if self.obs_frames is not None else self._observations).data_ptr()
+
+    def gather_stacked(self, idx, dst):
+        """dst[i] = the stacked actor observation of storage row idx[i] (frame-only storage), one
+        hg_gather_stacked launch on the current stream; dst [rows, F*W] of the storage dtype, or
+        bfloat16."""
+        from humanoid import _native as N
+        T, Nn, F, W = self.num_transitions_per_env, self.num_envs, self.frame_stack, self.frame_width
+        if (idx.dtype != torch.int64 or not idx.is_contiguous() or not dst.is_contiguous()
+                or dst.shape != (idx.numel(), F * W)):
+            raise RuntimeError("gather_stacked: idx contiguous int64, dst contiguous [rows, F*W]")
+        codes = N.DTYPE_CODES
+        s = ctypes.c_void_p(torch.cuda.current_stream(idx.device).cuda_stream)
+        p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        rc = N.lib().hg_gather_stacked(p(idx), idx.numel(), p(self.obs_frames), p(self.obs_init), p(self.dones), T, Nn,
+                                       F, W, codes[str(self.obs_dtype)[6:]], p(dst), codes[str(dst.dtype)[6:]], s)
+        if rc != 0:
+            raise RuntimeError(f"hg_gather_stacked failed ({rc})")
+
     def add_transitions(self, transition: Transition):
         if self.step >= self.num_transitions_per_env:
             raise AssertionError("Rollout buffer overflow")
         t = self.step
-        self.observations[t].copy_(transition.observations)
+        if self.obs_frames is not None:
+            if t == 0:
+                self.obs_init.copy_(transition.observations)
+            self.obs_frames[t].copy_(transition.observations[:, -self.frame_width:])
+        else:
+            self._observations[t].copy_(transition.observations)
         if self.privileged_observations is not None:
             self.privileged_observations[t].copy_(transition.critic_observations)
         self.actions[t].copy_(transition.actions)

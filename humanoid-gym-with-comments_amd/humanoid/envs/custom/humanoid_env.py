@@ -264,12 +264,16 @@ class XBotLFreeEnv(BaseTask):
         self.last_dof_vel = self._view(T["LAST_DOF_VEL"])
         self.last_root_vel = self._view(T["LAST_ROOT_VEL"])
         self.commands = self._view(T["COMMANDS"])
-        self._obs2 = self._view(T["OBS_BUF"])
-        self._priv2 = self._view(T["PRIV_BUF"])
-        # the two halves of each double buffer as fixed views (no tensor indexing per access)
-        self._obs2v = tuple(self._obs2.unbind(0))
-        self._priv2v = tuple(self._priv2.unbind(0))
-        self._parity = 0
+        # observation histories: one sliding window per env row (HG_T_OBS_BUF / HG_T_PRIV_BUF); the
+        # stacks are the [N, F * width] column slices at the sim's head slot (hg_obs_head), one
+        # fixed strided view per head position (no tensor indexing per access)
+        self._obs_win = self._view(T["OBS_BUF"])
+        self._priv_win = self._view(T["PRIV_BUF"])
+        hw = int(self.hg.hg_obs_window_advance(self.sim))
+        fo, fp = int(self.cfg.env.frame_stack), int(self.cfg.env.c_frame_stack)
+        wo, wp = self._obs_win.shape[1] // (fo - 1 + hw), self._priv_win.shape[1] // (fp - 1 + hw)
+        self._obs_views = tuple(self._obs_win[:, h * wo:(h + fo) * wo] for h in range(hw))
+        self._priv_views = tuple(self._priv_win[:, h * wp:(h + fp) * wp] for h in range(hw))
         self.rew_buf = self._view(T["REW_BUF"])
         self._reset_u8 = self._view(T["RESET_BUF"])
         self._timeout_u8 = self._view(T["TIME_OUT_BUF"])
@@ -431,11 +435,11 @@ class XBotLFreeEnv(BaseTask):
 
     @property
     def obs_buf(self):
-        return self._obs2v[self._parity]
+        return self._obs_views[self.hg.hg_obs_head(self.sim)]
 
     @property
     def privileged_obs_buf(self):
-        return self._priv2v[self._parity]
+        return self._priv_views[self.hg.hg_obs_head(self.sim)]
 
     @property
     def dof_state(self):
@@ -483,7 +487,6 @@ class XBotLFreeEnv(BaseTask):
         mp = ctypes.c_void_p(mask_u8.data_ptr()) if mask_u8 is not None else None
         N.check(self.hg.hg_reset_masked(self.sim, mp, ctypes.c_uint64(self.common_step_counter), self._stream()),
                 self.sim)
-        self._parity ^= 1
         self._publish_extras()
 
     def step(self, actions):
@@ -513,7 +516,6 @@ class XBotLFreeEnv(BaseTask):
         N.check(self.hg.hg_post(self.sim, ctypes.c_uint64(self.common_step_counter), s), self.sim)
         if kt is not None:
             kt.stop("k_post")
-        self._parity ^= 1
         self._publish_extras()
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 

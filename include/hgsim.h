@@ -160,8 +160,10 @@ enum hg_tensor_id {
   HG_T_ACTIONS, HG_T_LAST_ACTIONS, HG_T_LAST_LAST_ACTIONS,
   HG_T_LAST_DOF_VEL, HG_T_LAST_ROOT_VEL,
   HG_T_COMMANDS,         /* [N,4] */
-  HG_T_OBS_BUF,          /* [N, frame_stack*47] row-major (policy input) */
-  HG_T_PRIV_BUF,         /* [N, c_frame_stack*73] row-major */
+  HG_T_OBS_BUF,          /* [N, (frame_stack - 1 + HW) * 47] observation history window per env: the
+                            stacked policy input is columns [h * 47, (h + frame_stack) * 47), h =
+                            hg_obs_head() (a strided [N, frame_stack*47] view; HW = hg_obs_window_advance) */
+  HG_T_PRIV_BUF,         /* [N, (c_frame_stack - 1 + HW) * 73], its stack columns [h * 73, (h + c_frame_stack) * 73) */
   HG_T_REW_BUF,          /* [N] */
   HG_T_RESET_BUF,        /* [N] bool */
   HG_T_TIME_OUT_BUF,     /* [N] bool */
@@ -207,6 +209,12 @@ int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream
  * bookkeeping, no device access) */
 int hg_ep_stats_slot(void* sim);
 int hg_post(void* sim, uint64_t common_step_counter, void* stream);
+/* first frame slot h of the current observation stacks in the HG_T_OBS_BUF / HG_T_PRIV_BUF
+ * windows (host-side bookkeeping): every hg_post / hg_reset_masked advances it by one and writes
+ * only the new frame; at h = HW - 1 the next launch moves the newest frame_stack - 1 frames to
+ * slots 0.. and h restarts at 0.  Replaces the deque re-stacking of humanoid_env.py:880-887. */
+int hg_obs_head(void* sim);
+int hg_obs_window_advance(void* sim);
 /* Runtime parameter update (curricula, e.g. the push-recovery ramp of config 5): copies *cfg into
  * the handle and, stream-ordered, into the device copy the kernels read.  Fields that size or
  * lay out the arena (num_envs, frame stacks, terrain tables, decimation) must be unchanged. */
@@ -257,16 +265,20 @@ int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int6
  * the global env id under data parallelism), their
  * Normal log-prob summed over actions, mu, sigma, value, and the observation / critic
  * observation rows, all into storage slot t (obs_out/critic_obs_out fp32, or fp16 when
- * obs_fp16).  mean [N,A], std [A], value [N], obs [N,obs_width], critic_obs [N,critic_width]:
- * contiguous device f32; value may be NULL (values computed later in one batched critic pass).
+ * obs_fp16).  mean [N,A], std [A], value [N]: contiguous device f32; obs row r's columns
+ * [obs_col0, obs_col0 + obs_width) at obs + r obs_ld (the newest frame only, for frame-only
+ * storage: obs_col0 = (F - 1) W, obs_width = W), critic_obs [N, critic_width] rows at stride
+ * critic_obs_ld (the envs' stacks are strided column slices of their history windows); value may
+ * be NULL (values computed later in one batched critic pass).
  * hg_rollout_env: rewards_out = rewards + gamma * values * time_outs (time_outs may be NULL),
  * dones_out = reset; values == NULL defers the time-out bootstrap (rewards_out = rewards) and
  * time_outs_out (optional) keeps the time-out flags for it. */
 int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
                    const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
-                   int64_t critic_obs_width, float* actions_out, float* logp_out, float* mu_out,
-                   float* sigma_out, float* value_out, void* obs_out, void* critic_obs_out, int obs_fp16,
-                   int row_offset, uint64_t seed, uint64_t counter, void* stream);
+                   int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
+                   float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
+                   void* obs_out, void* critic_obs_out, int obs_fp16, int row_offset, uint64_t seed,
+                   uint64_t counter, void* stream);
 int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
                    int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
                    void* stream);
@@ -293,6 +305,15 @@ typedef struct hg_gather_table {
 } hg_gather_table;
 int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_rows, const hg_gather_table* tabs, int ntab,
                       void* stream);
+/* Minibatch rows of a frame-only observation storage (replaces observations[batch_idx] when the
+ * rollout keeps one frame per env-step, rollout_storage.py:153-191 with the stacking of
+ * humanoid_env.py:880-887): dst[i] = the F*W stack of storage row s = idx[i] (t = s / N,
+ * e = s % N) rebuilt from frames [T, N, W] (the newest frame of each slot's stack), init
+ * [N, F*W] (slot 0's whole stack) and dones [T, N] (u8: a reset at post step r zeroes the frames
+ * older than slot r + 1's newest).  src_dtype F32 or F16 (frames and init), dst_dtype equal,
+ * BF16, or F32 from F16.  1 <= F <= 64.  One launch, one wave per row. */
+int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* frames, const void* init, const uint8_t* dones,
+                      int T, int N, int F, int W, int src_dtype, void* dst, int dst_dtype, void* stream);
 
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----

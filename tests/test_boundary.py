@@ -41,7 +41,8 @@ def test_library_loads_without_gpu():
     assert L.hg_arena_bytes(ctypes.byref(cfg)) == 0          # num_envs = 0 -> invalid
     cfg.num_envs, cfg.frame_stack, cfg.c_frame_stack = 4096, 15, 3
     nbytes = L.hg_arena_bytes(ctypes.byref(cfg))
-    assert 4096 * (705 + 219) * 4 * 2 < nbytes < 64 << 20    # SoA state + double-buffered obs
+    # SoA state + the observation history windows (14 + 26 frames of 47, 2 + 26 frames of 73 per env)
+    assert 4096 * (40 * 47 + 28 * 73) * 4 < nbytes < 128 << 20
     out = ctypes.c_void_p()
     rc = L.hg_create(ctypes.byref(cfg), None, None, 0, ctypes.byref(out))
     assert rc != 0 and b"null" in L.hg_last_error(None)

@@ -161,7 +161,6 @@ def _post_once(env, counter):
     N = _hg()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     N.check(N.lib().hg_post(env.sim, ctypes.c_uint64(counter), s), env.sim)
-    env._parity ^= 1
     torch.cuda.synchronize()
 
 
@@ -1424,3 +1423,69 @@ def test_sim2sim_mjcf_profile(tmp_path):
         assert np.isfinite(c["lin_vel_error"]) and np.isfinite(c["yaw_rate_error"])
     tr = np.load(out / "sim2sim_traces.npz")
     assert tr["q"].shape == (100, 12) and np.isfinite(tr["q"]).all() and np.isfinite(tr["target_q"]).all()
+
+
+def test_obs_window_stacking_over_wraps():
+    """The observation history windows (HG_T_OBS_BUF / HG_T_PRIV_BUF, hg_obs_head): over 60 steps
+    (two wraps of the window) every new stack is the previous one shifted by a frame, zeroed for
+    the envs the step reset — obs_{t+1}[:, :(F-1)W] == reset ? 0 : obs_t[:, W:] — bit for bit, for
+    both tables (the deque stacking of humanoid_env.py:880-887), with resets forced."""
+    _need_gpu()
+    env = _make_env(N_ENVS)
+    W, Wp = 47, 73
+    prev_o, prev_p = env.obs_buf.clone(), env.privileged_obs_buf.clone()
+    heads = set()
+    for k in range(60):
+        if k % 6 == 2:
+            env.episode_length_buf[k % N_ENVS:k % N_ENVS + 3] = 2400  # time-out resets next step
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+        heads.add(int(env.hg.hg_obs_head(env.sim)))
+        o, p = env.obs_buf, env.privileged_obs_buf
+        rs = env.reset_buf.view(-1, 1)
+        assert torch.equal(o[:, :-W], torch.where(rs, torch.zeros_like(prev_o[:, W:]), prev_o[:, W:])), k
+        assert torch.equal(p[:, :-Wp], torch.where(rs, torch.zeros_like(prev_p[:, Wp:]), prev_p[:, Wp:])), k
+        assert o.shape == (N_ENVS, 705) and p.shape == (N_ENVS, 219)
+        prev_o, prev_p = o.clone(), p.clone()
+    assert 0 in heads and len(heads) == int(env.hg.hg_obs_window_advance(env.sim))  # wrapped
+
+
+@pytest.mark.parametrize("obs_dtype", [torch.float32, torch.float16])
+def test_frame_only_storage_rebuilds_stacks(obs_dtype):
+    """Frame-only rollout storage (RolloutStorage obs_frames, hg_rollout_act writing the newest
+    frame, hg_gather_stacked): over a 30-step rollout of the env through PPO's fused path, with
+    resets forced and a window wrap inside, the rebuilt [T, N, 705] observations equal the stacks
+    the policy was given, bit for bit (in the storage dtype), and so do minibatch rows gathered
+    in the storage dtype and as bfloat16."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    torch.manual_seed(3)
+    n, T = 256, 30
+    env = _make_env(n)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128]).cuda()
+    ppo = PPO(ac, device="cuda:0")
+    ppo.init_storage(n, T, [705], [219], [12], obs_dtype=obs_dtype, obs_frames=(15, 47))
+    st = ppo.storage
+    assert st.obs_frames is not None and st.obs_frames.shape == (T, n, 47)
+    obs, cobs = env.obs_buf, env.privileged_obs_buf
+    rec, rec_c = [], []
+    with torch.inference_mode():
+        for t in range(T):
+            if t % 5 == 2:
+                env.episode_length_buf[7 * t % n:7 * t % n + 4] = 2400
+            rec.append(obs.clone())
+            rec_c.append(cobs.clone())
+            a = ppo.act(obs, cobs)
+            assert ppo.transition.fused_slot == t
+            obs, cobs, r, d, info = env.step(a)
+            ppo.process_env_step(r, d, info)
+    torch.cuda.synchronize()
+    want = torch.stack(rec).to(obs_dtype)
+    assert bool(st.dones.any())
+    assert torch.equal(st.observations, want)
+    assert torch.equal(st.privileged_observations, torch.stack(rec_c).to(obs_dtype))
+    idx = torch.randperm(T * n, device="cuda:0")[:1000].contiguous()
+    flat = want.flatten(0, 1)
+    for dt in (obs_dtype, torch.bfloat16):
+        dst = torch.empty(1000, 705, dtype=dt, device="cuda:0")
+        st.gather_stacked(idx, dst)
+        assert torch.equal(dst, flat[idx].to(dt)), dt
