@@ -331,11 +331,18 @@ extern "C" int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_r
 // ---------------------------------------------------------------------------------------------
 namespace {
 
+// up to two plain tables gathered by the same waves (the critic observations and the packed
+// per-sample table of the minibatch): one launch and one index load per row for all of them
+struct PlainTabs {
+  GatherTab t[2];
+  int ntab;
+};
+
 template <typename S, typename D>
 __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restrict__ idx, int64_t rows,
                                                         const S* __restrict__ frames, const S* __restrict__ init,
                                                         const uint8_t* __restrict__ dones, int T, int N, int F, int W,
-                                                        D* __restrict__ dst) {
+                                                        D* __restrict__ dst, PlainTabs P) {
   const int64_t i = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= rows) return;
@@ -347,25 +354,47 @@ __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restric
   const bool rs = lane < F - 1 && back >= 0 && dones[(int64_t)back * N + e] != 0;
   const uint64_t m = __ballot(rs);
   const int jz = m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0;  // positions j < jz are zero
-  const int64_t row = (int64_t)F * W;
-  D* __restrict__ out = dst + i * row;
-  constexpr int G = 8;  // frames per batch of loads in flight
-  for (int j0 = 0; j0 < F; j0 += G) {
-    for (int c = lane; c < W; c += 64) {
-      float v[G];
+  const int row = F * W;
+  D* __restrict__ out = dst + i * (int64_t)row;
+  const S* __restrict__ init_e = init + (int64_t)e * row;
+  // lanes along the whole F*W row (every store instruction 64 consecutive elements); element c of
+  // the row is frame j = c / W, column w = c % W, tracked incrementally (one division per chunk);
+  // KB loads in flight per lane before the stores
+  constexpr int KB = 16;
+  for (int base = 0; base < row; base += 64 * KB) {
+    int c = base + lane;
+    int j = c / W, w = c - j * W;
+    float v[KB];
 #pragma unroll
-      for (int g = 0; g < G; g++) {
-        const int j = j0 + g;
-        v[g] = 0.f;
-        if (j < F && j >= jz) {
-          const int tau = t - (F - 1 - j);
-          v[g] = tau >= 0 ? (float)frames[((int64_t)tau * N + e) * W + c] : (float)init[(int64_t)e * row + (int64_t)(j + t) * W + c];
-        }
+    for (int k = 0; k < KB; k++) {
+      v[k] = 0.f;
+      if (c < row && j >= jz) {
+        const int tau = t - (F - 1 - j);
+        v[k] = tau >= 0 ? (float)frames[((int64_t)tau * N + e) * W + w] : (float)init_e[(int64_t)(j + t) * W + w];
       }
-#pragma unroll
-      for (int g = 0; g < G; g++)
-        if (j0 + g < F) out[(int64_t)(j0 + g) * W + c] = (D)v[g];
+      c += 64;
+      w += 64;
+      while (w >= W) {
+        w -= W;
+        j++;
+      }
     }
+#pragma unroll
+    for (int k = 0; k < KB; k++) {
+      const int cc = base + lane + 64 * k;
+      if (cc < row) out[cc] = (D)v[k];
+    }
+  }
+  for (int q = 0; q < P.ntab; q++) {
+    const GatherTab& G = P.t[q];
+    if (G.cvt == 1)
+      gather_row_bf16<_Float16>((const _Float16*)G.src + s * G.width, (__bf16*)G.dst + i * G.width, G.width, lane);
+    else if (G.cvt == 2)
+      gather_row_bf16<float>((const float*)G.src + s * G.width, (__bf16*)G.dst + i * G.width, G.width, lane);
+    else if (G.es == 4)
+      gather_row<uint32_t>((const uint32_t*)G.src + s * G.width, (uint32_t*)G.dst + i * G.width, G.width, lane);
+    else
+      gather_row<uint16_t>((const uint16_t*)G.src + s * G.width, (uint16_t*)G.dst + i * G.width, G.width, lane);
   }
 }
 
@@ -373,16 +402,32 @@ __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restric
 
 extern "C" int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* frames, const void* init,
                                  const uint8_t* dones, int T, int N, int F, int W, int src_dtype, void* dst,
-                                 int dst_dtype, void* stream) {
-  if (!idx || rows <= 0 || !frames || !init || !dones || !dst || T <= 0 || N <= 0 || F <= 0 || F > 64 || W <= 0)
+                                 int dst_dtype, const hg_gather_table* tabs, int ntab, void* stream) {
+  if (!idx || rows <= 0 || !frames || !init || !dones || !dst || T <= 0 || N <= 0 || F <= 0 || F > 64 || W <= 0 ||
+      (int64_t)F * W > 0x7fffffff || ntab < 0 || ntab > 2 || (ntab > 0 && !tabs))
     return HG_ERR_ARG;
+  PlainTabs P;
+  P.ntab = 0;
+  for (int t = 0; t < ntab; t++) {  // the plain rows of the same storage rows (T*N of them)
+    const hg_gather_table& g = tabs[t];
+    if (!g.src || !g.dst || g.width <= 0) return HG_ERR_ARG;
+    const auto bytes = [](int ty) { return ty == HG_DTYPE_F32 ? 4 : (ty == HG_DTYPE_F16 || ty == HG_DTYPE_BF16) ? 2 : 0; };
+    const int sb = bytes(g.src_dtype), db = bytes(g.dst_dtype);
+    if (!sb || !db) return HG_ERR_ARG;
+    int cvt = 0;
+    if (g.src_dtype != g.dst_dtype) {
+      if (g.dst_dtype != HG_DTYPE_BF16) return HG_ERR_ARG;
+      cvt = g.src_dtype == HG_DTYPE_F16 ? 1 : 2;
+    }
+    P.t[P.ntab++] = GatherTab{g.src, g.dst, g.width, sb, cvt};
+  }
   const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
   if (blocks > 0x7fffffff) return HG_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const dim3 g((unsigned)blocks), b(TPB);
 #define HG_GS(ST, DT) \
   hipLaunchKernelGGL((k_gather_stacked<ST, DT>), g, b, 0, s, idx, rows, (const ST*)frames, (const ST*)init, dones, T, N, F, \
-                     W, (DT*)dst)
+                     W, (DT*)dst, P)
   if (src_dtype == HG_DTYPE_F32 && dst_dtype == HG_DTYPE_F32) HG_GS(float, float);
   else if (src_dtype == HG_DTYPE_F32 && dst_dtype == HG_DTYPE_BF16) HG_GS(float, __bf16);
   else if (src_dtype == HG_DTYPE_F16 && dst_dtype == HG_DTYPE_F16) HG_GS(_Float16, _Float16);

@@ -174,7 +174,8 @@ def load_library(path=LIB_PATH):
                                  ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
     L.hg_gather_stacked.restype = ctypes.c_int
     L.hg_gather_stacked.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                    ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp]
+                                    ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(GatherTable),
+                                    ctypes.c_int, vp]
     L.hg_ep_stats_slot.restype = ctypes.c_int
     L.hg_ep_stats_slot.argtypes = [vp]
     L.hg_obs_head.restype = ctypes.c_int

@@ -11,6 +11,7 @@ run as one pass that reads the incoming gradient and the layer's ELU output once
 pre-activation) is kept for the backward: elu'(h) = y + 1 for h <= 0.  Parameters stay in the
 nn.Sequential (state_dict keys unchanged).  Device float32 only.
 """
+import contextlib
 import ctypes
 import os
 
@@ -302,26 +303,66 @@ def x6_images(jobs, dev):
     return imgs
 
 
-def _forward_images(params, n, rows, dev, dx):
-    """{layer: image} of W for the routed bf16-split forward GEMMs of an n-layer MLP call on ``rows``
-    rows and, when ``dx``, of W^T for its routed bf16-split input-grad GEMMs — built in one launch."""
-    fwd, dxi = {}, {}
+def _image_specs(params, n, rows, dx):
+    """The operand images an n-layer MLP call on ``rows`` rows uses: (kind, layer, W, trans, R, K)
+    for its routed bf16-split forward GEMMs (kind "f": W itself) and, when ``dx``, input-grad GEMMs
+    (kind "d": W^T)."""
+    out = []
     if not (X6_IMAGE and GEMM):
-        return fwd, dxi
-    jobs, keys = [], []
+        return out
     for i in range(n):
         W = params[2 * i]
         if not W.is_contiguous():
             continue
         nn_, kk = W.shape
         if i < n - 1 and _route(_GEMM_FWD, rows, kk, nn_) >= X6_TILE0:
-            jobs.append((W, 0, nn_, kk))
-            keys.append((fwd, i))
+            out.append(("f", i, W, 0, nn_, kk))
         if dx and i > 0 and _route(_GEMM_DX, rows, nn_, kk) >= X6_TILE0:
-            jobs.append((W, 1, kk, nn_))
-            keys.append((dxi, i))
-    for (d, i), im in zip(keys, x6_images(jobs, dev)):
-        d[i] = im
+            out.append(("d", i, W, 1, kk, nn_))
+    return out
+
+
+_SCOPE = None  # {(weight address, trans): image} while an image_scope is active
+
+
+@contextlib.contextmanager
+def image_scope(specs, dev):
+    """The weight images of several fusable MLPs (``specs``: [(net, rows)]) built in ONE launch
+    for the MLP calls inside the block — one image launch per PPO minibatch instead of one per
+    network.  The weights must not change inside the block."""
+    global _SCOPE
+    jobs, keys = [], []
+    for net, rows in specs:
+        if not fusable(net):
+            continue
+        params = _params(net)
+        for _, _, W, trans, R, K in _image_specs(params, len(params) // 2, rows, True):
+            key = (W.data_ptr(), trans)
+            if key not in keys:
+                keys.append(key)
+                jobs.append((W, trans, R, K))
+    prev = _SCOPE
+    _SCOPE = dict(zip(keys, x6_images(jobs, dev)))
+    try:
+        yield
+    finally:
+        _SCOPE = prev
+
+
+def _forward_images(params, n, rows, dev, dx):
+    """{layer: image} of W for the routed bf16-split forward GEMMs of an n-layer MLP call on ``rows``
+    rows and, when ``dx``, of W^T for its routed bf16-split input-grad GEMMs — taken from the active
+    image_scope or built in one launch."""
+    fwd, dxi = {}, {}
+    specs = _image_specs(params, n, rows, dx)
+    if not specs:
+        return fwd, dxi
+    if _SCOPE is not None and all((W.data_ptr(), trans) in _SCOPE for _, _, W, trans, _, _ in specs):
+        imgs = [_SCOPE[(W.data_ptr(), trans)] for _, _, W, trans, _, _ in specs]
+    else:
+        imgs = x6_images([(W, trans, R, K) for _, _, W, trans, R, K in specs], dev)
+    for (kind, i, _, _, _, _), im in zip(specs, imgs):
+        (fwd if kind == "f" else dxi)[i] = im
     return fwd, dxi
 
 

@@ -16,6 +16,7 @@ the fused Adam kernel as a tensor; the three loss means are accumulated on the d
 once per update.  The host therefore never waits for the GPU inside the minibatch loop.  On the
 CPU the reference's host-side arithmetic is kept verbatim (this is what the golden tests pin).
 """
+import contextlib
 import ctypes
 import os
 
@@ -392,10 +393,14 @@ class PPO:
         outputs in one fused HIP forward launch pair and one backward launch (hg_loss.py).
         Returns (loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean]."""
         ac = self.actor_critic
-        mu = ac._mlp(ac.actor, obs_b)
-        ac.distribution = _DiagGaussian(mu, ac.std.expand_as(mu))
-        est_lin_vel = ac.base_get_lin_vel(obs_b)
-        value_b = ac.evaluate(critic_b)
+        scope = (hg_mlp.image_scope([(ac.actor, obs_b.shape[0]), (ac.base_lin_vel, obs_b.shape[0]),
+                                     (ac.critic, critic_b.shape[0])], obs_b.device)
+                 if ac.policy_dtype == "fp32" and ac.fused_mlp and obs_b.is_cuda else contextlib.nullcontext())
+        with scope:  # the three networks' weight images in one launch
+            mu = ac._mlp(ac.actor, obs_b)
+            ac.distribution = _DiagGaussian(mu, ac.std.expand_as(mu))
+            est_lin_vel = ac.base_get_lin_vel(obs_b)
+            value_b = ac.evaluate(critic_b)
         data = {"actions": actions_b, "old_logp": old_logp_b, "advantages": adv_b, "target_values": target_values_b,
                 "returns": returns_b, "old_mu": old_mu_b, "old_sigma": old_sigma_b,
                 "lin_vel_target": lin_vel_b if lin_vel_b.dtype == torch.float32 else lin_vel_b.float()}
@@ -589,9 +594,11 @@ class PPO:
         """Captured minibatch body: gather rows -> losses -> backward (+ KL mean, loss sums)."""
         if self._flat_grad is not None:
             self._flat_grad.zero_()
-        gather_rows(idx, self._mb_tables)
         if self.storage.obs_frames is not None:
-            self.storage.gather_stacked(idx, self._mb_obs)
+            # frame-only storage: the stacked obs rows and the plain tables in one launch
+            self.storage.gather_stacked(idx, self._mb_obs, self._mb_tables)
+        else:
+            gather_rows(idx, self._mb_tables)
         crit_b = self._mb_critic
         b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
         pk = self._mb_packed

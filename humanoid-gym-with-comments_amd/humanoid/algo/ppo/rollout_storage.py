@@ -105,20 +105,29 @@ class RolloutStorage:
         """Address identifying the actor observation buffers (captured-graph keys)."""
         return (self.obs_frames if self.obs_frames is not None else self._observations).data_ptr()
 
-    def gather_stacked(self, idx, dst):
+    def gather_stacked(self, idx, dst, tables=()):
         """dst[i] = the stacked actor observation of storage row idx[i] (frame-only storage), one
         hg_gather_stacked launch on the current stream; dst [rows, F*W] of the storage dtype, or
-        bfloat16."""
+        bfloat16.  ``tables``: up to two more (src [T*N, w], dst [rows, w]) pairs gathered for the
+        same rows in the same launch (as gather_rows)."""
         from humanoid import _native as N
         T, Nn, F, W = self.num_transitions_per_env, self.num_envs, self.frame_stack, self.frame_width
         if (idx.dtype != torch.int64 or not idx.is_contiguous() or not dst.is_contiguous()
                 or dst.shape != (idx.numel(), F * W)):
             raise RuntimeError("gather_stacked: idx contiguous int64, dst contiguous [rows, F*W]")
         codes = N.DTYPE_CODES
+        if len(tables) > 2:
+            raise ValueError("gather_stacked takes at most two plain tables")
+        tabs = (N.GatherTable * 2)()
+        for k, (src, d) in enumerate(tables):
+            _check_table(src, d, idx.numel(), T * Nn)
+            tabs[k] = N.GatherTable(src.data_ptr(), d.data_ptr(), src.shape[1], codes[str(src.dtype)[6:]],
+                                    codes[str(d.dtype)[6:]])
         s = ctypes.c_void_p(torch.cuda.current_stream(idx.device).cuda_stream)
         p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
         rc = N.lib().hg_gather_stacked(p(idx), idx.numel(), p(self.obs_frames), p(self.obs_init), p(self.dones), T, Nn,
-                                       F, W, codes[str(self.obs_dtype)[6:]], p(dst), codes[str(dst.dtype)[6:]], s)
+                                       F, W, codes[str(self.obs_dtype)[6:]], p(dst), codes[str(dst.dtype)[6:]], tabs,
+                                       len(tables), s)
         if rc != 0:
             raise RuntimeError(f"hg_gather_stacked failed ({rc})")
 
@@ -222,6 +231,16 @@ class RolloutStorage:
                        old_logp[idx], old_mu[idx], old_sigma[idx], (None, None), None)
 
 
+def _check_table(src, dst, rows, src_rows):
+    from humanoid import _native as N
+    conv = src.dtype == dst.dtype or (dst.dtype == torch.bfloat16 and src.dtype in (torch.float16, torch.float32))
+    if (src.dim() != 2 or not src.is_contiguous() or not dst.is_contiguous() or not conv
+            or dst.shape != (rows, src.shape[1]) or src.shape[0] != src_rows
+            or str(src.dtype)[6:] not in N.DTYPE_CODES or str(dst.dtype)[6:] not in N.DTYPE_CODES):
+        raise RuntimeError("gather_rows: src [R, W] and dst [rows, W] must be contiguous float32 / float16 / "
+                           "bfloat16, same dtype or a bfloat16 dst")
+
+
 def gather_rows(idx, tables):
     """dst[i] = src[idx[i]] for up to three (src, dst) pairs of row-major [rows, width] device
     tensors (float32 / float16 / bfloat16), in one launch of the HIP gather kernel
@@ -236,12 +255,7 @@ def gather_rows(idx, tables):
     rows, src_rows = idx.numel(), tables[0][0].shape[0]
     tabs = (N.GatherTable * 3)()
     for t, (src, dst) in enumerate(tables):
-        conv = src.dtype == dst.dtype or (dst.dtype == torch.bfloat16 and src.dtype in (torch.float16, torch.float32))
-        if (src.dim() != 2 or not src.is_contiguous() or not dst.is_contiguous() or not conv
-                or dst.shape != (rows, src.shape[1]) or src.shape[0] != src_rows
-                or str(src.dtype)[6:] not in N.DTYPE_CODES or str(dst.dtype)[6:] not in N.DTYPE_CODES):
-            raise RuntimeError("gather_rows: src [R, W] and dst [rows, W] must be contiguous float32 / float16 / "
-                               "bfloat16, same dtype or a bfloat16 dst")
+        _check_table(src, dst, rows, src_rows)
         tabs[t] = N.GatherTable(src.data_ptr(), dst.data_ptr(), src.shape[1], N.DTYPE_CODES[str(src.dtype)[6:]],
                                 N.DTYPE_CODES[str(dst.dtype)[6:]])
     s = ctypes.c_void_p(torch.cuda.current_stream(idx.device).cuda_stream)

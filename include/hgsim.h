@@ -311,9 +311,12 @@ int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_rows, const 
  * e = s % N) rebuilt from frames [T, N, W] (the newest frame of each slot's stack), init
  * [N, F*W] (slot 0's whole stack) and dones [T, N] (u8: a reset at post step r zeroes the frames
  * older than slot r + 1's newest).  src_dtype F32 or F16 (frames and init), dst_dtype equal,
- * BF16, or F32 from F16.  1 <= F <= 64.  One launch, one wave per row. */
+ * BF16, or F32 from F16.  1 <= F <= 64.  Up to two plain [T*N, width] tables (tabs, ntab <= 2, as
+ * hg_gather_rows_ex) are gathered for the same rows by the same waves.  One launch, one wave per
+ * row. */
 int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* frames, const void* init, const uint8_t* dones,
-                      int T, int N, int F, int W, int src_dtype, void* dst, int dst_dtype, void* stream);
+                      int T, int N, int F, int W, int src_dtype, void* dst, int dst_dtype,
+                      const hg_gather_table* tabs, int ntab, void* stream);
 
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----

@@ -18,7 +18,7 @@ def cls(n):
     if n.startswith("Cijk") or "gemm" in n.lower():
         return "gemm"
     for k in ("k_step", "elu_kernel", "k_act_bwd", "k_colsum", "index_elementwise", "reduce_kernel", "k_post",
-              "k_stack", "k_skinny", "k_adam", "k_sqnorm", "k_ppo_loss", "k_kl", "copyBuffer", "FillFunctor",
+              "k_stack", "k_window", "k_skinny", "k_adam", "k_sqnorm", "k_ppo_loss", "k_kl", "copyBuffer", "FillFunctor",
               "gather", "k_act", "k_env", "k_gae", "k_lr"):
         if k in n:
             return k

@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-OURS = ("k_step", "k_gemm", "k_post", "k_post_step", "k_stack", "k_stack_stats", "k_ep_stats", "k_gae_scan", "k_gae_norm", "k_heights",
+OURS = ("k_step", "k_gemm", "k_post", "k_post_step", "k_stack", "k_stack_stats", "k_window_stats", "k_gather_stacked", "k_gather_rows", "k_x6_image_jobs", "k_ep_stats", "k_gae_scan", "k_gae_norm", "k_heights",
         "k_act", "k_env", "k_sqnorm", "k_adam", "k_ppo_loss_rows", "k_ppo_loss_final", "k_ppo_loss_bwd",
         "k_act_bwd_vec", "k_act_bwd_small", "k_colsum_final", "k_skinny_fwd", "k_skinny_dx", "k_skinny_dw")
 

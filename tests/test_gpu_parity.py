@@ -1485,7 +1485,14 @@ def test_frame_only_storage_rebuilds_stacks(obs_dtype):
     assert torch.equal(st.privileged_observations, torch.stack(rec_c).to(obs_dtype))
     idx = torch.randperm(T * n, device="cuda:0")[:1000].contiguous()
     flat = want.flatten(0, 1)
+    crit = st.privileged_observations.flatten(0, 1)
+    extra = torch.randn(T * n, 43, device="cuda:0")
     for dt in (obs_dtype, torch.bfloat16):
         dst = torch.empty(1000, 705, dtype=dt, device="cuda:0")
         st.gather_stacked(idx, dst)
         assert torch.equal(dst, flat[idx].to(dt)), dt
+        # with the plain tables of the minibatch gathered by the same launch
+        dst.zero_()
+        dc, de = torch.empty(1000, 219, dtype=dt, device="cuda:0"), torch.empty(1000, 43, device="cuda:0")
+        st.gather_stacked(idx, dst, [(crit, dc), (extra, de)])
+        assert torch.equal(dst, flat[idx].to(dt)) and torch.equal(dc, crit[idx].to(dt)) and torch.equal(de, extra[idx])
