@@ -25,9 +25,13 @@ ITERS = int(os.environ.get("ITERS", 30))
 TILES = [int(t) for t in os.environ.get("TILES", "19,20,21,22,23,24,25,26").split(",")]
 FWD = [("actor0_mb", 24576, 705, 512), ("actor1_mb", 24576, 512, 256), ("linvel0_mb", 24576, 705, 128),
        ("critic0_mb", 24576, 219, 768), ("critic1_mb", 24576, 768, 256), ("actor2_mb", 24576, 256, 128),
-       ("actor0_roll", 4096, 705, 512), ("critic0_vals", 98304, 219, 768), ("critic1_vals", 98304, 768, 256)]
+       ("actor0_roll", 4096, 705, 512), ("actor1_roll", 4096, 512, 256), ("actor2_roll", 4096, 256, 128),
+       ("critic0_vals", 98304, 219, 768), ("critic1_vals", 98304, 768, 256), ("critic2_vals", 98304, 256, 128)]
+
 DX = [("actor_dx1", 24576, 256, 512), ("actor_dx2", 24576, 128, 256), ("critic_dx1", 24576, 256, 768),
       ("critic_dx2", 24576, 128, 256), ("linvel_dx1", 24576, 128, 128)]
+FWD = [f for f in FWD if not os.environ.get("SHAPES") or f[0] in os.environ["SHAPES"].split(",")]
+DX = [f for f in DX if not os.environ.get("SHAPES") or f[0] in os.environ["SHAPES"].split(",")]
 
 
 def stream():
@@ -95,6 +99,10 @@ for tag, rows, k, n in FWD:
                "img_us": round(timeit(imaged), 2), "img2_us": round(timeit(imaged2), 2),
                "image_build_us": round(timeit(lambda: image(W, 0, n, k, img)), 2),
                "a_image_build_us": round(timeit(lambda: image(x, 0, rows, k, aimg)), 2)}
+        if tile == TILES[0]:  # the f32-MFMA 64x64 tile (the small-row route) for reference
+            rec["tile5_us"] = round(timeit(lambda: ck(L.hg_gemm_f32(
+                0, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0, y0.data_ptr(),
+                y0.stride(0), None, rows, n, k, 1, 5, stream()), "t5")), 2)
         print(json.dumps(rec), flush=True)
 
 for tag, rows, kr, n in DX:
@@ -139,7 +147,7 @@ DW = [("actor_dw0", 24576, 512, 705), ("actor_dw1", 24576, 256, 512), ("actor_dw
       ("critic_dw0", 24576, 768, 219), ("critic_dw1", 24576, 256, 768), ("linvel_dw0", 24576, 128, 705),
       ("linvel_dw1", 24576, 128, 128)]
 DW_TILES = [int(t) for t in os.environ.get("DW_TILES", "19,20,21,22,23,25").split(",")]
-for tag, rows, n, k in DW:
+for tag, rows, n, k in ([] if os.environ.get("SKIP_DW") else DW):
     gh = torch.randn(rows, n, device=dev)
     x = torch.randn(rows, k, device=dev)
     ref = gh.double().t() @ x.double()
