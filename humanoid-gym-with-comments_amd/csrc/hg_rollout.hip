@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hg_common.h"
 
@@ -45,7 +46,7 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
                                             int64_t cobs_w, int64_t obs_ld, int64_t obs_c0, int64_t cobs_ld,
                                             float* __restrict__ act_out, float* __restrict__ logp_out,
                                             float* __restrict__ mu_out, float* __restrict__ sigma_out,
-                                            float* __restrict__ value_out, OT* __restrict__ obs_out,
+                                            float* __restrict__ value_out, int64_t obs_out_ld, OT* __restrict__ obs_out,
                                             OT* __restrict__ cobs_out, int row_offset, uint64_t seed,
                                             uint64_t counter, int env_blocks) {
   if ((int)blockIdx.x < env_blocks) {
@@ -106,7 +107,7 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
     const int64_t r = o ? q : q - n;
     const int64_t w = o ? obs_w : cobs_w;
     const float* __restrict__ src = o ? obs + r * obs_ld + obs_c0 : cobs + r * cobs_ld;
-    OT* __restrict__ dst = (o ? obs_out : cobs_out) + r * w;
+    OT* __restrict__ dst = o ? obs_out + r * obs_out_ld : cobs_out + r * w;
     int64_t c = lane;
     for (; c + 192 < w; c += 256) {
       const float a = src[c], b = src[c + 64], d = src[c + 128], e = src[c + 192];
@@ -138,10 +139,11 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
                               const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
                               int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
                               float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
-                              void* obs_out, void* critic_obs_out, int obs_fp16, int row_offset, uint64_t seed,
-                              uint64_t counter, void* stream) {
+                              void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
+                              uint64_t seed, uint64_t counter, void* stream) {
   if (!mean || !std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out ||
       !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 || obs_col0 < 0 ||
+      (obs_out_ld != 0 && obs_out_ld < obs_width) ||
       obs_ld < obs_col0 + obs_width || (critic_obs_width > 0 && (!critic_obs || !critic_obs_out ||
                                                                  critic_obs_ld < critic_obs_width)))
     return HG_ERR_ARG;
@@ -150,16 +152,17 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
   const int64_t copy_rows = critic_obs_width > 0 ? 2 * (int64_t)num_envs : num_envs;
   const int copy_blocks = (int)std::min<int64_t>((copy_rows + TPB / 64 - 1) / (TPB / 64), 2048);
   const int64_t cw = critic_obs_width > 0 ? critic_obs_width : 0;
+  const int64_t old = obs_out_ld ? obs_out_ld : obs_width;
   hipStream_t s = (hipStream_t)stream;
   if (obs_fp16)
     hipLaunchKernelGGL(k_act<__half>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
                        critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, critic_obs_ld,
-                       actions_out, logp_out, mu_out, sigma_out, value_out, (__half*)obs_out,
+                       actions_out, logp_out, mu_out, sigma_out, value_out, old, (__half*)obs_out,
                        (__half*)critic_obs_out, row_offset, seed, counter, env_blocks);
   else
     hipLaunchKernelGGL(k_act<float>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
                        critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, critic_obs_ld,
-                       actions_out, logp_out, mu_out, sigma_out, value_out, (float*)obs_out, (float*)critic_obs_out,
+                       actions_out, logp_out, mu_out, sigma_out, value_out, old, (float*)obs_out, (float*)critic_obs_out,
                        row_offset, seed, counter, env_blocks);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
@@ -322,7 +325,7 @@ extern "C" int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_r
 // ---------------------------------------------------------------------------------------------
 // Minibatch rows of a frame-only observation storage (RolloutStorage with obs_frames): slot t of
 // the rollout keeps only the newest W-element frame of the stacked observation the policy saw,
-// slot 0 also the whole stack (init).  The stack of storage row s = t N + e is rebuilt as the
+// env-major ([N, T, W]: a row's frames are one contiguous run), slot 0 also the whole stack (init).  The stack of storage row s = t N + e is rebuilt as the
 // reference's deque would have held it (humanoid_env.py:880-887): position j < F holds the
 // newest frame of slot tau = t - (F - 1 - j) (tau < 0: position j + t of init), zero when the env
 // was reset by a post step r with tau <= r <= t - 1 (dones[r][e]; the reset zeroes the history
@@ -336,13 +339,17 @@ namespace {
 struct PlainTabs {
   GatherTab t[2];
   int ntab;
+  int early;  // every table 4-byte, no conversion, <= 256 wide: its loads are issued with the frames'
 };
+constexpr int PK = 4;  // plain-table elements per lane on the early path (256 / 64): one 16-byte access
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-byte-aligned 16-byte accesses
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
 
-template <typename S, typename D>
+template <typename S, typename D, bool EARLY>
 __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restrict__ idx, int64_t rows,
                                                         const S* __restrict__ frames, const S* __restrict__ init,
-                                                        const uint8_t* __restrict__ dones, int T, int N, int F, int W,
-                                                        D* __restrict__ dst, PlainTabs P) {
+                                                        const uint8_t* __restrict__ dones, int64_t dts, int64_t des,
+                                                        int T, int N, int F, int W, D* __restrict__ dst, PlainTabs P) {
   const int64_t i = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= rows) return;
@@ -350,42 +357,104 @@ __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restric
   int64_t s = idx[i];
   s = s < 0 ? 0 : (s >= total ? total - 1 : s);  // never read out of bounds
   const int t = (int)(s / N), e = (int)(s - (int64_t)t * N);
-  const int back = t - 1 - lane;
-  const bool rs = lane < F - 1 && back >= 0 && dones[(int64_t)back * N + e] != 0;
-  const uint64_t m = __ballot(rs);
-  const int jz = m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0;  // positions j < jz are zero
-  const int row = F * W;
-  D* __restrict__ out = dst + i * (int64_t)row;
-  const S* __restrict__ init_e = init + (int64_t)e * row;
-  // lanes along the whole F*W row (every store instruction 64 consecutive elements); element c of
-  // the row is frame j = c / W, column w = c % W, tracked incrementally (one division per chunk);
-  // KB loads in flight per lane before the stores
-  constexpr int KB = 16;
-  for (int base = 0; base < row; base += 64 * KB) {
-    int c = base + lane;
-    int j = c / W, w = c - j * W;
-    float v[KB];
+  // the plain tables' row loads first (they depend on s only): in flight with the reset scan
+  // and the frame loads, stored at the end; lane l holds elements 4l .. 4l + 3
+  u32x4u pv[2];
+  if (EARLY) {
 #pragma unroll
-    for (int k = 0; k < KB; k++) {
-      v[k] = 0.f;
-      if (c < row && j >= jz) {
-        const int tau = t - (F - 1 - j);
-        v[k] = tau >= 0 ? (float)frames[((int64_t)tau * N + e) * W + w] : (float)init_e[(int64_t)(j + t) * W + w];
-      }
-      c += 64;
-      w += 64;
-      while (w >= W) {
-        w -= W;
-        j++;
-      }
-    }
+    for (int q = 0; q < 2; q++) {
+      if (q >= P.ntab) break;
+      const uint32_t* __restrict__ src = (const uint32_t*)P.t[q].src + s * P.t[q].width;
+      const int w = (int)P.t[q].width, c = 4 * lane;
+      if (c + 3 < w) {
+        pv[q] = *reinterpret_cast<const u32x4u*>(src + c);
+      } else {
 #pragma unroll
-    for (int k = 0; k < KB; k++) {
-      const int cc = base + lane + 64 * k;
-      if (cc < row) out[cc] = (D)v[k];
+        for (int k = 0; k < 4; k++) pv[q][k] = c + k < w ? src[c + k] : 0u;
+      }
     }
   }
-  for (int q = 0; q < P.ntab; q++) {
+  const int back = t - 1 - lane;
+  const bool rs = lane < F - 1 && back >= 0 && dones[(int64_t)back * dts + (int64_t)e * des] != 0;
+  const uint64_t m = __ballot(rs);
+  const int jz = m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0;  // positions j < jz are zero
+  // element c of the row: zero below Z (the history a reset cleared), slot 0's stack below Bnd
+  // (positions before the rollout: init position j + t, i.e. init row + t W + c), then the
+  // env's frames tau = t - (F - 1) + j .. t — one contiguous run in the env-major frame table
+  const int row = F * W;
+  const int Z = jz * W;
+  const int Bnd = (t < F - 1 ? F - 1 - t : 0) * W;
+  const S* __restrict__ srcA = init + (int64_t)e * row + (int64_t)t * W;
+  const int64_t offB = ((int64_t)e * T + t - (F - 1)) * W;  // frames + offB + c, for c >= Bnd only
+  D* __restrict__ out = dst + i * (int64_t)row;
+  auto elem = [&](int c) -> float {
+    return c < Z ? 0.f : (c < Bnd ? (float)srcA[c] : (float)frames[offB + c]);
+  };
+  if constexpr (std::is_same<S, float>::value && std::is_same<D, float>::value) {
+    // 16-byte accesses: each lane moves groups of 4 consecutive elements (4-byte-aligned vector
+    // loads / stores), a group straddling Z or Bnd element by element
+    constexpr int KV = 3;  // 768 elements per pass: a 705-wide stack in one
+    for (int base = 0; base < row; base += 256 * KV) {
+      f32x4u v[KV];
+#pragma unroll
+      for (int k = 0; k < KV; k++) {
+        const int c = base + 4 * (lane + 64 * k);
+        if (c + 3 < row && (c >= Z || c + 3 < Z) && (c >= Bnd || c + 3 < Bnd)) {
+          if (c + 3 < Z) v[k] = (f32x4u){0.f, 0.f, 0.f, 0.f};
+          else if (c + 3 < Bnd) v[k] = *reinterpret_cast<const f32x4u*>(srcA + c);
+          else v[k] = *reinterpret_cast<const f32x4u*>(frames + offB + c);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++) v[k][q] = c + q < row ? elem(c + q) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KV; k++) {
+        const int c = base + 4 * (lane + 64 * k);
+        if (c + 3 < row) {
+          *reinterpret_cast<f32x4u*>(out + c) = v[k];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            if (c + q < row) out[c + q] = v[k][q];
+        }
+      }
+    }
+  } else {
+    constexpr int KB = 16;
+    for (int base = 0; base < row; base += 64 * KB) {
+      float v[KB];
+#pragma unroll
+      for (int k = 0; k < KB; k++) {
+        const int c = base + lane + 64 * k;
+        v[k] = c < row ? elem(c) : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < KB; k++) {
+        const int c = base + lane + 64 * k;
+        if (c < row) out[c] = (D)v[k];
+      }
+    }
+  }
+  if (EARLY) {
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      if (q >= P.ntab) break;
+      uint32_t* __restrict__ d = (uint32_t*)P.t[q].dst + i * P.t[q].width;
+      const int w = (int)P.t[q].width, c = 4 * lane;
+      if (c + 3 < w) {
+        *reinterpret_cast<u32x4u*>(d + c) = pv[q];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          if (c + k < w) d[c + k] = pv[q][k];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {  // constant indices: no dynamic indexing of the kernel argument
+    if (q >= P.ntab) break;
     const GatherTab& G = P.t[q];
     if (G.cvt == 1)
       gather_row_bf16<_Float16>((const _Float16*)G.src + s * G.width, (__bf16*)G.dst + i * G.width, G.width, lane);
@@ -401,8 +470,9 @@ __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restric
 }  // namespace
 
 extern "C" int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* frames, const void* init,
-                                 const uint8_t* dones, int T, int N, int F, int W, int src_dtype, void* dst,
-                                 int dst_dtype, const hg_gather_table* tabs, int ntab, void* stream) {
+                                 const uint8_t* dones, int64_t dones_ts, int64_t dones_es, int T, int N, int F, int W,
+                                 int src_dtype, void* dst, int dst_dtype, const hg_gather_table* tabs, int ntab,
+                                 void* stream) {
   if (!idx || rows <= 0 || !frames || !init || !dones || !dst || T <= 0 || N <= 0 || F <= 0 || F > 64 || W <= 0 ||
       (int64_t)F * W > 0x7fffffff || ntab < 0 || ntab > 2 || (ntab > 0 && !tabs))
     return HG_ERR_ARG;
@@ -421,13 +491,21 @@ extern "C" int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* f
     }
     P.t[P.ntab++] = GatherTab{g.src, g.dst, g.width, sb, cvt};
   }
+  P.early = 1;
+  for (int t = 0; t < P.ntab; t++) P.early &= (P.t[t].es == 4 && P.t[t].cvt == 0 && P.t[t].width <= 64 * PK);
   const int64_t blocks = (rows + TPB / 64 - 1) / (TPB / 64);
   if (blocks > 0x7fffffff) return HG_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const dim3 g((unsigned)blocks), b(TPB);
-#define HG_GS(ST, DT) \
-  hipLaunchKernelGGL((k_gather_stacked<ST, DT>), g, b, 0, s, idx, rows, (const ST*)frames, (const ST*)init, dones, T, N, F, \
-                     W, (DT*)dst, P)
+#define HG_GS(ST, DT)                                                                                          \
+  do {                                                                                                        \
+    if (P.early)                                                                                              \
+      hipLaunchKernelGGL((k_gather_stacked<ST, DT, true>), g, b, 0, s, idx, rows, (const ST*)frames,          \
+                         (const ST*)init, dones, dones_ts, dones_es, T, N, F, W, (DT*)dst, P);                \
+    else                                                                                                      \
+      hipLaunchKernelGGL((k_gather_stacked<ST, DT, false>), g, b, 0, s, idx, rows, (const ST*)frames,         \
+                         (const ST*)init, dones, dones_ts, dones_es, T, N, F, W, (DT*)dst, P);                \
+  } while (0)
   if (src_dtype == HG_DTYPE_F32 && dst_dtype == HG_DTYPE_F32) HG_GS(float, float);
   else if (src_dtype == HG_DTYPE_F32 && dst_dtype == HG_DTYPE_BF16) HG_GS(float, __bf16);
   else if (src_dtype == HG_DTYPE_F16 && dst_dtype == HG_DTYPE_F16) HG_GS(_Float16, _Float16);

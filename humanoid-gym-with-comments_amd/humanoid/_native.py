@@ -170,10 +170,11 @@ def load_library(path=LIB_PATH):
     L.hg_kl_lr_rule.argtypes = [vp, vp, vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, vp]
     L.hg_rollout_act.restype = ctypes.c_int
     L.hg_rollout_act.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
-                                 ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp,
-                                 ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
+                                 ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp, ctypes.c_int64,
+                                 vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
     L.hg_gather_stacked.restype = ctypes.c_int
-    L.hg_gather_stacked.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+    L.hg_gather_stacked.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.POINTER(GatherTable),
                                     ctypes.c_int, vp]
     L.hg_ep_stats_slot.restype = ctypes.c_int

@@ -63,7 +63,7 @@ def _slot_views(st, t):
               "mu": st.mu[t], "sigma": st.sigma[t], "rewards": st.rewards[t], "dones": st.dones[t]}
         sl.update(p_actions=vp(sl["actions"].data_ptr()), p_logp=vp(st.actions_log_prob[t].data_ptr()),
                   p_mu=vp(sl["mu"].data_ptr()), p_sigma=vp(sl["sigma"].data_ptr()), p_values=vp(sl["values"].data_ptr()),
-                  p_obs=vp((st.obs_frames if st.obs_frames is not None else st.observations)[t].data_ptr()),
+                  p_obs=vp(st.obs_frames[:, t].data_ptr() if st.obs_frames is not None else st.observations[t].data_ptr()),
                   p_priv=vp(priv[t].data_ptr()) if priv is not None else None,
                   p_rewards=vp(sl["rewards"].data_ptr()), p_dones=vp(sl["dones"].data_ptr()))
         cache[t] = sl
@@ -231,7 +231,7 @@ class PPO:
             mean.shape[1], ctypes.c_int64(w), ctypes.c_int64(critic_obs.shape[1] if priv is not None else 0),
             ctypes.c_int64(obs.stride(0)), ctypes.c_int64(c0), ctypes.c_int64(critic_obs.stride(0)),
             sl["p_actions"], sl["p_logp"], sl["p_mu"], sl["p_sigma"], sl["p_values"] if value is not None else None,
-            sl["p_obs"], sl["p_priv"], int(st.obs_dtype == torch.float16), int(self.row_offset),
+            sl["p_obs"], ctypes.c_int64(st.obs_frames.stride(0) if st.obs_frames is not None else 0), sl["p_priv"], int(st.obs_dtype == torch.float16), int(self.row_offset),
             ctypes.c_uint64(self._rollout_seed), ctypes.c_uint64(self._rollout_counter), s))
         self._rollout_counter += 1
         tr.actions = sl["actions"]
@@ -596,7 +596,7 @@ class PPO:
             self._flat_grad.zero_()
         if self.storage.obs_frames is not None:
             # frame-only storage: the stacked obs rows and the plain tables in one launch
-            self.storage.gather_stacked(idx, self._mb_obs, self._mb_tables)
+            self.storage.gather_stacked(idx, self._mb_obs, self._mb_tables, use_prepared=True)
         else:
             gather_rows(idx, self._mb_tables)
         crit_b = self._mb_critic
@@ -647,6 +647,7 @@ class PPO:
             cur.wait_stream(side)
             self._graph_warm = True
             return out
+        st.prepare_gather()  # before a capture: the captured gathers read its persistent buffer
         if self._graphs is None or self._graphs[2] != mb or self._graphs[3] != self._storage_key():
             self._capture(mb)
         ga, gb = self._graphs[0], self._graphs[1]

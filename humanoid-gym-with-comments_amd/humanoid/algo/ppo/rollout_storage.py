@@ -63,7 +63,10 @@ class RolloutStorage:
             if F * W != int(obs_shape[0]) or len(obs_shape) != 1:
                 raise ValueError(f"obs_frames {obs_frames} do not tile the observation shape {obs_shape}")
             self.frame_stack, self.frame_width = F, W
-            self.obs_frames = z(W, dtype=obs_dtype)  # [T, N, W]: the newest frame of each slot's stack
+            # [N, T, W] env-major: the newest frame of each slot's stack, a minibatch row's frames
+            # one contiguous run; slot t of all envs is the strided view obs_frames[:, t]
+            self.obs_frames = torch.zeros(N, T, W, device=device, dtype=obs_dtype)
+            self._dones_t = None  # [N, T] u8 copy of the dones for the minibatch gathers (prepare_gather)
             self.obs_init = torch.zeros(N, F * W, device=device, dtype=obs_dtype)  # slot 0's stack
             self._observations = None
         else:
@@ -101,15 +104,26 @@ class RolloutStorage:
         self.gather_stacked(idx, out)
         return out.view(T, N, -1)
 
+    def prepare_gather(self):
+        """Env-major copy of the dones ([N, T]: a row's reset scan reads one run) for the
+        minibatch gathers of this update; the buffer is persistent (captured graphs read it)."""
+        if self.obs_frames is None:
+            return
+        if self._dones_t is None:
+            self._dones_t = torch.empty(self.num_envs, self.num_transitions_per_env, dtype=torch.uint8,
+                                        device=self.dones.device)
+        self._dones_t.copy_(self.dones.view(self.num_transitions_per_env, self.num_envs).t())
+
     def obs_key(self):
         """Address identifying the actor observation buffers (captured-graph keys)."""
         return (self.obs_frames if self.obs_frames is not None else self._observations).data_ptr()
 
-    def gather_stacked(self, idx, dst, tables=()):
+    def gather_stacked(self, idx, dst, tables=(), use_prepared=False):
         """dst[i] = the stacked actor observation of storage row idx[i] (frame-only storage), one
         hg_gather_stacked launch on the current stream; dst [rows, F*W] of the storage dtype, or
         bfloat16.  ``tables``: up to two more (src [T*N, w], dst [rows, w]) pairs gathered for the
-        same rows in the same launch (as gather_rows)."""
+        same rows in the same launch (as gather_rows).  ``use_prepared``: read the env-major dones
+        copy of prepare_gather (the caller refreshed it after the rollout)."""
         from humanoid import _native as N
         T, Nn, F, W = self.num_transitions_per_env, self.num_envs, self.frame_stack, self.frame_width
         if (idx.dtype != torch.int64 or not idx.is_contiguous() or not dst.is_contiguous()
@@ -125,9 +139,13 @@ class RolloutStorage:
                                     codes[str(d.dtype)[6:]])
         s = ctypes.c_void_p(torch.cuda.current_stream(idx.device).cuda_stream)
         p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
-        rc = N.lib().hg_gather_stacked(p(idx), idx.numel(), p(self.obs_frames), p(self.obs_init), p(self.dones), T, Nn,
-                                       F, W, codes[str(self.obs_dtype)[6:]], p(dst), codes[str(dst.dtype)[6:]], tabs,
-                                       len(tables), s)
+        if self._dones_t is not None and use_prepared:  # env-major copy (prepare_gather)
+            dones, dts, des = self._dones_t, 1, T
+        else:
+            dones, dts, des = self.dones, Nn, 1
+        rc = N.lib().hg_gather_stacked(p(idx), idx.numel(), p(self.obs_frames), p(self.obs_init), p(dones), dts, des,
+                                       T, Nn, F, W, codes[str(self.obs_dtype)[6:]], p(dst), codes[str(dst.dtype)[6:]],
+                                       tabs, len(tables), s)
         if rc != 0:
             raise RuntimeError(f"hg_gather_stacked failed ({rc})")
 
@@ -138,7 +156,7 @@ class RolloutStorage:
         if self.obs_frames is not None:
             if t == 0:
                 self.obs_init.copy_(transition.observations)
-            self.obs_frames[t].copy_(transition.observations[:, -self.frame_width:])
+            self.obs_frames[:, t].copy_(transition.observations[:, -self.frame_width:])
         else:
             self._observations[t].copy_(transition.observations)
         if self.privileged_observations is not None:

@@ -267,7 +267,8 @@ int hg_gae_normalize(float* advantages, const double* stats, int64_t count, int6
  * observation rows, all into storage slot t (obs_out/critic_obs_out fp32, or fp16 when
  * obs_fp16).  mean [N,A], std [A], value [N]: contiguous device f32; obs row r's columns
  * [obs_col0, obs_col0 + obs_width) at obs + r obs_ld (the newest frame only, for frame-only
- * storage: obs_col0 = (F - 1) W, obs_width = W), critic_obs [N, critic_width] rows at stride
+ * storage: obs_col0 = (F - 1) W, obs_width = W) into obs_out rows obs_out_ld apart (0: packed,
+ * obs_width), critic_obs [N, critic_width] rows at stride
  * critic_obs_ld (the envs' stacks are strided column slices of their history windows); value may
  * be NULL (values computed later in one batched critic pass).
  * hg_rollout_env: rewards_out = rewards + gamma * values * time_outs (time_outs may be NULL),
@@ -277,8 +278,8 @@ int hg_rollout_act(const float* mean, const float* std, const float* value, cons
                    const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
                    int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
                    float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
-                   void* obs_out, void* critic_obs_out, int obs_fp16, int row_offset, uint64_t seed,
-                   uint64_t counter, void* stream);
+                   void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
+                   uint64_t seed, uint64_t counter, void* stream);
 int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
                    int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
                    void* stream);
@@ -308,15 +309,16 @@ int hg_gather_rows_ex(const int64_t* idx, int64_t rows, int64_t src_rows, const 
 /* Minibatch rows of a frame-only observation storage (replaces observations[batch_idx] when the
  * rollout keeps one frame per env-step, rollout_storage.py:153-191 with the stacking of
  * humanoid_env.py:880-887): dst[i] = the F*W stack of storage row s = idx[i] (t = s / N,
- * e = s % N) rebuilt from frames [T, N, W] (the newest frame of each slot's stack), init
- * [N, F*W] (slot 0's whole stack) and dones [T, N] (u8: a reset at post step r zeroes the frames
- * older than slot r + 1's newest).  src_dtype F32 or F16 (frames and init), dst_dtype equal,
+ * e = s % N) rebuilt from frames [N, T, W] (env-major: the newest frame of each slot's stack, a
+ * row's frames one contiguous run), init [N, F*W] (slot 0's whole stack) and the u8 dones of
+ * slot t, env e at dones[t dones_ts + e dones_es] (a reset at post step r zeroes the frames older
+ * than slot r + 1's newest).  src_dtype F32 or F16 (frames and init), dst_dtype equal,
  * BF16, or F32 from F16.  1 <= F <= 64.  Up to two plain [T*N, width] tables (tabs, ntab <= 2, as
  * hg_gather_rows_ex) are gathered for the same rows by the same waves.  One launch, one wave per
  * row. */
 int hg_gather_stacked(const int64_t* idx, int64_t rows, const void* frames, const void* init, const uint8_t* dones,
-                      int T, int N, int F, int W, int src_dtype, void* dst, int dst_dtype,
-                      const hg_gather_table* tabs, int ntab, void* stream);
+                      int64_t dones_ts, int64_t dones_es, int T, int N, int F, int W, int src_dtype, void* dst,
+                      int dst_dtype, const hg_gather_table* tabs, int ntab, void* stream);
 
 /* ---- PPO optimizer: fused global-norm clip + Adam (replaces
  * nn.utils.clip_grad_norm_(params, max_grad_norm); optimizer.step(), ppo.py:212-214) ----

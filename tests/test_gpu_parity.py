@@ -1465,7 +1465,7 @@ def test_frame_only_storage_rebuilds_stacks(obs_dtype):
     ppo = PPO(ac, device="cuda:0")
     ppo.init_storage(n, T, [705], [219], [12], obs_dtype=obs_dtype, obs_frames=(15, 47))
     st = ppo.storage
-    assert st.obs_frames is not None and st.obs_frames.shape == (T, n, 47)
+    assert st.obs_frames is not None and st.obs_frames.shape == (n, T, 47)  # env-major
     obs, cobs = env.obs_buf, env.privileged_obs_buf
     rec, rec_c = [], []
     with torch.inference_mode():
@@ -1496,3 +1496,8 @@ def test_frame_only_storage_rebuilds_stacks(obs_dtype):
         dc, de = torch.empty(1000, 219, dtype=dt, device="cuda:0"), torch.empty(1000, 43, device="cuda:0")
         st.gather_stacked(idx, dst, [(crit, dc), (extra, de)])
         assert torch.equal(dst, flat[idx].to(dt)) and torch.equal(dc, crit[idx].to(dt)) and torch.equal(de, extra[idx])
+        # with the env-major dones copy the graphed update reads
+        st.prepare_gather()
+        dst.zero_()
+        st.gather_stacked(idx, dst, [(crit, dc)], use_prepared=True)
+        assert torch.equal(dst, flat[idx].to(dt)) and torch.equal(dc, crit[idx].to(dt))
