@@ -837,6 +837,8 @@ int x6_img_dispatch(int tile, int mode, int img, GemmX6Args xa, bool vec, bool e
     case 24: return launch_x6_img<128, 128, 2, 2, 2>(mode, img, xa, vec, elu, s);
     case 25: return launch_x6_img<256, 128, 4, 2, 1>(mode, img, xa, vec, elu, s);
     case 26: return launch_x6_img<128, 128, 2, 4, 2>(mode, img, xa, vec, elu, s);
+    case 27: return launch_x6_img<128, 256, 2, 4, 1>(mode, img, xa, vec, elu, s);
+    case 28: return launch_x6_img<64, 256, 2, 4, 1>(mode, img, xa, vec, elu, s);
     default: return launch_x6_img<64, 128, 2, 2, 1>(mode, img, xa, vec, elu, s);  // 19
   }
 }
@@ -876,12 +878,12 @@ int launch_x6(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-constexpr int NTILES = 26;
+constexpr int NTILES = 28;
 // block rows of a tile id (the column-partial row count of mode 1)
 int tile_bm(int tile) {
   if (tile == 25) return 256;
   return (tile <= 2 || (tile >= 8 && tile <= 10) || tile == 12 || tile == 13 || tile == 16 || tile == 17 ||
-          (tile >= 20 && tile <= 22) || tile == 24 || tile == 26)
+          (tile >= 20 && tile <= 22) || tile == 24 || tile == 26 || tile == 27)
              ? 128
              : 64;
 }
@@ -1018,6 +1020,8 @@ extern "C" int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B
     case 24: return launch_x6<128, 128, 2, 2, 2>(mode, xa, vec, elu, s);
     case 25: return launch_x6<256, 128, 4, 2, 1>(mode, xa, vec, elu, s);
     case 26: return launch_x6<128, 128, 2, 4, 2>(mode, xa, vec, elu, s);
+    case 27: return launch_x6<128, 256, 2, 4, 1>(mode, xa, vec, elu, s);
+    case 28: return launch_x6<64, 256, 2, 4, 1>(mode, xa, vec, elu, s);
     default: return launch_x6<64, 128, 2, 2, 1>(mode, xa, vec, elu, s);  // 19
   }
 }
@@ -1046,6 +1050,8 @@ extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, in
     case 24: return launch_x6<128, 128, 2, 2, 2>(md, xa, vec, false, s);
     case 25: return launch_x6<256, 128, 4, 2, 1>(md, xa, vec, false, s);
     case 26: return launch_x6<128, 128, 2, 4, 2>(md, xa, vec, false, s);
+    case 27: return launch_x6<128, 256, 2, 4, 1>(md, xa, vec, false, s);
+    case 28: return launch_x6<64, 256, 2, 4, 1>(md, xa, vec, false, s);
     default: return launch_x6<64, 128, 2, 2, 1>(md, xa, vec, false, s);
   }
 }

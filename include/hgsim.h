@@ -467,7 +467,7 @@ int hg_linear_act_tile(int64_t rows, int n, int k);
  *     Y unused); colpart (may be NULL) receives the column sums of C per row tile,
  *     [hg_gemm_colpart_rows(M, tile), N], reduced later in fixed order (hg_colsum_jobs).
  * tile 1..18 = f32-MFMA block tiles (exact f32 products, f32 accumulation, v_mfma_f32_32x32x2_f32);
- * tile 19..26 = the same product on the bf16 matrix cores with every f32 operand split exactly
+ * tile 19..28 = the same product on the bf16 matrix cores with every f32 operand split exactly
  * into three bf16 terms and the six products of total order <= 2 accumulated in f32
  * (v_mfma_f32_32x32x16_bf16; error per element below torch's f32 GEMM's, csrc/hg_gemm.hip);
  * hg_gemm_tile picks one.  Rows of A, B, C 4-byte aligned (16-byte rows take the vector-load
@@ -480,12 +480,12 @@ int hg_gemm_tile(int mode, int64_t M, int N, int K);
  * s < slices of the reduction over K rows, C + s * cstride [M, N] (ldc) =
  * sum_{k in slice s} A(m, k) B(n, k), with kmajor 0: A [K, M] (lda), B [K, N] (ldb) (the row-major
  * activations / gradients themselves), kmajor 1: A [M, K], B [N, K] (their transposes) — the
- * slices summed later in fixed order (hg_colsum_jobs).  tile 19..26 (the bf16-split kernels of
+ * slices summed later in fixed order (hg_colsum_jobs).  tile 19..28 (the bf16-split kernels of
  * hg_gemm_f32). */
 int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                       int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile, void* stream);
 int64_t hg_gemm_colpart_rows(int64_t M, int tile);
-/* Operand images of the bf16-split tiles (19..26): an f32 operand X with `rows` rows (the
+/* Operand images of the bf16-split tiles (19..28): an f32 operand X with `rows` rows (the
  * product's M or N side) and reduction length K, split once into the three exact bf16 terms and
  * stored in the kernels' LDS fragment order (16-deep k chunks, count rounded up to even; three
  * planes; rows padded to a multiple of 256; zero past rows / K; csrc/hg_gemm.hip), so a GEMM block

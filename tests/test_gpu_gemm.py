@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 pytestmark = pytest.mark.gpu
 
 REL = 1e-6
-TILES = list(range(1, 27))  # 1..18 f32 MFMA, 19..26 bf16-split (6-term)
+TILES = list(range(1, 29))  # 1..18 f32 MFMA, 19..28 bf16-split (6-term)
 
 
 def _need_gpu():
@@ -123,7 +123,7 @@ def test_gemm_wgrad_matches_fp64(rows, n, k, S):
     bound = REL * (gh.double().abs().t() @ x.double().abs()) * 1.5  # + the slice sum's roundings
     ght, xt = gh.t().contiguous(), x.t().contiguous()
     for kmajor, (A, B) in ((0, (gh, x)), (1, (ght, xt))):
-        for tile in range(19, 27):
+        for tile in range(19, 29):
             part = torch.full((S, n, k + 2), 5.0, device=dev)  # strided output: the pad columns untouched
             rc = L.hg_gemm_f32_wgrad(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), part.data_ptr(), k + 2,
                                      n * (k + 2), n, k, rows, S, kmajor, tile, _stream())
@@ -165,7 +165,7 @@ def test_gemm_images_bitwise_equal(rows, k, n):
     aimg = _image(L, x, 0, rows, k)
     for mode, B, trans in ((0, W, 0), (1, Wd, 1)):
         bimg = _image(L, B, trans, n, k)
-        for tile in range(19, 27):
+        for tile in range(19, 29):
             parts = int(L.hg_gemm_colpart_rows(rows, tile))
             outs = []
             for form in ("staged", "b_image", "ab_image"):
@@ -216,7 +216,7 @@ def test_gemm_wgrad_images_match_fp64(rows, n, k, S):
     ref = gh.double().t() @ x.double()
     bound = REL * (gh.double().abs().t() @ x.double().abs()) * 1.5
     ai, bi = _image(L, gh, 1, n, rows), _image(L, x, 1, k, rows)
-    for tile in range(19, 27):
+    for tile in range(19, 29):
         part = torch.full((S, n, k + 2), 5.0, device=dev)
         rc = L.hg_gemm_wgrad_img(ai.data_ptr(), bi.data_ptr(), part.data_ptr(), k + 2, n * (k + 2), n, k, rows, S,
                                  tile, _stream())
