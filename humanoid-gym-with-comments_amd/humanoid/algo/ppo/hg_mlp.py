@@ -247,7 +247,8 @@ _GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG,
 # Weight gradients stay on hipBLASLt: the bf16-split kernel with
 # split-K slices (LDS-transposed staging of the row-major gh and x, or explicit transposes) was
 # 0.57-0.94x of its tuned TN kernels on every shape.
-_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 22)], (128, 128): [(_BIG, 5)]}
+# The 64x256 tile on 8 waves (28) with the W^T image: 256->512 72.9 -> 67.5 us (x6_image_probe_wide.jsonl).
+_GEMM_DX = {(256, 512): [(_BIG, 28)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 22)], (128, 128): [(_BIG, 5)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
 # The bf16-split tiles read B (the weight) from an image split once per MLP call
 # (hg_gemm_x6_image_jobs: every routed layer's forward and input-grad image in ONE launch) and
