@@ -548,6 +548,7 @@ class PPO:
         self._packed = torch.empty(st.num_transitions_per_env * st.num_envs, sum(widths), dtype=torch.float32,
                                    device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
+        self._one_grad = torch.ones((), dtype=torch.float32, device=dev)
         # [value, surrogate, lin-vel loss sums, KL mean of the current minibatch]: the fused loss
         # accumulates into it directly
         self._stats4 = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -619,7 +620,8 @@ class PPO:
             self._sums.add_(torch.stack([value_loss.detach(), surrogate_loss.detach(), lin_vel_loss.detach()]))
         if self._dp and self._adaptive:
             self._kl_slot.copy_(self._kl)
-        loss.backward()
+        # d loss / d loss = 1 from a persistent tensor: no fill launch per minibatch in the graph
+        loss.backward(gradient=self._one_grad)
 
     def _mb_step(self):
         """Captured minibatch step: adaptive learning rate, global-norm clip, fused Adam."""
