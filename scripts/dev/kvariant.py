@@ -73,8 +73,19 @@ DIV = [("  float s = denom > 1e-6f * a * e ? fminf(fmaxf((b * f - c * e) / denom
        ("    C.cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);",
         "    C.cn = dist > 1e-9f ? __builtin_amdgcn_rcpf(dist) * dv : mk(0.f, -1.f, 0.f);")]
 
+# compiler-flag variants (same source): AMDGPU machine-scheduler strategies for the latency-bound
+# per-wave chain (scheduling only: bitwise identical results)
+FLAG_VARIANTS = {
+    "ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "iter_ilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "memclause": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+    "trackers": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+    "bias_lat": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
+}
+
 VARIANTS = {
     "base": [],
+    "ilp": [], "iter_ilp": [], "memclause": [], "trackers": [], "bias_lat": [],
     "no_round2": [("const int rounds = nitems > 32 ? 2 : 1;", "const int rounds = 1;")],
     "pgs_spec": [(PGS_NG_OLD, PGS_NG_NEW), (PGS_OLD, PGS_NEW)],
     "fastdiv": DIV,
@@ -96,7 +107,7 @@ def build(names):
         hip = os.path.join(PKG, "csrc", f"_kvar_{name}.hip")   # next to hg_common.h
         open(hip, "w").write(s)
         try:
-            r = subprocess.run([HIPCC] + FLAGS + ["-c", hip, "-o", os.path.join(d, "hg_physics.o"),
+            r = subprocess.run([HIPCC] + FLAGS + FLAG_VARIANTS.get(name, []) + ["-c", hip, "-o", os.path.join(d, "hg_physics.o"),
                                                   "-Rpass-analysis=kernel-resource-usage"],
                                capture_output=True, text=True)
         finally:
