@@ -1125,7 +1125,8 @@ __global__ void __launch_bounds__(64 * PWAVES) k_post_step(HgState S, const hg_c
 // row's sliding window instead of a copy of the whole stack; one block per (env, table) row.  The
 // last block also folds the episode statistics (ep_stats[k] = acc[k] / n_reset / episode_length_s
 // when any env reset) and clears the accumulators.
-__global__ void __launch_bounds__(256) k_window_stats(HgWindow A, HgWindow B, const float* __restrict__ frame_a,
+constexpr int WIN_ROWS = 4;  // (env, table) rows per k_window_stats block, one wave each
+__global__ void __launch_bounds__(64 * WIN_ROWS) k_window_stats(HgWindow A, HgWindow B, const float* __restrict__ frame_a,
                                                       const float* __restrict__ frame_b,
                                                       const uint8_t* __restrict__ reset, int n, float* ep_stats,
                                                       float inv_len_s, int ring_slot) {
@@ -1146,7 +1147,10 @@ __global__ void __launch_bounds__(256) k_window_stats(HgWindow A, HgWindow B, co
     if (k < 24) acc[k] = 0.f;
     return;
   }
-  const int b = blockIdx.x;
+  // one wave per (env, table) row, WIN_ROWS rows per block
+  const int b = blockIdx.x * WIN_ROWS + (threadIdx.x >> 6);
+  if (b >= 2 * n) return;
+  const int lane = threadIdx.x & 63;
   const bool a = b < n;
   const HgWindow& T = a ? A : B;
   const int e = a ? b : b - n;
@@ -1157,11 +1161,11 @@ __global__ void __launch_bounds__(256) k_window_stats(HgWindow A, HgWindow B, co
   float* __restrict__ h0 = row + (size_t)T.head * T.width;
   if (T.shift_src >= 0) {  // h0 == row; source and destination slots do not overlap (HW >= frames - 1)
     const float* __restrict__ src = row + (size_t)T.shift_src * T.width;
-    for (int k = threadIdx.x; k < hist; k += blockDim.x) h0[k] = rs ? 0.f : src[k];
+    for (int k = lane; k < hist; k += 64) h0[k] = rs ? 0.f : src[k];
   } else if (rs) {
-    for (int k = threadIdx.x; k < hist; k += blockDim.x) h0[k] = 0.f;
+    for (int k = lane; k < hist; k += 64) h0[k] = 0.f;
   }
-  for (int k = threadIdx.x; k < T.width; k += blockDim.x) h0[hist + k] = fr[k];
+  for (int k = lane; k < T.width; k += 64) h0[hist + k] = fr[k];
 }
 
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
@@ -1174,8 +1178,8 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
   else
     hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
                        frame_priv);
-  const int g = 2 * n + 1;  // one block per (env, table) row + the statistics block
-  hipLaunchKernelGGL(k_window_stats, dim3(g), dim3(64), 0, stream, obs, priv, frame_obs, frame_priv, S->reset_buf, n,
-                     S->ep_stats, inv_len_s, ep_slot);
+  const int g = (2 * n + WIN_ROWS - 1) / WIN_ROWS + 1;  // WIN_ROWS (env, table) rows per block + the statistics block
+  hipLaunchKernelGGL(k_window_stats, dim3(g), dim3(64 * WIN_ROWS), 0, stream, obs, priv, frame_obs, frame_priv,
+                     S->reset_buf, n, S->ep_stats, inv_len_s, ep_slot);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
