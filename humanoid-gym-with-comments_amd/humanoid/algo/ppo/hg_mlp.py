@@ -151,8 +151,10 @@ def _skinny_backward_act(g, h, W, red):
 # 31 -> 17 us (S=16), 128x256 52 -> 20 us (S=32), 256x512 79 -> 55 us (S=4), 768x219 105 -> 78 us
 # (S=32), 256x768 106 -> 86 us (S=4).
 # Re-measured with the chunk sum included (scripts/probes/dw_split_probe.py,
-# profiles/r3_gemm/dw_split_with_chunk_sum.jsonl): 512x705 S=2 176 us -> S=16 161 us; the others
-# keep their factors (within 1-2 us of the best).
+# profiles/r3_gemm/dw_split_with_chunk_sum.jsonl): 512x705 S=2 176 us -> S=16 161 us on hipBLASLt's
+# default kernel for that bmm (a TunableOp entry tuned for it measured 185 us in place,
+# dw_split_tuned_s16.jsonl, so the table keeps no entry for it); the others keep their factors
+# (within 1-2 us of the best).
 _DW_SPLIT = {(128, 256): 32, (128, 128): 16, (256, 512): 4, (128, 705): 8, (512, 705): 16, (768, 219): 32,
              (256, 768): 4}
 
