@@ -149,9 +149,22 @@ class OnPolicyRunner:
             if on_gpu and lazy:
                 losses = self.alg.update(sync=False)
                 ev[2].record()
+                # the loss means go to pinned host memory behind the update (a copy queued on the
+                # stream, read one iteration later): a plain float() of a device tensor would wait
+                # for this iteration's whole update and leave the GPU idle while the host queues
+                # the next rollout
+                means3 = (losses[0], losses[1], losses[3])
+                if all(torch.is_tensor(x) for x in means3):  # device 0-d means (graphed update)
+                    dev_means = torch.stack(means3)
+                    host_means = torch.empty(dev_means.shape, dtype=torch.float32, pin_memory=True)
+                    host_means.copy_(dev_means, non_blocking=True)
+                    copied = torch.cuda.Event()
+                    copied.record()
+                else:  # the eager warm-up update returned host floats
+                    host_means, copied = torch.tensor([float(x) for x in means3]), None
                 if pending is not None:
                     self._resolve_stats(*pending)
-                pending = (ev, losses)
+                pending = (ev, host_means, copied)
                 ep_infos.clear()
                 continue
             mean_value_loss, mean_surrogate_loss, sym_loss, mean_base_lin_vel_loss = self.alg.update()
@@ -176,11 +189,13 @@ class OnPolicyRunner:
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, "model_{}.pt".format(self.current_learning_iteration)))
 
-    def _resolve_stats(self, ev, losses):
-        """last_iteration_stats from an iteration's phase events and device loss means (waits for
-        that iteration's end only)."""
+    def _resolve_stats(self, ev, host_means, copied):
+        """last_iteration_stats from an iteration's phase events and its loss means (copied to
+        pinned host memory behind that iteration's update; waits for that iteration's end only)."""
         ev[2].synchronize()
-        v, s, _, lv = [float(x) for x in losses]
+        if copied is not None:
+            copied.synchronize()
+        v, s, lv = [float(x) for x in host_means.tolist()]
         self.last_iteration_stats = dict(collection_time=ev[0].elapsed_time(ev[1]) * 1e-3,
                                          learn_time=ev[1].elapsed_time(ev[2]) * 1e-3,
                                          value_loss=v, surrogate_loss=s, lin_vel_loss=lv)
