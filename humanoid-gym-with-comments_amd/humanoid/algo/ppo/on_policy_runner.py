@@ -99,6 +99,12 @@ class OnPolicyRunner:
         lenbuffer = deque(maxlen=100)
         cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
         cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        # per-step episode-end records of the rollout, read by the host once per iteration (the
+        # reference reads the finished episodes' sums every step: a host wait per policy step)
+        T = self.num_steps_per_env
+        ep_done = torch.zeros(T, self.env.num_envs, dtype=torch.bool, device=self.device)
+        ep_ret = torch.zeros(T, self.env.num_envs, dtype=torch.float, device=self.device)
+        ep_len = torch.zeros(T, self.env.num_envs, dtype=torch.float, device=self.device)
         tot_iter = self.current_learning_iteration + num_learning_iterations
         # without a log writer nothing in the loop needs the iteration's numbers on the host: its
         # phase events and loss means are read one iteration later (after the next iteration's
@@ -115,7 +121,7 @@ class OnPolicyRunner:
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 ev[0].record()
             with torch.inference_mode():
-                for _ in range(self.num_steps_per_env):
+                for step in range(self.num_steps_per_env):
                     actions = self.alg.act(obs, critic_obs)
                     obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
                     critic_obs = privileged_obs if privileged_obs is not None else obs
@@ -132,11 +138,12 @@ class OnPolicyRunner:
                             ep_infos.append(ep)
                         cur_reward_sum += rewards
                         cur_episode_length += 1
-                        new_ids = (dones > 0).nonzero(as_tuple=False)
-                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
-                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
-                        cur_reward_sum[new_ids] = 0
-                        cur_episode_length[new_ids] = 0
+                        done = dones.reshape(-1) > 0
+                        ep_done[step].copy_(done)
+                        ep_ret[step].copy_(cur_reward_sum)
+                        ep_len[step].copy_(cur_episode_length)
+                        cur_reward_sum.masked_fill_(done, 0)
+                        cur_episode_length.masked_fill_(done, 0)
                 if on_gpu:
                     ev[1].record()
                 stop = time.time()
@@ -179,6 +186,15 @@ class OnPolicyRunner:
                                              value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
                                              lin_vel_loss=mean_base_lin_vel_loss)
             if self.log_dir is not None:
+                # the rollout's finished episodes in step order, env order within a step (the
+                # order the reference appends them in): one host read per iteration, after the
+                # update's own host read
+                d, r, ln = ep_done.cpu(), ep_ret.cpu(), ep_len.cpu()
+                for t in range(self.num_steps_per_env):
+                    ids = d[t].nonzero(as_tuple=False)[:, 0]
+                    if ids.numel():
+                        rewbuffer.extend(r[t][ids].numpy().tolist())
+                        lenbuffer.extend(ln[t][ids].numpy().tolist())
                 self.log(locals())
                 if it % self.save_interval == 0:
                     self.save(os.path.join(self.log_dir, "model_{}.pt".format(it)))
