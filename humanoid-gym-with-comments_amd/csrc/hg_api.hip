@@ -489,4 +489,8 @@ extern "C" int hg_set_env_props(void* sim, const float* friction, const float* b
   return hipGetLastError() == hipSuccess ? HG_OK : fail(s, HG_ERR_HIP, "k_set_props launch failed");
 }
 
+#ifndef HG_SRC_HASH
+#error "build through the Makefile: HG_SRC_HASH stamps the sources the library is built from"
+#endif
+extern "C" const char* hg_source_hash(void) { return HG_SRC_HASH; }
 extern "C" const char* hg_version(void) { return "hg_sim 0.3 (gfx950, K_step: 32 lanes/env, LDS-resident, MFMA Delassus, register PGS)"; }

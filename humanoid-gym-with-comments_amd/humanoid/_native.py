@@ -106,7 +106,8 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_mlp_act_backward_bf16", "hg_linear_skinny_forward_bf16", "hg_linear_skinny_backward_bf16",
            "hg_cast_bf16_jobs", "hg_linear_act_forward", "hg_linear_act_tile", "hg_gemm_f32", "hg_gemm_tile",
            "hg_gemm_colpart_rows", "hg_gemm_f32_wgrad", "hg_gemm_x6_image_bytes", "hg_gemm_x6_image_jobs", "hg_gemm_wgrad_img",
-           "hg_gemm_f32_img", "hg_linear_skinny_backward_act", "hg_linear_skinny_colpart_rows", "hg_version"]
+           "hg_gemm_f32_img", "hg_linear_skinny_backward_act", "hg_linear_skinny_colpart_rows", "hg_version",
+           "hg_source_hash"]
 
 _LIB = None
 
@@ -119,8 +120,26 @@ class GatherTable(ctypes.Structure):
                 ("src_dtype", ctypes.c_int32), ("dst_dtype", ctypes.c_int32)]
 
 
+def source_hash(pkg_root=PKG_ROOT):
+    """sha256 (first 16 hex digits) of the library's sources in the Makefile's stamp order (SRCS,
+    csrc/hg_common.h, include/hgsim.h), as the Makefile computes it; None when the sources are
+    not in the tree."""
+    import hashlib
+    try:
+        with open(os.path.join(pkg_root, "Makefile")) as f:
+            srcs = next(ln.split("=", 1)[1].split() for ln in f if ln.startswith("SRCS ="))
+        h = hashlib.sha256()
+        for rel in srcs + ["csrc/hg_common.h", "../include/hgsim.h"]:
+            with open(os.path.join(pkg_root, rel), "rb") as f:
+                h.update(f.read())
+        return h.hexdigest()[:16]
+    except (OSError, StopIteration):
+        return None
+
+
 def load_library(path=LIB_PATH):
-    """Load libhgsim.so and declare signatures.  Raises if the HIP library is missing."""
+    """Load libhgsim.so and declare signatures.  Raises if the HIP library is missing, or if it
+    was built from other sources than the tree's (a stale binary: hg_source_hash)."""
     if not os.path.exists(path):
         raise RuntimeError(
             f"hg_sim HIP library not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
@@ -128,6 +147,14 @@ def load_library(path=LIB_PATH):
     # torch first, so libamdhip64.so.7 resolves to the runtime torch already loaded (one HIP runtime)
     import torch  # noqa: F401
     L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    L.hg_source_hash.restype = ctypes.c_char_p
+    L.hg_source_hash.argtypes = []
+    want = source_hash()
+    if want is not None and path == os.path.join(PKG_ROOT, "csrc", "libhgsim.so"):
+        got = L.hg_source_hash().decode()
+        if got != want:
+            raise RuntimeError(f"{path} was built from other sources (stamp {got}, tree {want}): rebuild it "
+                               "(`make -C humanoid-gym-with-comments_amd`)")
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     L.hg_arena_bytes.restype = sz
     L.hg_arena_bytes.argtypes = [ctypes.POINTER(HgCfg)]

@@ -57,6 +57,11 @@ class OnPolicyRunner:
                                + "_" + train_cfg["runner"]["run_name"])
         self.device = device
         self.env = env
+        if hasattr(env, "stable_observations"):
+            # PPO copies each observation stack into its rollout storage before the next env.step
+            # (hg_rollout_act, or a clone in the non-fused act), so the env may hand out its live
+            # window views instead of a fresh copy per step
+            env.stable_observations = False
         num_critic_obs = env.num_privileged_obs if env.num_privileged_obs is not None else env.num_obs
         policy_cls = {"ActorCritic": ActorCritic}[self.cfg["policy_class_name"]]
         actor_critic = policy_cls(env.num_obs, num_critic_obs, env.num_actions, **self.policy_cfg).to(self.device)

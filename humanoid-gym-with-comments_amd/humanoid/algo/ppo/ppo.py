@@ -255,8 +255,12 @@ class PPO:
         t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
         t.action_mean = self.actor_critic.action_mean.detach()
         t.action_sigma = self.actor_critic.action_std.detach()
-        t.observations = obs
-        t.critic_observations = critic_obs
+        # the reference keeps the obs tensors and copies them into the storage after env.step
+        # (ppo.py:123-125, rollout_storage.py:90-91), relying on the env allocating new ones per
+        # step; hg_sim's window views are rewritten in place by the next step (a reset zeroes the
+        # older frames), so a device tensor is copied here, before the step
+        t.observations = obs.clone() if obs.is_cuda else obs
+        t.critic_observations = critic_obs.clone() if critic_obs.is_cuda else critic_obs
         return t.actions
 
     def process_env_step(self, rewards, dones, infos):

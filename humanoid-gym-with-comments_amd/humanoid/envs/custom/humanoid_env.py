@@ -147,6 +147,13 @@ class XBotLFreeEnv(BaseTask):
         super().__init__(cfg, sim_params, physics_engine, sim_device, headless)
         self._init_buffers()
         self._prepare_reward_function()
+        # step() / get_observations() hand out tensors that stay valid across later steps, as the
+        # reference's (its compute_observations allocates a new obs_buf per step,
+        # humanoid_env.py:880-887): a copy of the current window stack.  OnPolicyRunner turns this
+        # off — its PPO copies the stack into the rollout storage before the next step — and then
+        # the returned tensors are the live strided window views, valid until the next step()
+        # (a reset zeroes that env's older frames in place).
+        self.stable_observations = True
         self.init_done = True
         # reset_idx(all) + compute_observations() (humanoid_env.py:176-178)
         self._launch_reset(None)
@@ -517,7 +524,13 @@ class XBotLFreeEnv(BaseTask):
         if kt is not None:
             kt.stop("k_post")
         self._publish_extras()
-        return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
+        return self.get_observations(), self.get_privileged_observations(), self.rew_buf, self.reset_buf, self.extras
+
+    def get_observations(self):
+        return self.obs_buf.clone() if self.stable_observations else self.obs_buf
+
+    def get_privileged_observations(self):
+        return self.privileged_obs_buf.clone() if self.stable_observations else self.privileged_obs_buf
 
     def reset_idx(self, env_ids):
         """reset_idx (humanoid_env.py:1109-1163) for the given env ids, as a device mask; also

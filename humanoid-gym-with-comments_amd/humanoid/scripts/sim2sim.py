@@ -222,6 +222,7 @@ def run(policy, profile="mjcf", commands=((0.4, 0.0, 0.0),), duration=10.0, envs
     alive = torch.ones(n, dtype=torch.bool, device=env.device)
     tr = {k: [] for k in ("base_vel", "base_wz", "target_q", "q", "height")}
     q_all = []
+    env.rows_dropped.zero_()  # the counter is cumulative over the sim's life (include/hgsim.h)
     with torch.no_grad():
         for k in range(steps):
             env.commands[:, :3] = cmd

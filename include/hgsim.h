@@ -181,7 +181,8 @@ enum hg_tensor_id {
   HG_T_EP_STATS_RING,    /* [HG_EP_RING, 24] EP_STATS as left by each post/reset launch, launch k in row
                             k % HG_EP_RING (hg_ep_stats_slot): the per-step extras["episode"] snapshot
                             without a copy launch */
-  HG_T_ROWS_DROPPED,     /* [N] int32: constraint rows / contact points the row budget dropped, summed over substeps */
+  HG_T_ROWS_DROPPED,     /* [N] int32: constraint rows / contact points the row budget dropped, summed over substeps;
+                         * zero at hg_create, CUMULATIVE afterwards (resets do not clear it: zero it before a run) */
   HG_T_COUNT
 };
 
@@ -512,8 +513,10 @@ int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, con
 int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M, int N,
                       int64_t K, int slices, int tile, void* stream);
 
-/* library build info */
+/* library build info; hg_source_hash: first 16 hex digits of the sha256 of the sources the
+ * library was built from (the Makefile's SRCS, csrc/hg_common.h, include/hgsim.h, concatenated) */
 const char* hg_version(void);
+const char* hg_source_hash(void);
 
 #ifdef __cplusplus
 }
