@@ -234,6 +234,7 @@ class PPO:
             sl["p_obs"], ctypes.c_int64(st.obs_frames.stride(0) if st.obs_frames is not None else 0), sl["p_priv"], int(st.obs_dtype == torch.float16), int(self.row_offset),
             ctypes.c_uint64(self._rollout_seed), ctypes.c_uint64(self._rollout_counter), s))
         self._rollout_counter += 1
+        st.writes += 1
         tr.actions = sl["actions"]
         tr.values = sl["values"]
         tr.actions_log_prob = sl["logp"]

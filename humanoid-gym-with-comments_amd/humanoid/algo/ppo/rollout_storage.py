@@ -87,6 +87,8 @@ class RolloutStorage:
         self.saved_hidden_states_a = None
         self.saved_hidden_states_c = None
         self.step = 0
+        self.writes = 0          # bumped by every write of a slot (add_transitions, PPO's fused act)
+        self._obs_cache = None   # frame-only storage: (key, rebuilt [T, N, obs])
         self.gae_fn = None  # optional override (tests); default: HIP kernel
         self.time_outs = None  # [T, N, 1] u8, only when PPO defers the value pass (device path)
         self.values_deferred = False
@@ -95,14 +97,21 @@ class RolloutStorage:
 
     @property
     def observations(self):
-        """[T, N, obs] actor observations (frame-only storage: rebuilt on each access)."""
+        """[T, N, obs] actor observations.  Frame-only storage: a READ-ONLY reconstruction (writing
+        into it does not reach the storage — write through add_transitions), rebuilt from the
+        frames + dones once per change of the storage (``writes``) and cached until the next."""
         if self.obs_frames is None:
             return self._observations
+        key = (self.writes, self.step)
+        if self._obs_cache is not None and self._obs_cache[0] == key:
+            return self._obs_cache[1]
         T, N = self.num_transitions_per_env, self.num_envs
         idx = torch.arange(T * N, device=self.device, dtype=torch.int64)
         out = torch.empty(T * N, self.obs_shape[0], dtype=self.obs_dtype, device=self.device)
         self.gather_stacked(idx, out)
-        return out.view(T, N, -1)
+        out = out.view(T, N, -1)
+        self._obs_cache = (key, out)
+        return out
 
     def prepare_gather(self):
         """Env-major copy of the dones ([N, T]: a row's reset scan reads one run) for the
@@ -153,6 +162,7 @@ class RolloutStorage:
         if self.step >= self.num_transitions_per_env:
             raise AssertionError("Rollout buffer overflow")
         t = self.step
+        self.writes += 1
         if self.obs_frames is not None:
             if t == 0:
                 self.obs_init.copy_(transition.observations)

@@ -15,7 +15,7 @@ Recipe:
     on them are "parity unpinned" (see DESIGN.md).
 
 Usage:  python tests/golden/gen_goldens.py [name ...]   (writes tests/golden/*.npz; names: gae actor_critic
-        ppo_update env math pipeline heights terrain mjcf)
+        ppo_update ppo_update_full env math pipeline heights terrain mjcf)
 """
 import importlib.util
 import os
@@ -229,6 +229,49 @@ def gen_ppo_update(mods):
                lin_vel_loss=np.float64(lvloss), learning_rate=np.float64(ppo.learning_rate))
     out.update(sd_to_np(ac.state_dict(), "final/"))
     np.savez_compressed(os.path.join(OUT, "ppo_update.npz"), **out)
+
+
+def gen_ppo_update_full(mods):
+    """ppo_update_full.npz: the reference's PPO.update (ppo.py:144-226) at the production network
+    dims on a 2048 x 24 rollout (12288-row minibatches), inputs from ppo_full_recipe (regenerated by
+    the test, not committed).  Outputs: the three loss means, the learning rate and every final
+    parameter; also the per-minibatch KL means (the adaptive rule's input; asserted to sit inside
+    one branch of the rule with a 1.5x margin, so the LR schedule is not decided by rounding)."""
+    import ppo_full_recipe as R
+    AC = mods["actor_critic"].ActorCritic
+    PPO = mods["ppo"].PPO
+    torch.manual_seed(0)
+    ac = AC(**R.DIMS)
+    shapes = [(k, tuple(v.shape)) for k, v in ac.state_dict().items()]
+    init = R.parameters(shapes)
+    ac.load_state_dict({k: torch.from_numpy(v) for k, v in init.items()})
+    ppo = PPO(ac, device="cpu", **R.PPO_KW)
+    ppo.init_storage(R.N_ENVS, R.T, [R.DIMS["num_actor_obs"]], [R.DIMS["num_critic_obs"]], [R.DIMS["num_actions"]])
+    st = ppo.storage
+    for k, v in R.storage(init["std"]).items():
+        getattr(st, k).copy_(torch.from_numpy(v))
+    st.step = R.T
+    kls = []
+    real_mean = torch.mean
+
+    def mean_spy(x, *a, **kw):   # the KL mean of ppo.py:165 is the only torch.mean of a 1-d tensor there
+        m = real_mean(x, *a, **kw)
+        if x.dim() == 1 and not a and not kw:
+            kls.append(float(m))
+        return m
+    torch.mean = mean_spy
+    try:
+        torch.manual_seed(R.PERM_SEED)
+        vloss, sloss, sym, lvloss = ppo.update()
+    finally:
+        torch.mean = real_mean
+    lo, hi = R.PPO_KW["desired_kl"] / 2.0, R.PPO_KW["desired_kl"] * 2.0
+    print("ppo_update_full: minibatch KL means", kls, "lr", ppo.learning_rate)
+    assert len(kls) == 8 and all(k < lo / 1.5 or lo * 1.5 < k < hi / 1.5 or k > hi * 1.5 for k in kls), kls
+    out = dict(value_loss=np.float64(vloss), surrogate_loss=np.float64(sloss), lin_vel_loss=np.float64(lvloss),
+               learning_rate=np.float64(ppo.learning_rate), kl_means=np.asarray(kls, np.float64))
+    out.update({"final/" + k: v.detach().numpy().copy() for k, v in ac.state_dict().items()})
+    np.savez_compressed(os.path.join(OUT, "ppo_update_full.npz"), **out)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -771,6 +814,8 @@ def main(only=None):
         gen_actor_critic(mods)
     if run("ppo_update"):
         gen_ppo_update(mods)
+    if run("ppo_update_full"):
+        gen_ppo_update_full(mods)
     install_stubs()
     from humanoid.envs.custom import humanoid_env as he
     if run("env"):

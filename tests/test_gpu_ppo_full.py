@@ -1,0 +1,169 @@
+"""The production update against the reference at production shapes.
+
+``ppo_update_full.npz`` is the reference's PPO.update (/root/reference/humanoid/algo/ppo/
+ppo.py:144-226, actor_critic.py:53-89) on the production networks (705 / 219 / 12, actor
+[512, 256, 128], critic [768, 256, 128], lin-vel [128, 128]) with 12288-row minibatches
+(tests/golden/ppo_full_recipe.py builds the inputs here and in the generator).  At that size every
+route of hg_mlp runs: the bf16-split forward / input-gradient tiles, the weight images, the
+f32-MFMA tiles of the small layers, the skinny output layers, the split-K weight gradients, the
+fused loss, the KL / LR rule and the fused clip + Adam.
+
+Stated tolerance: the three loss means within 1e-4 relative (surrogate: 1e-3
+relative + 1e-6), the learning rate within 1e-12 (the KL means sit 1.57x inside the rule's raise
+branch), and the parameter updates (final - init) element-wise within DELTA_RTOL relative +
+DELTA_SCALE of the tensor's largest update + DELTA_ULPS ulp of the parameter for all but DELTA_OUTLIER_FRAC of each tensor's elements, every
+element within DELTA_MAX_ABS.  The outliers are Adam's first step: m̂/sqrt(v̂) = sign(g), so an
+element whose minibatch gradient is at the f32 summation noise may move by +lr on one side and
+-lr on the other; the bound is 2 x (the first steps' learning rates) plus the tight term.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import ppo_full_recipe as R  # noqa: E402
+
+DELTA_RTOL, DELTA_SCALE, DELTA_ULPS = 2e-4, 1e-5, 8.0
+DELTA_OUTLIER_FRAC = 1e-3
+DELTA_MAX_ABS = 6e-5
+
+
+def _setup(monkeypatch):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from humanoid.algo.ppo import ActorCritic, PPO
+    torch.manual_seed(0)
+    ac = ActorCritic(**R.DIMS)
+    shapes = [(k, tuple(v.shape)) for k, v in ac.state_dict().items()]
+    init = R.parameters(shapes)
+    ac.load_state_dict({k: torch.from_numpy(v) for k, v in init.items()})
+    ppo = PPO(ac, device="cuda:0", **R.PPO_KW)
+    ppo.init_storage(R.N_ENVS, R.T, [R.DIMS["num_actor_obs"]], [R.DIMS["num_critic_obs"]], [R.DIMS["num_actions"]])
+    data = R.storage(init["std"])
+    real = torch.randperm
+
+    def randperm_cpu(n, *a, out=None, device=None, **kw):
+        # the reference draws the permutation on the CPU generator (storage on the CPU there)
+        p = real(n)
+        if out is not None:
+            out.copy_(p)
+            return out
+        return p.to(device or "cpu")
+    monkeypatch.setattr(torch, "randperm", randperm_cpu)
+    return ac, ppo, init, data
+
+
+def _load_storage(ppo, data, perturb=None):
+    st = ppo.storage
+    for k, v in data.items():
+        t = torch.from_numpy(v)
+        if perturb is not None and k == perturb:
+            t = t.to(torch.bfloat16).float()
+        getattr(st, k).copy_(t)
+    st.step = R.T
+
+
+def _compare(ac, losses, lr, g, init):
+    """(failures, stats) of one update against the golden.  Parameters are compared through the
+    update itself, delta = final - init (about 1e-4 per element: comparing the ~0.03-sized final
+    values would hide a 1e-3 relative error of the step), element-wise against
+    DELTA_RTOL |delta_ref| + DELTA_SCALE max |delta_ref| + DELTA_ULPS ulp(param) (elements whose
+    Adam steps cancel have a tiny delta whose relative error is meaningless; the final add rounds
+    at the parameter's ulp once per Adam step)."""
+    fails, stats = [], {}
+    vloss, sloss, _, lvloss = losses
+    for name, got, want, rtol, atol in (("value_loss", vloss, g["value_loss"], 1e-4, 0.0),
+                                        ("surrogate_loss", sloss, g["surrogate_loss"], 1e-3, 1e-6),
+                                        ("lin_vel_loss", lvloss, g["lin_vel_loss"], 1e-4, 0.0)):
+        stats[name] = [float(got), float(want)]
+        if not abs(float(got) - float(want)) <= atol + rtol * abs(float(want)):
+            fails.append(f"{name} {float(got)!r} vs {float(want)!r}")
+    stats["learning_rate"] = [lr, float(g["learning_rate"])]
+    if not abs(lr - float(g["learning_rate"])) <= 1e-12 * float(g["learning_rate"]):
+        fails.append(f"learning_rate {lr!r} vs {float(g['learning_rate'])!r}")
+    per = {}
+    for k, v in ac.state_dict().items():
+        p0 = init[k].astype(np.float64)
+        want = g["final/" + k].astype(np.float64) - p0
+        got = v.detach().cpu().numpy().astype(np.float64) - p0
+        d = np.abs(got - want)
+        noise = DELTA_ULPS * np.spacing(np.abs(init[k])).astype(np.float64) + DELTA_SCALE * np.abs(want).max()
+        rel = d / (np.abs(want) + noise)
+        out = d > DELTA_RTOL * np.abs(want) + noise
+        per[k] = dict(n=int(d.size), outside=int(out.sum()), rel_p50=float(np.quantile(rel, 0.5)),
+                      rel_p999=float(np.quantile(rel, 0.999)), max_abs=float(d.max()),
+                      delta_ref_max=float(np.abs(want).max()))
+        if out.mean() > DELTA_OUTLIER_FRAC or d.max() > DELTA_MAX_ABS:
+            fails.append(f"{k}: {int(out.sum())} of {d.size} outside, p50 rel {per[k]['rel_p50']:.2e}, "
+                         f"max |d delta| {d.max():.3g}")
+    stats["params"] = per
+    return fails, stats
+
+
+def _report(tag, stats):
+    path = os.environ.get("HG_TOL_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": f"ppo_full/{tag}", **stats}) + "\n")
+
+
+def test_ppo_update_full_dims_eager_matches_reference(golden, monkeypatch):
+    """The first update() (the eager warm-up path, fused loss and kernels, no graph)."""
+    ac, ppo, init, data = _setup(monkeypatch)
+    g = golden("ppo_update_full.npz")
+    _load_storage(ppo, data)
+    torch.manual_seed(R.PERM_SEED)
+    losses = ppo.update()
+    assert ppo._graphs is None
+    fails, stats = _compare(ac, losses, ppo.learning_rate, g, init)
+    _report("eager", stats)
+    assert not fails, "; ".join(fails)
+
+
+def _restore(ppo, init):
+    """Parameters, Adam state and learning rate back to the start, in place (the captured graph
+    keeps reading the same tensors)."""
+    with torch.no_grad():
+        for k, p in ppo.actor_critic.named_parameters():
+            p.copy_(torch.from_numpy(init[k]))
+        for st in ppo.optimizer.state.values():
+            for t in st.values():
+                t.zero_()
+    ppo.learning_rate = R.PPO_KW["learning_rate"]
+
+
+def test_ppo_update_full_dims_graphed_matches_reference(golden, monkeypatch):
+    """The production path: the whole update replayed from one captured HIP graph."""
+    ac, ppo, init, data = _setup(monkeypatch)
+    g = golden("ppo_update_full.npz")
+    _load_storage(ppo, data)
+    torch.manual_seed(R.PERM_SEED)
+    ppo.update()                       # warm-up (eager)
+    _restore(ppo, init)
+    _load_storage(ppo, data)
+    torch.manual_seed(R.PERM_SEED)
+    losses = ppo.update()              # captured + replayed
+    assert ppo._graphs is not None and ppo._graphs[1] is None, "expected the one-graph update"
+    fails, stats = _compare(ac, losses, ppo.learning_rate, g, init)
+    _report("graphed", stats)
+    assert not fails, "; ".join(fails)
+
+
+def test_ppo_update_full_dims_detects_bf16_level_error(golden, monkeypatch):
+    """Sensitivity: the same update with the actor observations rounded to bf16 (the error a
+    single-term bf16 product would make in the first layer) must FAIL the golden comparison."""
+    ac, ppo, init, data = _setup(monkeypatch)
+    g = golden("ppo_update_full.npz")
+    _load_storage(ppo, data, perturb="observations")
+    torch.manual_seed(R.PERM_SEED)
+    losses = ppo.update()
+    fails, stats = _compare(ac, losses, ppo.learning_rate, g, init)
+    _report("bf16_mutation", stats)
+    assert fails, "a bf16-level input error went undetected by the golden comparison"

@@ -73,3 +73,25 @@ def test_gae_requires_hip_on_cpu():
     st = RolloutStorage(2, 3, [3], [4], [1])
     with pytest.raises(RuntimeError):
         st.compute_returns(torch.zeros(2, 1), 0.99, 0.95)
+
+
+def test_ppo_update_full_dims_cpu(golden):
+    """The production-size golden (ppo_update_full.npz) on the CPU path (the reference's
+    arithmetic verbatim): the same comparison the GPU test applies (tests/test_gpu_ppo_full.py)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import ppo_full_recipe as R
+    from test_gpu_ppo_full import _compare, _load_storage
+    g = golden("ppo_update_full.npz")
+    torch.manual_seed(0)
+    ac = ActorCritic(**R.DIMS)
+    init = R.parameters([(k, tuple(v.shape)) for k, v in ac.state_dict().items()])
+    ac.load_state_dict({k: torch.from_numpy(v) for k, v in init.items()})
+    ppo = PPO(ac, device="cpu", **R.PPO_KW)
+    ppo.init_storage(R.N_ENVS, R.T, [705], [219], [12])
+    _load_storage(ppo, R.storage(init["std"]))
+    torch.manual_seed(R.PERM_SEED)
+    losses = ppo.update()
+    fails, _ = _compare(ac, losses, ppo.learning_rate, g, init)
+    assert not fails, "; ".join(fails)
