@@ -519,7 +519,8 @@ class PPO:
     # HIP-graph update: the minibatch step is captured once as two graphs and replayed
     #   A: gather the minibatch rows (static index buffer) -> losses -> backward into the flat
     #      gradient buffer; KL mean; loss sums
-    #   (world_size > 1: all-reduce of the flat gradients and of the KL mean, eager RCCL calls)
+    #   (data parallel: all-reduce of the flat gradients and of the KL mean — captured in the one
+    #   update graph on RCCL, eager between the two graphs' replays on gloo)
     #   B: adaptive learning rate, global-norm clip, fused Adam
     # The first update() runs eagerly on a side stream (the warm-up graph capture needs); the
     # graphs are captured at the start of the second one.  Minibatch order: one randperm per
@@ -574,19 +575,26 @@ class PPO:
         if critic is not obs:
             tables.insert(1 if not frames else 0, (critic, self._mb_critic))
         self._mb_tables, self._mb_widths = tables, widths
-        # world size 1: the whole update (epochs x minibatches, each with its LR rule and Adam step)
-        # is ONE graph reading its row indices from a static permutation buffer; with ranks to
-        # all-reduce between the backward and the step, two graphs per minibatch
-        self._whole = not self._dp and self._flat_grad is None
+        # the whole update (epochs x minibatches, each with its LR rule and Adam step) is ONE graph
+        # reading its row indices from a static permutation buffer: at world size 1, and with ranks
+        # on RCCL, whose gradient all-reduce is captured inside the graph between each backward and
+        # its step (RCCL kernels replay like any other node; the communicator exists from the
+        # eager warm-up update).  gloo cannot be captured: two graphs per minibatch with the
+        # all-reduce between their replays.
+        self._whole = (not self._dp and self._flat_grad is None) or self._collective_in_graph()
         if self._whole:
             nmb = self.num_mini_batches
             self._perm = torch.zeros(nmb * mb, dtype=torch.int64, device=dev)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: the process group's watchdog thread may query its events meanwhile
+            with torch.cuda.graph(g, capture_error_mode="thread_local" if self._dp else "global"):
                 for _ in range(self.num_learning_epochs):
                     for i in range(nmb):
-                        self.optimizer.zero_grad(set_to_none=True)  # fresh gradients from each backward
-                        self._mb_backward(self._perm[i * mb:(i + 1) * mb])
+                        if self._flat_grad is None:
+                            self.optimizer.zero_grad(set_to_none=True)  # fresh gradients from each backward
+                        self._mb_backward(self._perm[i * mb:(i + 1) * mb])  # zeroes the flat buffer (dp)
+                        if self._dp:
+                            dist.all_reduce(self._flat_grad)  # gradients + the KL slot, in the graph
                         self._mb_step()
             self._graphs = (g, None, mb, self._storage_key())
             return
@@ -595,6 +603,12 @@ class PPO:
         with torch.cuda.graph(gb, pool=ga.pool()):
             self._mb_step()
         self._graphs = (ga, gb, mb, self._storage_key())
+
+    def _collective_in_graph(self):
+        """RCCL ("nccl" backend): the per-minibatch gradient all-reduce is captured in the update
+        graph (HG_DP_GRAPH_COLLECTIVE=0 keeps the two-graph form with an eager all-reduce)."""
+        return (self._dp and dist.is_initialized() and dist.get_backend() == "nccl"
+                and os.environ.get("HG_DP_GRAPH_COLLECTIVE", "1") != "0")
 
     def _mb_backward(self, idx):
         """Captured minibatch body: gather rows -> losses -> backward (+ KL mean, loss sums)."""

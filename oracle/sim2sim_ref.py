@@ -75,7 +75,14 @@ class Sim2SimRef:
 
     def __init__(self, hc, model, policy, root, q, qd, mass0, fric, cmds, precision="f64", cycle_time=0.64,
                  obs_scales=(2.0, 1.0, 1.0, 0.05), clip_obs=18.0, clip_actions=18.0, frame_stack=15,
-                 default_dof_pos=None, lam=None, cause_slots=None):
+                 default_dof_pos=None, lam=None, cause_slots=None, joint_perm=None, joint_sign=None,
+                 omega_frame="base", euler="sim2sim", phase="sincos"):
+        """Convention switches (scripts/onnx_sweep.py; defaults = the reference script's loop):
+        joint_perm / joint_sign: the policy's joint i is the simulator's joint joint_perm[i] times
+        joint_sign[i], for the observed q - q_default, qd, the last action and the action applied
+        (obs and action together); omega_frame "base" (sim2sim.py's IMU gyro) | "world" | "neg";
+        euler "sim2sim" (sim2sim.py:57-77 + its wrap) | "0_2pi" (isaacgym get_euler_xyz's range) |
+        "neg"; phase "sincos" | "neg" (half a cycle shifted) | "swap" (cos, sin)."""
         n = root.shape[0]
         self.n, self.hc, self.policy = n, hc, policy
         self.sim = P.RefSim(hc, model, n, precision)
@@ -100,28 +107,40 @@ class Sim2SimRef:
         # {name: warm-start impulse slots}, e.g. base-box corners vs ground, hand / box pairs
         self.cause_slots = cause_slots or {}
         self.fall_cause = np.full(n, "", dtype=object)
+        self.perm = np.arange(12) if joint_perm is None else np.asarray(joint_perm, np.int64)
+        self.sign = np.ones(12) if joint_sign is None else np.asarray(joint_sign, np.float64)
+        self.omega_frame, self.euler, self.phase = omega_frame, euler, phase
+        self.travel = np.zeros(n)                      # base displacement along the command (m)
+        self.x0 = self.sim.root[:, 0:2].astype(np.float64).copy()
 
     def frame(self):
         s = self.sim
         quat = s.root[:, 3:7].astype(np.float64)
-        omega = quat_rotate_inverse(quat, s.root[:, 10:13].astype(np.float64))
+        w_world = s.root[:, 10:13].astype(np.float64)
+        omega = {"base": lambda: quat_rotate_inverse(quat, w_world), "world": lambda: w_world,
+                 "neg": lambda: -quat_rotate_inverse(quat, w_world)}[self.omega_frame]()
         ph = 2.0 * math.pi * self.k * self.dt / self.cycle_time
+        sn, cs = {"sincos": (math.sin(ph), math.cos(ph)), "neg": (-math.sin(ph), -math.cos(ph)),
+                  "swap": (math.cos(ph), math.sin(ph))}[self.phase]
         f = np.empty((self.n, 47))
-        f[:, 0], f[:, 1] = math.sin(ph), math.cos(ph)
+        f[:, 0], f[:, 1] = sn, cs
         f[:, 2] = self.cmds[:, 0] * self.lin_s
         f[:, 3] = self.cmds[:, 1] * self.lin_s
         f[:, 4] = self.cmds[:, 2] * self.ang_s
-        f[:, 5:17] = (s.q - self.default) * self.pos_s
-        f[:, 17:29] = s.qd * self.vel_s
+        f[:, 5:17] = (s.q - self.default)[:, self.perm] * self.sign * self.pos_s
+        f[:, 17:29] = s.qd[:, self.perm] * self.sign * self.vel_s
         f[:, 29:41] = self.action
         f[:, 41:44] = omega
-        f[:, 44:47] = quat_to_euler(quat)
+        e = quat_to_euler(quat)
+        f[:, 44:47] = {"sim2sim": e, "0_2pi": np.mod(e, 2.0 * math.pi), "neg": -e}[self.euler]
         return np.clip(f, -self.clip_obs, self.clip_obs)
 
     def step(self):
         self.hist = np.concatenate([self.hist[:, 47:], self.frame()], axis=1)
         self.action = np.clip(self.policy(self.hist), -self.clip_act, self.clip_act)
-        self.sim.step(self.action)
+        applied = np.empty_like(self.action)
+        applied[:, self.perm] = self.action * self.sign
+        self.sim.step(applied)
         self.k += 1
         s = self.sim
         fell = (np.linalg.norm(s.contact[:, 0, :], axis=1) > 1.0) | (s.nonfinite != 0)
@@ -138,6 +157,12 @@ class Sim2SimRef:
         self.err_v += live * np.linalg.norm(vb[:, :2] - self.cmds[:, :2], axis=1)
         self.err_w += live * np.abs(wb[:, 2] - self.cmds[:, 2])
         self.alive_steps += live
+        # displacement along the commanded direction, frozen at the fall
+        d = s.root[:, 0:2].astype(np.float64) - self.x0
+        c = self.cmds[:, :2]
+        cn = np.linalg.norm(c, axis=1)
+        along = np.where(cn > 0, (d * c).sum(1) / np.maximum(cn, 1e-12), 0.0)
+        self.travel = np.where(self.alive, along, self.travel)
 
     def run(self, steps):
         for _ in range(steps):
@@ -148,4 +173,4 @@ class Sim2SimRef:
         a = np.maximum(self.alive_steps, 1.0)
         return dict(fell=(self.fall_step >= 0), fall_step=self.fall_step.copy(), lin_vel_error=self.err_v / a,
                     yaw_rate_error=self.err_w / a, survival_s=self.alive_steps * self.dt,
-                    fall_cause=list(self.fall_cause))
+                    fall_cause=list(self.fall_cause), travel_m=self.travel.copy())

@@ -119,6 +119,8 @@ def _worker(rank, world, port, out_path, rccl=False):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     elif rccl:
         os.environ["HG_DP_FORCE"] = "1"
+        if rccl == "eager":  # the two-graph form with the eager all-reduce between the replays
+            os.environ["HG_DP_GRAPH_COLLECTIVE"] = "0"
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         assert dist.get_backend() == "nccl"
     import bench
@@ -230,24 +232,27 @@ def test_dp_graphed_update_matches_single_process(tmp_path):
         assert abs(a - float(b)) <= 1e-5 * max(1.0, abs(float(b)))
 
 
-def test_rccl_two_graph_update_matches_single_process(tmp_path):
-    """The RCCL code path executed: a world-size-1 "nccl" group with the
-    multi-rank update forced (HG_DP_FORCE=1) — parameter broadcast, the flat gradient buffer, the
-    backward graph -> dist.all_reduce on RCCL -> step graph per minibatch, the advantage-statistics
-    all-reduce.  At world size 1 the all-reduce is the identity, so the parameters must equal the
-    one-graph single-process update bit for bit."""
+@pytest.mark.parametrize("mode", ["graph", "eager"])
+def test_rccl_update_matches_single_process(tmp_path, mode):
+    """The RCCL code path executed: a world-size-1 "nccl" group with the multi-rank update forced
+    (HG_DP_FORCE=1) — parameter broadcast, the flat gradient buffer with the KL slot, the
+    advantage-statistics all-reduce, and per minibatch backward -> all_reduce on RCCL -> step:
+    mode "graph" (the default) captures the collective inside the ONE update
+    graph; mode "eager" is the two-graph form with the all-reduce between the replays.  At world
+    size 1 the all-reduce is the identity, so the parameters must equal the single-process
+    update bit for bit."""
     _need_gpu()
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     runs = {}
-    for name, rccl in (("rccl", True), ("single", False)):
+    for name, rccl in (("rccl", mode), ("single", False)):
         p = ctx.Process(target=_worker, args=(0, 1, _port(), str(tmp_path / f"{name}.pt"), rccl))
         p.start()
         p.join(240)
         assert p.exitcode == 0, f"{name} process exit code {p.exitcode}"
         runs[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
     R, S = runs["rccl"], runs["single"]
-    assert R["backend"] == "nccl" and R["dp"] and R["graphed"] and not R["whole"]
+    assert R["backend"] == "nccl" and R["dp"] and R["graphed"] and R["whole"] == (mode == "graph")
     assert S["backend"] is None and not S["dp"] and S["whole"]
     assert R["calls"] == S["calls"] == 3
     assert R["lr"] == S["lr"]

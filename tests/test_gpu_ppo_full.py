@@ -31,7 +31,11 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 import ppo_full_recipe as R  # noqa: E402
 
 DELTA_RTOL, DELTA_SCALE, DELTA_ULPS = 2e-4, 1e-5, 8.0
-DELTA_OUTLIER_FRAC = 1e-3
+# measured (profiles/r4_tol/tol_report_k20.jsonl): at most 4 of 90240 elements (4.4e-5) of one
+# tensor outside the element tolerance, max |d delta| 1.7e-7; the bounds keep room for Adam's
+# first-step sign flips of near-zero gradients (2 x 1.5e-5) and a bf16-level error fails them
+# with 87 % of actor.0.weight outside
+DELTA_OUTLIER_FRAC = 5e-4
 DELTA_MAX_ABS = 6e-5
 
 
