@@ -273,10 +273,11 @@ def load_library(path=LIB_PATH):
                                         ctypes.POINTER(vp), ctypes.c_int, vp]
     L.hg_gemm_f32_img.restype = ctypes.c_int
     L.hg_gemm_f32_img.argtypes = [ctypes.c_int, vp, ctypes.c_int64, vp, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64,
-                                  vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]
+                                  vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int64, ctypes.c_int64, vp]
     L.hg_gemm_wgrad_img.restype = ctypes.c_int
     L.hg_gemm_wgrad_img.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
-                                    ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp]
+                                    ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, vp]
     L.hg_gemm_tile.restype = ctypes.c_int
     L.hg_gemm_tile.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
     L.hg_gemm_colpart_rows.restype = ctypes.c_int64

@@ -388,7 +388,8 @@ def gemm_forward(h, W, b, elu=True, tile=0, out=None, img=None):
         raise RuntimeError("gemm_forward: out must be a float32 [rows, n] tensor with unit column stride")
     if img is not None:
         rc = L.hg_gemm_f32_img(0, h.data_ptr(), h.stride(0), None, img.data_ptr(), b.data_ptr(), None, 0,
-                               y.data_ptr(), y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
+                               y.data_ptr(), y.stride(0), None, rows, n, k, 1 if elu else 0, tile, 0,
+                               img.numel() * img.element_size(), _stream(h.device))
     else:
         rc = L.hg_gemm_f32(0, h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0,
                            y.data_ptr(), y.stride(0), None, rows, n, k, 1 if elu else 0, tile, _stream(h.device))
@@ -416,7 +417,7 @@ def gemm_input_grad(gh, W, y_prev, gb, red=None, tile=0, img=None):
     if img is not None:
         rc = L.hg_gemm_f32_img(1, gh.data_ptr(), gh.stride(0), None, img.data_ptr(), None, y_prev.data_ptr(),
                                y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,
-                               _stream(gh.device))
+                               0, img.numel() * img.element_size(), _stream(gh.device))
     else:
         rc = L.hg_gemm_f32(1, gh.data_ptr(), gh.stride(0), W.data_ptr(), W.stride(0), None, y_prev.data_ptr(),
                            y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, kr, 1, tile,

@@ -51,6 +51,10 @@ def timeit(fn):
     return e0.elapsed_time(e1) * 1e3 / ITERS
 
 
+def nbytes(t):
+    return t.numel() * t.element_size()
+
+
 def ck(rc, what):
     if rc != 0:
         raise RuntimeError(f"{what} rc={rc}")
@@ -84,11 +88,13 @@ for tag, rows, k, n in FWD:
 
         def imaged():
             ck(L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), None, img.data_ptr(), b.data_ptr(), None, 0,
-                                 y1.data_ptr(), y1.stride(0), None, rows, n, k, 1, tile, stream()), "img")
+                                 y1.data_ptr(), y1.stride(0), None, rows, n, k, 1, tile, 0, nbytes(img), stream()),
+               "img")
 
         def imaged2():
             ck(L.hg_gemm_f32_img(0, None, 0, aimg.data_ptr(), img.data_ptr(), b.data_ptr(), None, 0,
-                                 y2.data_ptr(), y2.stride(0), None, rows, n, k, 1, tile, stream()), "img2")
+                                 y2.data_ptr(), y2.stride(0), None, rows, n, k, 1, tile, nbytes(aimg), nbytes(img),
+                                 stream()), "img2")
 
         plain()
         imaged()
@@ -122,7 +128,7 @@ for tag, rows, kr, n in DX:
 
         def imaged():
             ck(L.hg_gemm_f32_img(1, g.data_ptr(), g.stride(0), None, img.data_ptr(), None, y.data_ptr(), y.stride(0),
-                                 o1.data_ptr(), o1.stride(0), c1.data_ptr(), rows, n, kr, 1, tile, stream()), "img")
+                                 o1.data_ptr(), o1.stride(0), c1.data_ptr(), rows, n, kr, 1, tile, 0, nbytes(img), stream()), "img")
 
         plain()
         imaged()
@@ -171,7 +177,7 @@ for tag, rows, n, k in ([] if os.environ.get("SKIP_DW") else DW):
             dw = torch.empty(n, k, device=dev)
 
             def ours():
-                ck(L.hg_gemm_wgrad_img(ai.data_ptr(), bi.data_ptr(), part.data_ptr(), k, n * k, n, k, rows, S, tile,
+                ck(L.hg_gemm_wgrad_img(ai.data_ptr(), bi.data_ptr(), part.data_ptr(), k, n * k, n, k, rows, S, tile, nbytes(ai), nbytes(bi),
                                        stream()), "wgrad_img")
                 red.add(part, dw, n * k, S)
                 red.launch(dev)
