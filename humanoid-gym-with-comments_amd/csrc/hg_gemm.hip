@@ -739,227 +739,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_gemm_x6p: the bf16-split product with BOTH operands as images (hg_gemm_x6_image_jobs layout)
-// and an NS-stage LDS-DMA pipeline.  k_gemm_x6 double-buffers and drains every DMA at each
-// chunk's barrier (__syncthreads = vmcnt(0) + s_barrier), so a chunk's copy latency (L2 / HBM,
-// ~1 us) must hide under ONE chunk of MFMAs; here chunk c + NS - 1 is issued while chunk c is
-// computed, and the wait before chunk c's barrier is vmcnt(NS - 2 chunks' DMA instructions) —
-// the copies of the younger chunks stay in flight.  One barrier per chunk: after it every wave has
-// finished reading chunk c - 1, whose stage the next DMA then overwrites.
-//   MODE 0 forward C = act(A B^T + bias), MODE 1 input grad (+ ELU backward, colpart), MODE 2
-//   split-K weight gradient (slice s of kslice reduction rows -> C + s * cstride).
-// KG = 1 (16-deep chunks).  The arithmetic (products, their order, the accumulation) is k_gemm_x6's:
-// results are bitwise equal to the image-fed k_gemm_x6 of the same block tile.
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  // gfx9 s_waitcnt: vmcnt [3:0] + [15:14], expcnt [6:4] = 7, lgkmcnt [11:8] = 15 (no wait)
-  switch (n) {
-#define HG_VM(N) \
-  case N: __builtin_amdgcn_s_waitcnt(((N) & 15) | ((((N) >> 4) & 3) << 14) | (7 << 4) | (15 << 8)); break;
-    HG_VM(0) HG_VM(1) HG_VM(2) HG_VM(3) HG_VM(4) HG_VM(5) HG_VM(6) HG_VM(7) HG_VM(8) HG_VM(9) HG_VM(10)
-    HG_VM(11) HG_VM(12) HG_VM(13) HG_VM(14) HG_VM(15) HG_VM(16) HG_VM(17) HG_VM(18) HG_VM(19) HG_VM(20)
-    HG_VM(21) HG_VM(22) HG_VM(23) HG_VM(24)
-#undef HG_VM
-    default: __builtin_amdgcn_s_waitcnt(0); break;
-  }
-}
-
-template <int BM, int BN, int WGM, int WGN, int NS, int MODE, bool ELU>
-__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6p(GemmX6Args xa) {
-  constexpr int NW = WGM * WGN, NT = 64 * NW;
-  constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
-  constexpr int PA = BM * 2, PB = BN * 2;  // 16-byte slots per plane of one 16-deep chunk
-  constexpr int STAGE = 3 * PA + 3 * PB;
-  constexpr int UA = BM / 32, UB = BN / 32;
-  constexpr int NDMA = 3 * (UA + UB);       // 1 KB DMA instructions per chunk (block)
-  constexpr int DPW = NDMA / NW;            // issued by every wave (the rest by the first waves)
-  static_assert(NS >= 2 && NS <= 5, "pipeline depth");
-  static_assert(TM >= 1 && TN >= 1 && BM == 32 * TM * WGM && BN == 32 * TN * WGN, "wave tiling");
-  static_assert(NS * STAGE * 4 >= WGM * BN, "epilogue reduction buffer fits the staging LDS");
-  static_assert(MODE == 0 || MODE == 1 || MODE == 2, "modes");
-  __shared__ __attribute__((aligned(16))) bf16x8 lds[NS * STAGE];
-  const GemmArgs& g = xa.g;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int i = lane & 31, h = lane >> 5;
-  const unsigned nb = gridDim.x;
-  unsigned L = blockIdx.x;
-  if ((nb & 7u) == 0) L = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
-  if ((int64_t)L >= g.tiles * xa.slices) return;
-  const int slice = (int)((int64_t)L % xa.slices);
-  const int64_t tile = (int64_t)L / xa.slices;
-  const int64_t tm_idx = tile / g.tiles_n;
-  const int64_t m0 = tm_idx * BM;
-  const int n0 = (int)(tile % g.tiles_n) * BN;
-  const int wm0 = (wave % WGM) * (32 * TM), wn0 = (wave / WGM) * (32 * TN);
-  const int64_t mmax = g.M - 1;
-  const int nmax = g.N - 1;
-  const int64_t kbeg = MODE == 2 ? (int64_t)slice * xa.kslice : 0;
-  const int64_t kend = MODE == 2 ? min<int64_t>((int64_t)g.K, kbeg + xa.kslice) : g.K;
-  const int64_t nk = kend - kbeg;
-  const int nchunks = nk > 0 ? (int)((nk + 15) / 16) : 0;
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int m = 0; m < TM; m++)
-#pragma unroll
-    for (int n = 0; n < TN; n++) acc[m][n] = (f32x16)0.f;
-
-  const int64_t cabs0 = kbeg / 16;
-  const bf16x8* baseA = reinterpret_cast<const bf16x8*>(g.A) + m0 * 2 + lane;
-  const bf16x8* baseB = reinterpret_cast<const bf16x8*>(g.B) + (int64_t)n0 * 2 + lane;
-  // chunk c's copies into stage S: unit q = (plane p, 32-row unit u) of A then B
-  auto dma = [&](int c, bf16x8* S) {
-#pragma unroll
-    for (int t = 0; t < (NDMA + NW - 1) / NW; t++) {
-      const int q = wave + NW * t;
-      if (NDMA % NW != 0 && q >= NDMA) break;
-      const bool isA = q < 3 * UA;
-      const int qq = isA ? q : q - 3 * UA;
-      const int U = isA ? UA : UB;
-      const int u = qq % U, p = qq / U;
-      const int64_t pitch = isA ? g.lda : g.ldb;
-      const bf16x8* src = (isA ? baseA : baseB) + ((cabs0 + c) * 3 + p) * pitch + u * 64;
-      bf16x8* dst = S + (isA ? p * PA : 3 * PA + p * PB) + u * 64;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-    }
-  };
-  // prologue: chunks 0 .. NS - 2 in flight
-#pragma unroll
-  for (int c = 0; c < NS - 1; c++)
-    if (c < nchunks) dma(c, lds + c * STAGE);
-  for (int c = 0; c < nchunks; c++) {
-    // chunk c landed (this wave's copies; the younger chunks' may stay in flight), then every
-    // wave's (barrier); after the barrier, chunk c - 1's stage is free for chunk c + NS - 1
-    const int younger = min(NS - 2, nchunks - 1 - c);
-    wait_vmcnt(younger * DPW);
-    // a bare s_barrier: __syncthreads' release fence would drain every DMA in flight (vmcnt(0))
-    __builtin_amdgcn_s_barrier();
-    if (c + NS - 1 < nchunks) dma(c + NS - 1, lds + ((c + NS - 1) % NS) * STAGE);
-    const bf16x8* cur = lds + (c % NS) * STAGE;
-    bf16x8 a[3][TM], b[3][TN];
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-#pragma unroll
-      for (int m = 0; m < TM; m++) a[p][m] = cur[p * PA + x6_slot(BM, 0, wm0 + 32 * m + i, h)];
-#pragma unroll
-      for (int n = 0; n < TN; n++) b[p][n] = cur[3 * PA + p * PB + x6_slot(BN, 0, wn0 + 32 * n + i, h)];
-    }
-#pragma unroll
-    for (int m = 0; m < TM; m++)
-#pragma unroll
-      for (int n = 0; n < TN; n++) {
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b[0][n], acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[1][n], acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[2][n], acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[0][n], acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[1][n], acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[0][n], acc[m][n], 0, 0, 0);
-      }
-  }
-
-  // epilogue (k_gemm_x6's).  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2) + 4h, column i.
-  if (MODE == 0 || MODE == 2) {
-    float* Cs = g.C + (MODE == 2 ? (int64_t)slice * xa.cstride : 0);
-#pragma unroll
-    for (int n = 0; n < TN; n++) {
-      const int cidx = n0 + wn0 + 32 * n + i;
-      if (cidx > nmax) continue;
-      const float bc = (MODE == 0 && g.bias) ? g.bias[cidx] : 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; m++) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
-          if (r <= mmax) {
-            float v = acc[m][n][q] + bc;
-            if (MODE == 0 && ELU) v = v > 0.f ? v : expm1f(v);
-            Cs[r * g.ldc + cidx] = v;
-          }
-        }
-      }
-    }
-  } else {
-    __syncthreads();  // every wave is past its last chunk's LDS reads before the reduction buffer
-    float* red = reinterpret_cast<float*>(lds);  // [WGM][BN] column partials of the waves along M
-#pragma unroll
-    for (int n = 0; n < TN; n++) {
-      const int cl = wn0 + 32 * n + i;
-      const int cidx = n0 + cl;
-      float cs = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; m++) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
-          float v = acc[m][n][q];
-          if (r <= mmax && cidx <= nmax) {
-            if (ELU) {
-              const float yv = g.Y[r * g.ldY + cidx];
-              v = yv > 0.f ? v : v * (yv + 1.f);
-            }
-            g.C[r * g.ldc + cidx] = v;
-          } else {
-            v = 0.f;
-          }
-          cs += v;
-        }
-      }
-      cs += __shfl_xor(cs, 32);
-      if (h == 0) red[(wave % WGM) * BN + cl] = cs;
-    }
-    if (g.colpart) {
-      __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
-        if (n0 + c <= nmax) {
-          float sum = 0.f;
-#pragma unroll
-          for (int w = 0; w < WGM; w++) sum += red[w * BN + c];
-          g.colpart[tm_idx * g.N + n0 + c] = sum;
-        }
-      }
-    }
-  }
-}
-
-template <int BM, int BN, int WGM, int WGN, int NS>
-int launch_x6p(int mode, GemmX6Args xa, bool elu, hipStream_t s) {
-  GemmArgs& g = xa.g;
-  g.tiles_n = (g.N + BN - 1) / BN;
-  const int64_t tiles_m = (g.M + BM - 1) / BM;
-  g.tiles = tiles_m * g.tiles_n;
-  if (mode != 2) xa.slices = 1;
-  if (g.tiles * xa.slices > 0x7fffffff) return HG_ERR_ARG;
-  const dim3 grid((unsigned)(g.tiles * xa.slices)), block(64 * WGM * WGN);
-#define HG_X6P(MD, E) hipLaunchKernelGGL((k_gemm_x6p<BM, BN, WGM, WGN, NS, MD, E>), grid, block, 0, s, xa)
-  if (mode == 2) HG_X6P(2, false);
-  else if (mode == 0 && elu) HG_X6P(0, true);
-  else if (mode == 0) HG_X6P(0, false);
-  else if (elu) HG_X6P(1, true);
-  else HG_X6P(1, false);
-#undef HG_X6P
-  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
-}
-
-// pipelined tiles (both operands as images): 29 + ...
-int x6p_dispatch(int tile, int mode, GemmX6Args xa, bool elu, hipStream_t s) {
-  switch (tile) {
-    case 29: return launch_x6p<128, 128, 2, 2, 3>(mode, xa, elu, s);
-    case 30: return launch_x6p<128, 128, 2, 2, 4>(mode, xa, elu, s);
-    case 31: return launch_x6p<128, 128, 2, 2, 2>(mode, xa, elu, s);
-    case 32: return launch_x6p<128, 64, 2, 2, 3>(mode, xa, elu, s);
-    case 33: return launch_x6p<256, 128, 4, 2, 2>(mode, xa, elu, s);
-    case 34: return launch_x6p<256, 128, 4, 2, 3>(mode, xa, elu, s);
-    case 35: return launch_x6p<128, 256, 2, 4, 2>(mode, xa, elu, s);
-    case 36: return launch_x6p<128, 128, 1, 4, 3>(mode, xa, elu, s);
-    case 37: return launch_x6p<256, 256, 4, 4, 2>(mode, xa, elu, s);
-    case 38: return launch_x6p<64, 128, 2, 2, 4>(mode, xa, elu, s);
-    default: return launch_x6p<128, 64, 2, 2, 4>(mode, xa, elu, s);  // 39
-  }
-}
-constexpr int X6P_FIRST = 29, X6P_LAST = 39;
-
 // Operand images of the bf16-split kernels, a list of operands in one launch.  An operand X with
 // R rows (the product's M or N side) and reduction length K: element (r, k) = P[r ld + k]
 // (trans 0: k-contiguous rows — W of the forward, activations, gradients as the A side) or
@@ -1150,9 +929,8 @@ extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void
                                const float* bias, const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart,
                                int64_t M, int N, int K, int act, int tile, int64_t aimg_bytes, int64_t bimg_bytes,
                                void* stream) {
-  const bool pipelined = tile >= X6P_FIRST && tile <= X6P_LAST;
   if ((!A && !Aimg) || !Bimg || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || (mode != 0 && mode != 1) || act < 0 ||
-      act > 1 || tile < 19 || (tile > NTILES && !pipelined) || (pipelined && !Aimg))
+      act > 1 || tile < 19 || tile > NTILES)
     return HG_ERR_ARG;
   if (!Aimg && lda < K) return HG_ERR_ARG;
   // the images must be the ones hg_gemm_x6_image_jobs builds for this product's shape
@@ -1166,16 +944,14 @@ extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void
   const int64_t la = Aimg ? img_rows(M) * 2 : lda;
   GemmArgs g{a, la, reinterpret_cast<const float*>(Bimg), img_rows(N) * 2, bias, Y, ldY, C, ldc, colpart, M, N, K, 0, 0};
   GemmX6Args xa{g, 0, 0, 1};
-  if (pipelined) return x6p_dispatch(tile, mode, xa, act == 1, (hipStream_t)stream);
   return x6_img_dispatch(tile, mode, Aimg ? 3 : 1, xa, vec, act == 1, (hipStream_t)stream);
 }
 
 extern "C" int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M,
                                  int N, int64_t K, int slices, int tile, int64_t aimg_bytes, int64_t bimg_bytes,
                                  void* stream) {
-  const bool pipelined = tile >= X6P_FIRST && tile <= X6P_LAST;
   if (!Aimg || !Bimg || !C || M <= 0 || N <= 0 || K <= 0 || K > 0x7fffffff || ldc < N || slices < 1 || tile < 19 ||
-      (tile > NTILES && !pipelined))
+      tile > NTILES)
     return HG_ERR_ARG;
   if (aimg_bytes != hg_gemm_x6_image_bytes(M, K) || bimg_bytes != hg_gemm_x6_image_bytes(N, K)) return HG_ERR_ARG;
   if (slices > 1 && cstride < M * (int64_t)ldc) return HG_ERR_ARG;
@@ -1185,7 +961,6 @@ extern "C" int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, i
   // slices start on whole 32-deep chunk pairs of the images
   const int64_t kslice = ((K + slices - 1) / slices + 31) & ~(int64_t)31;
   GemmX6Args xa{g, kslice, cstride, slices};
-  if (pipelined) return x6p_dispatch(tile, 2, xa, false, (hipStream_t)stream);
   return x6_img_dispatch(tile, 2, 3, xa, false, false, (hipStream_t)stream);
 }
 

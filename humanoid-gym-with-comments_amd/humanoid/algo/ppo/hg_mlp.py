@@ -168,8 +168,8 @@ _GEMM_DW = {}
 def _weight_grad(gh, x, red=None):
     rows, n = gh.shape
     k = x.shape[1]
-    route = _route(_GEMM_DW, rows, n, k) if (red is not None and gh.is_contiguous() and x.dim() == 2
-                                             and x.stride(1) == 1) else 0
+    ok = red is not None and gh.is_contiguous() and x.dim() == 2 and x.stride(1) == 1
+    route = _route(_GEMM_DW, rows, n, k) if ok else 0
     if route:
         tile, S = route
         L = N.lib()

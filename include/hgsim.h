@@ -505,16 +505,14 @@ int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* t
  * and A from its image (Aimg: rows M) or, Aimg NULL, staged from A (lda) as in hg_gemm_f32 — the
  * same epilogues and, bit for bit, the same result.  aimg_bytes / bimg_bytes: the images' sizes,
  * checked against hg_gemm_x6_image_bytes(M, K) / (N, K) (an image built for another shape is
- * refused; aimg_bytes is ignored when Aimg is NULL).  Tiles 29..39: the NS-stage LDS-DMA pipelined
- * kernels (both operands as images, Aimg required; bitwise the result of the image-fed tile of the
- * same block shape). */
+ * refused; aimg_bytes is ignored when Aimg is NULL). */
 int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, const void* Bimg, const float* bias,
                     const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K,
                     int act, int tile, int64_t aimg_bytes, int64_t bimg_bytes, void* stream);
 /* hg_gemm_f32_wgrad's split-K weight gradient from two images (Aimg: rows M, Bimg: rows N, both
  * with reduction K — build them with trans 1 from the row-major gh [K, M] and x [K, N]); the
  * slices start on 32-deep chunk pairs, ceil(K / slices) rounded up to a multiple of 32 rows each.
- * aimg_bytes / bimg_bytes as hg_gemm_f32_img; tiles 19..28 and the pipelined 29..39. */
+ * aimg_bytes / bimg_bytes as hg_gemm_f32_img. */
 int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M, int N,
                       int64_t K, int slices, int tile, int64_t aimg_bytes, int64_t bimg_bytes, void* stream);
 

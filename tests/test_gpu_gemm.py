@@ -148,16 +148,6 @@ def _nbytes(img):
     return img.numel() * img.element_size()
 
 
-# block shape (BM, BN, WGM, WGN) of the bf16-split tiles (csrc/hg_gemm.hip x6_img_dispatch,
-# x6p_dispatch); the pipelined tiles 29..39 must equal the image-fed tile of the same shape bitwise
-TILE_SHAPE = {19: (64, 128, 2, 2), 20: (128, 128, 2, 2), 21: (128, 128, 2, 4), 22: (128, 64, 2, 2), 23: (64, 64, 2, 2),
-              24: None, 25: (256, 128, 4, 2), 26: None, 27: (128, 256, 2, 4), 28: (64, 256, 2, 4)}
-PIPE_SHAPE = {29: (128, 128, 2, 2), 30: (128, 128, 2, 2), 31: (128, 128, 2, 2), 32: (128, 64, 2, 2),
-              33: (256, 128, 4, 2), 34: (256, 128, 4, 2), 35: (128, 256, 2, 4), 36: (128, 128, 1, 4),
-              37: (256, 256, 4, 4), 38: (64, 128, 2, 2), 39: (128, 64, 2, 2)}
-PIPELINED = sorted(PIPE_SHAPE)
-
-
 # (rows, k, n): the image forms (hg_gemm_x6_image_jobs + hg_gemm_f32_img, B from its image, A staged
 # or from its image) of modes 0 and 1 against hg_gemm_f32 with the per-block staging, bit for bit
 # (same split, same MFMA order), ragged shapes
@@ -182,9 +172,7 @@ def test_gemm_images_bitwise_equal(rows, k, n):
         for tile in range(19, 29):
             parts = int(L.hg_gemm_colpart_rows(rows, tile))
             outs = []
-            # the pipelined tiles of the same block shape (29..39, both images) join the comparison
-            pipe = [t for t in PIPELINED if PIPE_SHAPE[t] == TILE_SHAPE[tile]]
-            for form in ["staged", "b_image", "ab_image"] + [f"pipelined_{t}" for t in pipe]:
+            for form in ("staged", "b_image", "ab_image"):
                 out = torch.full((rows, n + 2), 3.0, device=dev)
                 cp = torch.full((parts, n), float("nan"), device=dev) if mode == 1 else None
                 bias = b.data_ptr() if mode == 0 else None
@@ -194,11 +182,10 @@ def test_gemm_images_bitwise_equal(rows, k, n):
                     rc = L.hg_gemm_f32(mode, x.data_ptr(), x.stride(0), B.data_ptr(), B.stride(0), bias, Y, ldY,
                                        out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _stream())
                 else:
-                    ab = form != "b_image"
-                    t = int(form.split("_")[1]) if form.startswith("pipelined") else tile
+                    ab = form == "ab_image"
                     rc = L.hg_gemm_f32_img(mode, None if ab else x.data_ptr(), 0 if ab else x.stride(0),
                                            aimg.data_ptr() if ab else None, bimg.data_ptr(), bias, Y, ldY,
-                                           out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, t, _nbytes(aimg),
+                                           out.data_ptr(), out.stride(0), cpp, rows, n, k, 1, tile, _nbytes(aimg),
                                            _nbytes(bimg), _stream())
                 assert rc == 0
                 outs.append((form, out, cp))
@@ -209,7 +196,7 @@ def test_gemm_images_bitwise_equal(rows, k, n):
                 if mode == 1:
                     assert torch.equal(c0, c1), f"tile {tile} {form} colpart"
     # arguments: a misaligned image, a mode without an image form, no A at all, an image of another
-    # shape (its byte size), a pipelined tile without the A image
+    # shape (its byte size), tiles outside the bf16-split range
     out = torch.empty(rows, n, device=dev)
     bimg = _image(L, W, 0, n, k)
     nb = _nbytes(bimg)
@@ -240,7 +227,7 @@ def test_gemm_wgrad_images_match_fp64(rows, n, k, S):
     ref = gh.double().t() @ x.double()
     bound = REL * (gh.double().abs().t() @ x.double().abs()) * 1.5
     ai, bi = _image(L, gh, 1, n, rows), _image(L, x, 1, k, rows)
-    for tile in list(range(19, 29)) + PIPELINED:
+    for tile in range(19, 29):
         part = torch.full((S, n, k + 2), 5.0, device=dev)
         rc = L.hg_gemm_wgrad_img(ai.data_ptr(), bi.data_ptr(), part.data_ptr(), k + 2, n * (k + 2), n, k, rows, S,
                                  tile, _nbytes(ai), _nbytes(bi), _stream())
