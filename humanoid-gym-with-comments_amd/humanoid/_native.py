@@ -107,7 +107,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_cast_bf16_jobs", "hg_linear_act_forward", "hg_linear_act_tile", "hg_gemm_f32", "hg_gemm_tile",
            "hg_gemm_colpart_rows", "hg_gemm_f32_wgrad", "hg_gemm_x6_image_bytes", "hg_gemm_x6_image_jobs", "hg_gemm_wgrad_img",
            "hg_gemm_f32_img", "hg_linear_skinny_backward_act", "hg_linear_skinny_colpart_rows", "hg_version",
-           "hg_source_hash", "hg_policy_forward"]
+           "hg_source_hash"]
 
 _LIB = None
 
@@ -278,10 +278,6 @@ def load_library(path=LIB_PATH):
     L.hg_gemm_wgrad_img.restype = ctypes.c_int
     L.hg_gemm_wgrad_img.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                     ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, vp]
-    L.hg_policy_forward.restype = ctypes.c_int
-    L.hg_policy_forward.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                    ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
-                                    ctypes.POINTER(vp), vp, vp, ctypes.c_int, vp, ctypes.c_int64, vp]
     L.hg_gemm_tile.restype = ctypes.c_int
     L.hg_gemm_tile.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
     L.hg_gemm_colpart_rows.restype = ctypes.c_int64

@@ -542,62 +542,16 @@ def mlp_forward(net, x):
     return _MLP.apply(x, *_params(net))
 
 
-# The rollout's policy forward in ONE launch (hg_policy_forward, csrc/hg_policy.hip): the actor
-# chain K0 -> 512 -> 256 -> 128 -> nout (<= 16) with the activations in LDS, the hidden products
-# on the bf16 matrix cores as exact three-term splits (the bf16-split GEMM's arithmetic), instead
-# of four launches with three [rows, n] activations written and read back.
-POLICY_FUSED = os.environ.get("HG_POLICY_FUSED", "1") != "0"
-_POLICY_DIMS = (512, 256, 128)
-
-
-def _policy_ok(params, x):
-    if not (POLICY_FUSED and len(params) == 8 and x.dim() == 2 and x.dtype == torch.float32 and x.is_cuda
-            and x.stride(1) == 1 and x.data_ptr() % 4 == 0 and x.shape[0] > 0):
-        return False
-    k = x.shape[1]
-    for (W, b), n in zip(((params[0], params[1]), (params[2], params[3]), (params[4], params[5])), _POLICY_DIMS):
-        if tuple(W.shape) != (n, k) or not W.is_contiguous() or not b.is_contiguous():
-            return False
-        k = n
-    Wl, bl = params[6], params[7]
-    return Wl.shape[1] == k and Wl.shape[0] <= 16 and Wl.is_contiguous() and bl.is_contiguous()
-
-
-def policy_forward(params, x, out=None):
-    """The actor MLP (params [W1, b1, ..., Wl, bl], _policy_ok) on x in one hg_policy_forward
-    launch; the hidden weights' operand images in one hg_gemm_x6_image_jobs launch."""
-    rows, k0 = x.shape
-    n1, n2, n3 = _POLICY_DIMS
-    nout = params[6].shape[0]
-    imgs = x6_images([(params[0], 0, n1, k0), (params[2], 0, n2, n1), (params[4], 0, n3, n2)], x.device)
-    y = torch.empty(rows, nout, dtype=torch.float32, device=x.device) if out is None else out
-    if y.numel() != rows * nout or not y.is_contiguous() or y.dtype != torch.float32:
-        raise RuntimeError("policy_forward: out must be a contiguous float32 tensor of rows x nout elements")
-    vp = ctypes.c_void_p
-    rc = N.lib().hg_policy_forward(x.data_ptr(), x.stride(0), rows, k0, n1, n2, n3,
-                                   (vp * 3)(*[im.data_ptr() for im in imgs]),
-                                   (ctypes.c_int64 * 3)(*[im.numel() * im.element_size() for im in imgs]),
-                                   (vp * 3)(params[1].data_ptr(), params[3].data_ptr(), params[5].data_ptr()),
-                                   params[6].data_ptr(), params[7].data_ptr(), nout, y.data_ptr(), nout,
-                                   _stream(x.device))
-    if rc != 0:
-        raise RuntimeError(f"hg_policy_forward failed ({rc})")
-    return y
-
-
 def mlp_infer(net, x, out=None):
-    """net(x) without autograd (rollout inference): the actor chain as one fused launch
-    (policy_forward) where it applies; otherwise hidden layers on the LDS-staged GEMM or the
+    """net(x) without autograd (rollout inference): hidden layers on the LDS-staged GEMM or the
     register-operand fused kernel where ``_GEMM_FWD`` / ``_FUSED_FWD_ROWS`` route them, torch's
-    Linear/ELU otherwise, and the skinny HIP kernel for the output layer (written into ``out``
-    when given)."""
+    Linear/ELU otherwise; the skinny HIP kernel for the output layer (written into ``out`` when
+    given)."""
     mods = list(net)
     h = x
     fimg = None
     if fusable(net):
         params = _params(net)
-        if _policy_ok(params, x):
-            return policy_forward([p.detach() for p in params], x, out)
         fimg = _forward_images(params, len(params) // 2, x.shape[0], x.device, False)[0]
     for j in range(0, len(mods) - 1, 2):
         lin = mods[j]

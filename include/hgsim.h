@@ -516,18 +516,6 @@ int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, con
 int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M, int N,
                       int64_t K, int slices, int tile, int64_t aimg_bytes, int64_t bimg_bytes, void* stream);
 
-/* The rollout's policy forward in ONE launch (replaces the actor MLP of actor_critic.py:36-149 on
- * the device rollout: hidden layers K0 -> n1 -> n2 -> n3 with bias + ELU, then n3 -> nout):
- * y[r][j] for r < rows, j < nout, from x rows (stride ldx, 4-byte aligned).  The hidden products
- * are f32 products on the bf16 matrix cores as the bf16-split GEMM tiles (three-term splits, six
- * products, f32 accumulation) with the weights from their operand images (hg_gemm_x6_image_jobs,
- * trans 0 from W_l [n_l, k_l]; images[l], image_bytes[l] = hg_gemm_x6_image_bytes(n_l, k_l)),
- * biases[l] f32 [n_l]; the output layer Wl [nout, n3] row-major, bl [nout], f32.  Instantiated
- * chain: n1, n2, n3 = 512, 256, 128; nout <= 16.  One block per 32 rows; activations stay in LDS. */
-int hg_policy_forward(const float* x, int64_t ldx, int64_t rows, int K0, int n1, int n2, int n3,
-                      const void* const* images, const int64_t* image_bytes, const float* const* biases,
-                      const float* Wl, const float* bl, int nout, float* y, int64_t ldy, void* stream);
-
 /* library build info; hg_source_hash: first 16 hex digits of the sha256 of the sources the
  * library was built from (the Makefile's SRCS, csrc/hg_common.h, include/hgsim.h, concatenated) */
 const char* hg_version(void);
