@@ -770,7 +770,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     {
       const uint32_t lt = (1u << l) - 1u;
       const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
-      if (l < NGRP) E.grp[l].mu = -1.f;  // single rows unless a contact claims the group below
+      // single rows unless a contact claims the group below (mu = +inf: the PGS disc projection
+      // never scales a single-row group, see A13)
+      if (l < NGRP) E.grp[l].mu = __builtin_huge_valf();
       // round 1: items 0..31 (model constants in registers for the whole launch); round 2 (when
       // the model has more than 32 items): items 32 + l, constants read here.  A contact's rank
       // among the active candidates decides its slot; round 2 ranks after all of round 1, so each
@@ -994,7 +996,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       const int g = l / 3, k = l % 3;
       E.grp[g].invD[k] = own ? __builtin_amdgcn_rcpf(Dd) : 0.f;
       if (k == 1) E.grp[g].Wba = W1;
-      if (k == 2) { E.grp[g].Wca = W2; E.grp[g].Wcb = W1; }
+      // a contact's tangent pair is updated from the same nu (Wcb unused: 0, see A13)
+      if (k == 2) { E.grp[g].Wca = W2; E.grp[g].Wcb = g < E.npts ? 0.f : W1; }
       if (l == 31) { E.grp[10].invD[2] = 0.f; E.grp[10].Wca = 0.f; E.grp[10].Wcb = 0.f; }  // virtual slot 32
       float v = v0;
 #pragma unroll
@@ -1006,11 +1009,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // lane of an env holds all 32 of its env's impulses (uniform per half-wave); the row velocity
     // v_r lives in lane r and is read with scalar v_readlane pairs.  Per group (a, b, c):
     //   a: lambda_a <- clamp(lambda_a + (tgt_a - v_a) / W_aa, lo_a, hi_a)   (normal / single row)
-    //   contact: the tangent pair's unconstrained steps from v_b + W_ba dl_a, v_c + W_ca dl_a,
-    //            projected onto the disc mu * lambda_a (as the oracle: both from the same nu)
-    //   singles: b from v_b + W_ba dl_a, then c from v_c + W_ca dl_a + W_cb dl_b
-    // then every row velocity takes the group's three updates (one FMA each).  Branch-free over
-    // the group kinds; groups empty in both envs of the wave are skipped (scalar branch).
+    //   b: lambda_b' <- clamp(lambda_b + (tgt_b - v_b - W_ba dl_a) / W_bb, lo_b, hi_b)
+    //   c: lambda_c' <- clamp(lambda_c + (tgt_c - v_c - W_ca dl_a - W_cb dl_b') / W_cc, lo_c, hi_c)
+    //   (b, c) <- (b', c') scaled onto the disc |.| <= mu lambda_a
+    // One instruction stream for both group kinds, through the group constants: a contact's
+    // tangent pair has tgt 0, bounds -+BIG (no clamp) and W_cb = 0 (both steps from the same nu,
+    // as the oracle); a single-row group has mu = +inf, so the disc test never scales it (lim =
+    // +-inf or NaN: nn2 > lim^2 is false).  Then every row velocity takes the group's three
+    // updates (one FMA each).  Groups empty in both envs of the wave are skipped (scalar branch).
     {
       float vrow = v0;
       const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;
@@ -1027,21 +1033,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
             const float na = clampf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0], G.hi[0]);
             const float da = na - la;
             const float vb1 = vb + G.Wba * da, vc1 = vc + G.Wca * da;
-            // both row kinds computed, picked per env (branch-free: one instruction stream for
-            // every group, no scalar branches on the chain)
-            float db, dc;
-            {
-              const float l1 = lb - vb1 * G.invD[1], l2 = lc - vc1 * G.invD[2];
-              const float lim = G.mu * na, nn2 = l1 * l1 + l2 * l2;
-              const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
-              const float nbs = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
-              const float dbs = nbs - lb;
-              const float vc2 = vc1 + G.Wcb * dbs;
-              const float ncs = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
-              const bool ct = G.mu >= 0.f;
-              db = ct ? l1 * sc - lb : dbs;
-              dc = ct ? l2 * sc - lc : ncs - lc;
-            }
+            const float nb = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
+            const float vc2 = vc1 + G.Wcb * (nb - lb);
+            const float nc = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
+            const float lim = G.mu * na, nn2 = __builtin_fmaf(nc, nc, nb * nb);  // the order of the oracle's l1^2 + l2^2
+            const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
+            const float db = nb * sc - lb, dc = nc * sc - lc;
             if (rc < RMAX) {
               vrow += wrow[ra] * da + wrow[rb] * db + wrow[rc < RMAX ? rc : 0] * dc;
               lam[rc < RMAX ? rc : 0] += dc;
