@@ -888,6 +888,215 @@ int tile_bm(int tile) {
              : 64;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight gradient on the bf16 matrix cores with LDS transpose reads (round 4):
+//   C_s[m][n] = sum_{r in slice s} A[r][m] B[r][n]     A = gh [R, M], B = x [R, N], both row-major
+// (the reduction runs over the ROWS of both operands, as dW = gh^T x).  Each 16-row chunk of both
+// operands is staged exactly as it lies in memory: coalesced float4 row segments -> registers ->
+// the exact three-term bf16 split (v_cvt_pk_bf16_f32 pairs) -> three row-major bf16 planes in LDS
+// ([16 rows][cols], rows padded by 64 B so a transposed read's four rows fall on disjoint banks).
+// ds_read_b64_tr_b16 then delivers the MFMA operand directly: for the 32x32x16 operand, lane
+// (i, h) needs 8 consecutive reduction rows 8h..8h+7 of column i, i.e. two transposed reads of 4
+// rows x 16 columns per 16-lane group (lane 4q + p addresses row q, columns 4p..4p+3; lane i of
+// the group receives column i).  No transposing staging pass, each element split once per block.
+// The six partial products as k_gemm_x6 (smallest first).  Split-K: slice s covers kslice rows and
+// writes C + s cstride; the slices are summed in fixed order by the column-sum launch.
+struct WgradArgs {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc, cstride;
+  int M, N;
+  int64_t R, kslice;
+  int slices, tiles_n;
+  int64_t tiles;
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t bf16_pair(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ f32x2 bf16_pair_f32(uint32_t u) {
+  f32x2 r;
+  r[0] = __uint_as_float(u << 16);
+  r[1] = __uint_as_float(u & 0xffff0000u);
+  return r;
+}
+// exact split of 4 consecutive values into three planes of 4 bf16 (8 bytes each)
+__device__ __forceinline__ void split3x4(const float v[4], uint2& p0, uint2& p1, uint2& p2) {
+  f32x2 a = {v[0], v[1]}, b = {v[2], v[3]};
+  const uint32_t a0 = bf16_pair(a), b0 = bf16_pair(b);
+  a -= bf16_pair_f32(a0);
+  b -= bf16_pair_f32(b0);
+  const uint32_t a1 = bf16_pair(a), b1 = bf16_pair(b);
+  a -= bf16_pair_f32(a1);
+  b -= bf16_pair_f32(b1);
+  p0 = make_uint2(a0, b0);
+  p1 = make_uint2(a1, b1);
+  p2 = make_uint2(bf16_pair(a), bf16_pair(b));
+}
+
+// one operand's 16-row chunk: COLS columns from col0, rows r0.. (rows at or past rend and columns at
+// or past ncols read 0); items (row, float4 column group), consecutive threads along a row
+template <int COLS, int NT>
+struct TrStage {
+  static constexpr int ITEMS = 16 * (COLS / 4);
+  static constexpr int IPT = (ITEMS + NT - 1) / NT;
+  static constexpr int PITCH = COLS * 2 + 64;  // bytes per LDS row of one plane
+  static constexpr int PLANE = 16 * PITCH;
+  float v[IPT][4];
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int64_t r0, int64_t rend, int col0,
+                                       int ncols, int tid) {
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int idx = tid + j * NT;
+      if (ITEMS % NT != 0 && idx >= ITEMS) break;
+      const int row = idx / (COLS / 4), c = col0 + 4 * (idx % (COLS / 4));
+      const int64_t r = r0 + row;
+      const float* p = P + r * ld + c;
+      if (r < rend && c + 3 < ncols) {
+        const f32x4u x = *reinterpret_cast<const f32x4u*>(p);
+        v[j][0] = x[0]; v[j][1] = x[1]; v[j][2] = x[2]; v[j][3] = x[3];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[j][e] = (r < rend && c + e < ncols) ? p[e] : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int idx = tid + j * NT;
+      if (ITEMS % NT != 0 && idx >= ITEMS) break;
+      const int row = idx / (COLS / 4), c4 = idx % (COLS / 4);
+      uint2 x0, x1, x2;
+      split3x4(v[j], x0, x1, x2);
+      char* d = S + row * PITCH + 8 * c4;
+      *reinterpret_cast<uint2*>(d) = x0;
+      *reinterpret_cast<uint2*>(d + PLANE) = x1;
+      *reinterpret_cast<uint2*>(d + 2 * PLANE) = x2;
+    }
+  }
+};
+
+// the 32x32x16 operand of columns c0 + 0..31 of a staged plane (rows 0..15 of the chunk)
+template <int PITCH>
+__device__ __forceinline__ bf16x8 tr_operand(const char* __restrict__ plane, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const char* a = plane + (8 * (g >> 1) + q) * PITCH + 2 * (c0 + 16 * (g & 1) + 4 * p);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * PITCH));
+  const short e[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, e);
+}
+
+template <int WGM, int WGN, int TM, int TN>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_wgrad_tr(WgradArgs w) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int BM = 32 * TM * WGM, BN = 32 * TN * WGN;
+  typedef TrStage<BM, NT> SA;
+  typedef TrStage<BN, NT> SB;
+  constexpr int STAGE = 3 * SA::PLANE + 3 * SB::PLANE;  // bytes
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const unsigned nb = gridDim.x;
+  unsigned L = blockIdx.x;
+  if ((nb & 7u) == 0) L = (blockIdx.x & 7u) * (nb >> 3) + (blockIdx.x >> 3);
+  if ((int64_t)L >= w.tiles * w.slices) return;
+  // the tiles of one slice are consecutive (one XCD's L2 serves the slice's rows to all of them)
+  const int slice = (int)((int64_t)L / w.tiles);
+  const int64_t tile = (int64_t)L % w.tiles;
+  const int m0 = (int)(tile / w.tiles_n) * BM, n0 = (int)(tile % w.tiles_n) * BN;
+  const int wm0 = (wave % WGM) * (32 * TM), wn0 = (wave / WGM) * (32 * TN);
+  const int64_t kbeg = (int64_t)slice * w.kslice;
+  const int64_t kend = min<int64_t>(w.R, kbeg + w.kslice);
+  const int nchunks = kend > kbeg ? (int)((kend - kbeg + 15) / 16) : 0;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; m++)
+#pragma unroll
+    for (int n = 0; n < TN; n++) acc[m][n] = (f32x16)0.f;
+
+  SA sa;
+  SB sb;
+  if (nchunks > 0) {
+    sa.load(w.A, w.lda, kbeg, kend, m0, w.M, tid);
+    sb.load(w.B, w.ldb, kbeg, kend, n0, w.N, tid);
+    sa.store(lds, tid);
+    sb.store(lds + 3 * SA::PLANE, tid);
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; c++) {
+    const char* cur = lds + (c & 1) * STAGE;
+    char* nxt = lds + ((c + 1) & 1) * STAGE;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      const int64_t r0 = kbeg + (int64_t)(c + 1) * 16;
+      sa.load(w.A, w.lda, r0, kend, m0, w.M, tid);
+      sb.load(w.B, w.ldb, r0, kend, n0, w.N, tid);
+    }
+    bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+#pragma unroll
+      for (int m = 0; m < TM; m++) a[p][m] = tr_operand<SA::PITCH>(cur + p * SA::PLANE, wm0 + 32 * m, lane);
+#pragma unroll
+      for (int n = 0; n < TN; n++)
+        b[p][n] = tr_operand<SB::PITCH>(cur + 3 * SA::PLANE + p * SB::PLANE, wn0 + 32 * n, lane);
+    }
+#pragma unroll
+    for (int m = 0; m < TM; m++)
+#pragma unroll
+      for (int n = 0; n < TN; n++) {
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b[0][n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[1][n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[2][n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[0][n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[1][n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[0][n], acc[m][n], 0, 0, 0);
+      }
+    if (more) {
+      sa.store(nxt, tid);
+      sb.store(nxt + 3 * SA::PLANE, tid);
+    }
+    __syncthreads();
+  }
+  // epilogue: acc register q of a 32x32 tile is row (q & 3) + 8 (q >> 2) + 4h, column i
+  float* Cs = w.C + (int64_t)slice * w.cstride;
+#pragma unroll
+  for (int n = 0; n < TN; n++) {
+    const int col = n0 + wn0 + 32 * n + i;
+    if (col >= w.N) continue;
+#pragma unroll
+    for (int m = 0; m < TM; m++)
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int row = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (row < w.M) Cs[(int64_t)row * w.ldc + col] = acc[m][n][q];
+      }
+  }
+}
+
+template <int WGM, int WGN, int TM, int TN>
+int launch_wgrad_tr(WgradArgs w, hipStream_t s) {
+  constexpr int BM = 32 * TM * WGM, BN = 32 * TN * WGN;
+  w.tiles_n = (w.N + BN - 1) / BN;
+  w.tiles = (int64_t)((w.M + BM - 1) / BM) * w.tiles_n;
+  if (w.tiles * w.slices > 0x7fffffff) return HG_ERR_ARG;
+  hipLaunchKernelGGL((k_wgrad_tr<WGM, WGN, TM, TN>), dim3((unsigned)(w.tiles * w.slices)), dim3(64 * WGM * WGN), 0, s, w);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+constexpr int WGRAD_TR0 = 40, WGRAD_TR1 = 48;  // tile ids of k_wgrad_tr (hg_gemm_f32_wgrad only)
+
 }  // namespace
 
 extern "C" int64_t hg_gemm_x6_image_bytes(int64_t rows, int64_t K) {
@@ -1035,17 +1244,33 @@ extern "C" int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B
 extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                                  int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile,
                                  void* stream) {
-  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || slices < 1 || tile < 19 || tile > NTILES ||
-      K > 0x7fffffff || (kmajor != 0 && kmajor != 1))
+  const bool tr = tile >= WGRAD_TR0 && tile <= WGRAD_TR1;
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || slices < 1 || (!tr && (tile < 19 || tile > NTILES)) ||
+      K > 0x7fffffff || (kmajor != 0 && kmajor != 1) || (tr && (kmajor != 0 || M > 0x7fffffff)))
     return HG_ERR_ARG;
   if (kmajor == 0 && (lda < M || ldb < N)) return HG_ERR_ARG;
   if (kmajor == 1 && (lda < K || ldb < K)) return HG_ERR_ARG;
   if (slices > 1 && cstride < M * (int64_t)ldc) return HG_ERR_ARG;
   if ((uintptr_t)A % 4 || (uintptr_t)B % 4 || (uintptr_t)C % 4) return HG_ERR_ARG;
-  GemmArgs g{A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, nullptr, M, N, (int)K, 0, 0};
   const int64_t kslice = ((K + slices - 1) / slices + 15) & ~(int64_t)15;
-  GemmX6Args xa{g, kslice, cstride, slices};
   hipStream_t s = (hipStream_t)stream;
+  if (tr) {
+    // tiles 40..48: k_wgrad_tr <WGM, WGN, TM, TN> (row-major operands, transposed LDS reads)
+    WgradArgs w{A, lda, B, ldb, C, ldc, cstride, (int)M, N, K, kslice, slices, 0, 0};
+    switch (tile) {
+      case 40: return launch_wgrad_tr<4, 2, 2, 3>(w, s);  // 256 x 192, 8 waves
+      case 41: return launch_wgrad_tr<4, 2, 2, 2>(w, s);  // 256 x 128, 8 waves
+      case 42: return launch_wgrad_tr<2, 2, 2, 2>(w, s);  // 128 x 128, 4 waves
+      case 43: return launch_wgrad_tr<2, 4, 2, 2>(w, s);  // 128 x 256, 8 waves
+      case 44: return launch_wgrad_tr<2, 2, 2, 3>(w, s);  // 128 x 192, 4 waves
+      case 45: return launch_wgrad_tr<4, 2, 1, 2>(w, s);  // 128 x 128, 8 waves
+      case 46: return launch_wgrad_tr<2, 2, 1, 1>(w, s);  // 64 x 64, 4 waves
+      case 47: return launch_wgrad_tr<2, 2, 1, 2>(w, s);  // 64 x 128, 4 waves
+      default: return launch_wgrad_tr<2, 2, 2, 1>(w, s);  // 48: 128 x 64, 4 waves
+    }
+  }
+  GemmArgs g{A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, nullptr, M, N, (int)K, 0, 0};
+  GemmX6Args xa{g, kslice, cstride, slices};
   const int md = kmajor ? 4 : 2;
   const bool vec = kmajor && lda % 4 == 0 && ldb % 4 == 0 && (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
   switch (tile) {
