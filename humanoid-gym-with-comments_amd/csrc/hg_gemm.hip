@@ -996,7 +996,7 @@ __device__ __forceinline__ bf16x8 tr_operand(const char* __restrict__ plane, int
   return __builtin_bit_cast(bf16x8, e);
 }
 
-template <int WGM, int WGN, int TM, int TN>
+template <int WGM, int WGN, int TM, int TN, int PF>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_wgrad_tr(WgradArgs w) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int BM = 32 * TM * WGM, BN = 32 * TN * WGN;
@@ -1025,23 +1025,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_wgrad_tr(WgradArgs w) {
 #pragma unroll
     for (int n = 0; n < TN; n++) acc[m][n] = (f32x16)0.f;
 
-  SA sa;
-  SB sb;
-  if (nchunks > 0) {
-    sa.load(w.A, w.lda, kbeg, kend, m0, w.M, tid);
-    sb.load(w.B, w.ldb, kbeg, kend, n0, w.N, tid);
-    sa.store(lds, tid);
-    sb.store(lds + 3 * SA::PLANE, tid);
-  }
-  __syncthreads();
-  for (int c = 0; c < nchunks; c++) {
+  // one chunk: the global loads of chunk c + PF into (la, lb), the MFMAs on stage c & 1, the split
+  // + LDS store of chunk c + 1 from (ha, hb) into the other stage, one barrier
+  auto step = [&](int c, SA& la, SB& lb, const SA& ha, const SB& hb) {
     const char* cur = lds + (c & 1) * STAGE;
     char* nxt = lds + ((c + 1) & 1) * STAGE;
-    const bool more = c + 1 < nchunks;
-    if (more) {
-      const int64_t r0 = kbeg + (int64_t)(c + 1) * 16;
-      sa.load(w.A, w.lda, r0, kend, m0, w.M, tid);
-      sb.load(w.B, w.ldb, r0, kend, n0, w.N, tid);
+    if (c + PF < nchunks) {
+      const int64_t r0 = kbeg + (int64_t)(c + PF) * 16;
+      la.load(w.A, w.lda, r0, kend, m0, w.M, tid);
+      lb.load(w.B, w.ldb, r0, kend, n0, w.N, tid);
     }
     bf16x8 a[3][TM], b[3][TN];
 #pragma unroll
@@ -1063,11 +1055,33 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_wgrad_tr(WgradArgs w) {
         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[1][n], acc[m][n], 0, 0, 0);
         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[0][n], acc[m][n], 0, 0, 0);
       }
-    if (more) {
-      sa.store(nxt, tid);
-      sb.store(nxt + 3 * SA::PLANE, tid);
+    if (c + 1 < nchunks) {
+      ha.store(nxt, tid);
+      hb.store(nxt + 3 * SA::PLANE, tid);
     }
     __syncthreads();
+  };
+  SA sa0, sa1;
+  SB sb0, sb1;
+  if (nchunks > 0) {
+    sa0.load(w.A, w.lda, kbeg, kend, m0, w.M, tid);
+    sb0.load(w.B, w.ldb, kbeg, kend, n0, w.N, tid);
+    sa0.store(lds, tid);
+    sb0.store(lds + 3 * SA::PLANE, tid);
+    if (PF == 2 && nchunks > 1) {
+      sa1.load(w.A, w.lda, kbeg + 16, kend, m0, w.M, tid);
+      sb1.load(w.B, w.ldb, kbeg + 16, kend, n0, w.N, tid);
+    }
+  }
+  __syncthreads();
+  if (PF == 1) {
+    for (int c = 0; c < nchunks; c++) step(c, sa0, sb0, sa0, sb0);
+  } else {
+    // two register sets: chunk c + 1 waits in one while chunk c + 2 loads into the other
+    for (int c = 0; c < nchunks; c += 2) {
+      step(c, sa0, sb0, sa1, sb1);
+      if (c + 1 < nchunks) step(c + 1, sa1, sb1, sa0, sb0);
+    }
   }
   // epilogue: acc register q of a 32x32 tile is row (q & 3) + 8 (q >> 2) + 4h, column i
   float* Cs = w.C + (int64_t)slice * w.cstride;
@@ -1085,17 +1099,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_wgrad_tr(WgradArgs w) {
   }
 }
 
-template <int WGM, int WGN, int TM, int TN>
+template <int WGM, int WGN, int TM, int TN, int PF = 1>
 int launch_wgrad_tr(WgradArgs w, hipStream_t s) {
   constexpr int BM = 32 * TM * WGM, BN = 32 * TN * WGN;
   w.tiles_n = (w.N + BN - 1) / BN;
   w.tiles = (int64_t)((w.M + BM - 1) / BM) * w.tiles_n;
   if (w.tiles * w.slices > 0x7fffffff) return HG_ERR_ARG;
-  hipLaunchKernelGGL((k_wgrad_tr<WGM, WGN, TM, TN>), dim3((unsigned)(w.tiles * w.slices)), dim3(64 * WGM * WGN), 0, s, w);
+  hipLaunchKernelGGL((k_wgrad_tr<WGM, WGN, TM, TN, PF>), dim3((unsigned)(w.tiles * w.slices)), dim3(64 * WGM * WGN), 0, s, w);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-constexpr int WGRAD_TR0 = 40, WGRAD_TR1 = 48;  // tile ids of k_wgrad_tr (hg_gemm_f32_wgrad only)
+constexpr int WGRAD_TR0 = 40, WGRAD_TR1 = 54;  // tile ids of k_wgrad_tr (hg_gemm_f32_wgrad only)
 
 }  // namespace
 
@@ -1255,7 +1269,7 @@ extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, in
   const int64_t kslice = ((K + slices - 1) / slices + 15) & ~(int64_t)15;
   hipStream_t s = (hipStream_t)stream;
   if (tr) {
-    // tiles 40..48: k_wgrad_tr <WGM, WGN, TM, TN> (row-major operands, transposed LDS reads)
+    // tiles 40..54: k_wgrad_tr <WGM, WGN, TM, TN, PF> (row-major operands, transposed LDS reads)
     WgradArgs w{A, lda, B, ldb, C, ldc, cstride, (int)M, N, K, kslice, slices, 0, 0};
     switch (tile) {
       case 40: return launch_wgrad_tr<4, 2, 2, 3>(w, s);  // 256 x 192, 8 waves
@@ -1266,7 +1280,14 @@ extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, in
       case 45: return launch_wgrad_tr<4, 2, 1, 2>(w, s);  // 128 x 128, 8 waves
       case 46: return launch_wgrad_tr<2, 2, 1, 1>(w, s);  // 64 x 64, 4 waves
       case 47: return launch_wgrad_tr<2, 2, 1, 2>(w, s);  // 64 x 128, 4 waves
-      default: return launch_wgrad_tr<2, 2, 2, 1>(w, s);  // 48: 128 x 64, 4 waves
+      case 48: return launch_wgrad_tr<2, 2, 2, 1>(w, s);  // 128 x 64, 4 waves
+      // the same tiles with the global loads two chunks ahead (two register sets)
+      case 49: return launch_wgrad_tr<4, 2, 2, 3, 2>(w, s);
+      case 50: return launch_wgrad_tr<4, 2, 2, 2, 2>(w, s);
+      case 51: return launch_wgrad_tr<2, 2, 2, 2, 2>(w, s);
+      case 52: return launch_wgrad_tr<2, 2, 1, 1, 2>(w, s);
+      case 53: return launch_wgrad_tr<2, 2, 1, 2, 2>(w, s);
+      default: return launch_wgrad_tr<4, 2, 1, 2, 2>(w, s);  // 54
     }
   }
   GemmArgs g{A, lda, B, ldb, nullptr, nullptr, 0, C, ldc, nullptr, M, N, (int)K, 0, 0};

@@ -143,6 +143,7 @@ def _skinny_backward_act(g, h, W, red):
     return wb[: n * k].view(n, k), wb[n * k:], gh_prev, gb_prev
 
 
+_BIG_ROWS = 1 << 40
 # Split-K factors for the weight gradients dW[n, k] = gh[R, n]^T x[R, k] at the 24576-row
 # minibatch: the reduction over R is cut into S row chunks computed as one batched GEMM; the chunk
 # sum runs in the batched end-of-backward column-sum launch.  Small outputs (128 x 256, 256 x 512,
@@ -159,10 +160,20 @@ _DW_SPLIT = {(128, 256): 32, (128, 128): 16, (256, 512): 4, (128, 705): 8, (512,
              (256, 768): 4}
 
 
-# Weight gradients on the bf16-split GEMM (hg_gemm_f32_wgrad, the row-major gh and x staged
-# through an LDS transpose): (n, k) -> [(max rows, tile, split-K slices)], first entry whose row
-# bound covers the call; the slices are summed in the batched end-of-backward column-sum launch.
-_GEMM_DW = {}
+# Weight gradients on the bf16-split GEMM with LDS transpose reads (hg_gemm_f32_wgrad tiles 40..54,
+# k_wgrad_tr: the row-major gh and x staged as they lie, read back with ds_read_b64_tr_b16):
+# (n, k) -> [(max rows, (tile, split-K slices))], first entry whose row bound covers the call
+# ((tile, S) = 0: the hipBLASLt route below); the slices are summed in the batched end-of-backward
+# column-sum launch.  Measured on MI355X per shape at 24576 rows (scripts/wgrad_tr_probe.py,
+# profiles/r4_gemm/wgrad_tr_probe.jsonl; kernel us + the slices' share of the column sums) against
+# the hipBLASLt kernels the runner's TunableOp table runs in the update (the traced minibatch,
+# profiles/r4_v1): actor 512x705 147.8 -> 106 + ~8 (tile 49: 256 x 192, loads two chunks ahead,
+# 32 slices), critic 256x768 76.6 -> 60 + ~8 (tile 49, 64 slices); the other products measured
+# within a few us of hipBLASLt or slower (768x219 70.5 vs 64 + 10, 256x512 50.9 vs 43 + 6,
+# 128x705 42.5 vs 39 + 6, 128x256 / 128x128 16.5 / 13.8 vs 17 + 7 / 12 + 6) and stay there.
+WGRAD_TR = os.environ.get("HG_WGRAD_TR", "1") != "0"
+_GEMM_DW = {(512, 705): [(8191, 0), (_BIG_ROWS, (49, 32))],
+            (256, 768): [(8191, 0), (_BIG_ROWS, (49, 64))]} if WGRAD_TR else {}
 
 
 def _weight_grad(gh, x, red=None):

@@ -20,7 +20,7 @@ dev = "cuda:0"
 R = int(os.environ.get("WG_ROWS", "24576"))
 SHAPES = [tuple(int(v) for v in s.split("x")) for s in os.environ.get("WG_SHAPES", "").split(",") if s] or \
     [(512, 705), (256, 512), (128, 256), (768, 219), (256, 768), (128, 705), (128, 128)]
-TILES = [int(v) for v in os.environ.get("WG_TILES", "40,41,42,43,44,45,46,47,48").split(",")]
+TILES = [int(v) for v in os.environ.get("WG_TILES", "40,41,42,43,44,45,46,47,48,49,50,51,52,53,54").split(",")]
 SPLITS = [int(v) for v in os.environ.get("WG_SPLITS", "8,16,24,32,48,64,96,128").split(",")]
 
 

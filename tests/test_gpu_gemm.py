@@ -107,7 +107,8 @@ def test_gemm_input_grad_matches_fp64(rows, kr, n):
 
 
 # (rows = reduction, n, k, slices): weight gradients dW [n, k] = gh^T x, split-K slices summed here
-WG_CASES = [(24576, 512, 705, 4), (777, 128, 219, 3), (33, 5, 7, 1), (100, 130, 66, 2), (4096, 256, 512, 16)]
+WG_CASES = [(24576, 512, 705, 4), (777, 128, 219, 3), (33, 5, 7, 1), (100, 130, 66, 2), (4096, 256, 512, 16),
+            (24576, 768, 219, 32), (250, 64, 300, 40)]
 
 
 @pytest.mark.parametrize("rows,n,k,S", WG_CASES)
@@ -132,6 +133,20 @@ def test_gemm_wgrad_matches_fp64(rows, n, k, S):
             err = (dw - ref).abs()
             assert (err <= bound).all(), f"kmajor {kmajor} tile {tile}: worst ratio {(err / bound).max().item():.3f}"
             assert (part[:, :, k:] == 5.0).all()
+    # k_wgrad_tr (tiles 40..54: row-major operands through LDS transpose reads), with x a column
+    # slice of a wider table (row stride not a multiple of 4: unaligned 16-byte row segments)
+    wide = torch.randn(rows, k + 19, device=dev)
+    xs = wide[:, 3:3 + k]
+    xs.copy_(x)
+    for tile in range(40, 55):
+        part = torch.full((S, n, k + 2), 5.0, device=dev)
+        rc = L.hg_gemm_f32_wgrad(gh.data_ptr(), gh.stride(0), xs.data_ptr(), xs.stride(0), part.data_ptr(), k + 2,
+                                 n * (k + 2), n, k, rows, S, 0, tile, _stream())
+        assert rc == 0
+        dw = part[:, :, :k].double().sum(0)
+        err = (dw - ref).abs()
+        assert (err <= bound).all(), f"tr tile {tile}: worst ratio {(err / bound).max().item():.3f}"
+        assert (part[:, :, k:] == 5.0).all()
 
 
 def _image(L, P, trans, rows, k):
@@ -256,6 +271,15 @@ def test_gemm_rejects_bad_arguments():
     a[0], a[4] = 1, 4
     a[1], a[2], a[13] = x.data_ptr(), 16, 16
     assert L.hg_gemm_f32(*a) != 0
+    # weight gradients: the transposed-read tiles take row-major (kmajor 0) operands only, and tile
+    # ids outside 19..28 / 40..54 are refused
+    part = torch.empty(4, 16, device="cuda:0")
+    wg = [x.data_ptr(), 4, y.data_ptr(), 4, part.data_ptr(), 16, 0, 4, 4, 8, 1, 0, 40, _stream()]
+    assert L.hg_gemm_f32_wgrad(*wg) == 0
+    for i, bad in ((11, 1), (12, 29), (12, 39), (12, 55), (10, 0)):
+        a = list(wg)
+        a[i] = bad
+        assert L.hg_gemm_f32_wgrad(*a) != 0
     torch.cuda.synchronize()
 
 
