@@ -1328,9 +1328,18 @@ def test_deferred_mlp_reductions_match():
     finally:
         hg_mlp.DEFER_REDUCTIONS = True
     assert g_d.keys() == g_i.keys() == g_t.keys()
+    # the deferred path routes the weight gradients in hg_mlp._GEMM_DW to the bf16-split k_wgrad_tr
+    # (its split-K slices need the batched column sums), the immediate path keeps hipBLASLt: those
+    # two differ by the split's error (<= 4e-8 of sum |gh||x| per element, tests/test_gpu_gemm.py)
+    # on top of the summation order, so they are held to a relative Frobenius bound instead
+    tr_routed = {n for n, p in ac.named_parameters() if tuple(p.shape) in hg_mlp._GEMM_DW}
     for n in g_d:
         if n.endswith("bias"):
             assert torch.equal(g_d[n], g_i[n]), n
+        elif n in tr_routed:
+            rel = float((g_d[n] - g_i[n]).norm() / g_i[n].norm())
+            assert rel <= 2e-6, (n, rel)
+            torch.testing.assert_close(g_d[n], g_i[n], rtol=1e-4, atol=1e-4, msg=lambda m: f"{n}: {m}")
         else:
             torch.testing.assert_close(g_d[n], g_i[n], rtol=1e-5, atol=1e-5, msg=lambda m: f"{n}: {m}")
         torch.testing.assert_close(g_d[n], g_t[n], rtol=2e-4, atol=2e-4, msg=lambda m: f"{n}: {m}")
