@@ -174,6 +174,12 @@ _DW_SPLIT = {(128, 256): 32, (128, 128): 16, (256, 512): 4, (128, 705): 8, (512,
 WGRAD_TR = os.environ.get("HG_WGRAD_TR", "1") != "0"
 _GEMM_DW = {(512, 705): [(8191, 0), (_BIG_ROWS, (49, 32))],
             (256, 768): [(8191, 0), (_BIG_ROWS, (49, 64))]} if WGRAD_TR else {}
+if os.environ.get("HG_WGRAD_TR") == "all":  # every weight gradient of the three networks
+    _GEMM_DW.update({(256, 512): [(8191, 0), (_BIG_ROWS, (54, 64))],
+                     (768, 219): [(8191, 0), (_BIG_ROWS, (54, 64))],
+                     (128, 705): [(8191, 0), (_BIG_ROWS, (48, 64))],
+                     (128, 256): [(8191, 0), (_BIG_ROWS, (54, 128))],
+                     (128, 128): [(8191, 0), (_BIG_ROWS, (46, 128))]})
 
 
 def _weight_grad(gh, x, red=None):

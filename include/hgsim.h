@@ -443,7 +443,9 @@ int hg_cast_bf16_jobs(const float* const* src, uint16_t* const* dst, const int64
 /* Batched column sums (the deferred reductions of one MLP backward in one launch: bias-gradient
  * tile partials and split-K weight-gradient chunks, replacing per-layer grad.sum(0) launches):
  * dst[j][c] = sum over p < parts[j] of src[j][p * width[j] + c], fixed order, for j < njobs <= 16.
- * parts > 16 uses hg_mlp_act_backward's own final reduction (identical bits). */
+ * parts > 16 uses hg_mlp_act_backward's own final reduction (identical bits), except on wide jobs
+ * (width >= 4096, a multiple of 4, 16-byte aligned: the split-K slices), which sum part p into
+ * accumulator p % 8 and combine the eight as a fixed tree (parts <= 16: p = 0 .. parts-1 in order). */
 int hg_colsum_jobs(const float* const* src, float* const* dst, const int64_t* width, const int* parts, int njobs,
                    void* stream);
 
