@@ -651,17 +651,32 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const KinLane K = kin_scan(E, M, l, gz, true);
     rnea_scan(E, M, l, K, scale0);
     __syncthreads();
-    // base totals (lane 0) — read the kinematics scratch before M overwrites it
-    if (l == 0) {
-      f3 f0 = ld3(E.u.kin.f[0]) + ld3(E.u.kin.f[1]) + ld3(E.u.kin.f[7]);
-      f3 n0 = ld3(E.u.kin.n[0]) + ld3(E.u.kin.n[1]) + cross(ld3(E.o[1]), ld3(E.u.kin.f[1])) + ld3(E.u.kin.n[7]) +
-              cross(ld3(E.o[7]), ld3(E.u.kin.f[7]));
-      E.h[0] = f0.x; E.h[1] = f0.y; E.h[2] = f0.z; E.h[3] = n0.x; E.h[4] = n0.y; E.h[5] = n0.z;
-      E.base_cm = E.cm[0] + E.cm[1] + E.cm[7];
-      f3 s = ld3(E.cs[0]) + ld3(E.cs[1]) + ld3(E.cs[7]);
-      st3(E.base_cs, s);
-#pragma unroll
-      for (int i = 0; i < 6; i++) E.base_cJ[i] = E.cJ[0][i] + E.cJ[1][i] + E.cJ[7][i];
+    // base totals (lane 0) — read the kinematics scratch before M overwrites it.  One total per
+    // lane (16 lanes: h 0..5, base_cm, base_cs 0..2, base_cJ 0..5), each with the operations and
+    // order of the serial form (f3 sums and cross products component by component): every LDS
+    // read of the phase is issued at once instead of lane 0's chain of 16 round trips
+    {
+      const int t = l < 16 ? l : 15;
+      const int c = t < 3 ? t : (t < 6 ? t - 3 : (t >= 7 && t < 10 ? t - 7 : 0));
+      const int c1 = c == 2 ? 0 : c + 1, c2 = c == 0 ? 2 : c - 1;  // cross component c = a[c1] b[c2] - a[c2] b[c1]
+      const int j = t >= 10 ? t - 10 : 0;
+      // rows of the three base-side links' arrays this lane sums: f (t < 3), n + o x f (3..5),
+      // cm (6), cs (7..9), cJ (10..15)
+      const float* src = t < 3 ? &E.u.kin.f[0][0] : (t < 6 ? &E.u.kin.n[0][0] : (t == 6 ? E.cm : (t < 10 ? &E.cs[0][0] : &E.cJ[0][0])));
+      const int pitch = t == 6 ? 1 : (t < 10 ? 3 : 6), col = t == 6 ? 0 : (t < 10 ? c : j);
+      float v0 = src[0 * pitch + col], v1 = src[1 * pitch + col], v7 = src[7 * pitch + col];
+      const float o1a = E.o[1][c1], o1b = E.o[1][c2], o7a = E.o[7][c1], o7b = E.o[7][c2];
+      const float f1a = E.u.kin.f[1][c1], f1b = E.u.kin.f[1][c2], f7a = E.u.kin.f[7][c1], f7b = E.u.kin.f[7][c2];
+      pin(v0); pin(v1); pin(v7);
+      float r = v0 + v1;
+      if (t >= 3 && t < 6) {
+        const float x1 = o1a * f1b - o1b * f1a, x7 = o7a * f7b - o7b * f7a;
+        r = ((r + x1) + v7) + x7;
+      } else {
+        r = r + v7;
+      }
+      float* dst = t < 6 ? &E.h[t] : (t == 6 ? &E.base_cm : (t < 10 ? &E.base_cs[t - 7] : &E.base_cJ[j]));
+      if (l < 16) *dst = r;
     }
     __syncthreads();
     // ---- A6/A7: M written straight into the factor's legs-first lower triangle (index i <-> dof
@@ -690,8 +705,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       A[12][i] = F.x; A[13][i] = F.y; A[14][i] = F.z;
       A[15][i] = Lm.x; A[16][i] = Lm.y; A[17][i] = Lm.z;
       const int first = b <= 6 ? 1 : 7;
-      for (int kb = b; kb >= first; kb--) A[i][kb - 1] = dot(ld3(E.a[kb]), Lm - cross(ld3(E.o[kb]), F));
-      A[i][i] += E.madd[b - 1];
+      // the ancestors kb = b, b - 1, .. first as six predicated slots with every LDS read issued
+      // up front (the variable-trip loop waited one round trip per ancestor); a slot past the
+      // leg's root stores into the row's unused padding column 19
+      const float madd = E.madd[b - 1];
+      f3 ak[6], ok[6];
+#pragma unroll
+      for (int m = 0; m < 6; m++) {
+        const int kc = b - m >= first ? b - m : b;
+        ak[m] = ld3(E.a[kc]);
+        ok[m] = ld3(E.o[kc]);
+        pin(ak[m]);
+        pin(ok[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < 6; m++) {
+        const int kb = b - m;
+        const float val = dot(ak[m], Lm - cross(ok[m], F));
+        A[i][kb >= first ? kb - 1 : 19] = kb == b ? val + madd : val;
+      }
     }
     __syncthreads();
     // ---- A8: Cholesky in registers, legs-first order: M's arrow structure gives L no
