@@ -174,12 +174,16 @@ _DW_SPLIT = {(128, 256): 32, (128, 128): 16, (256, 512): 4, (128, 705): 8, (512,
 WGRAD_TR = os.environ.get("HG_WGRAD_TR", "1") != "0"
 _GEMM_DW = {(512, 705): [(8191, 0), (_BIG_ROWS, (49, 32))],
             (256, 768): [(8191, 0), (_BIG_ROWS, (49, 64))]} if WGRAD_TR else {}
-if os.environ.get("HG_WGRAD_TR") == "all":  # every weight gradient of the three networks
-    _GEMM_DW.update({(256, 512): [(8191, 0), (_BIG_ROWS, (54, 64))],
-                     (768, 219): [(8191, 0), (_BIG_ROWS, (54, 64))],
-                     (128, 705): [(8191, 0), (_BIG_ROWS, (48, 64))],
-                     (128, 256): [(8191, 0), (_BIG_ROWS, (54, 128))],
-                     (128, 128): [(8191, 0), (_BIG_ROWS, (46, 128))]})
+# the other products' best tr tiles (probe); HG_WGRAD_TR=all routes all of them, a list such as
+# "256x512,128x705" only those: measured 0.25 ms per iteration slower for "all" on one box
+# (profiles/r4_ab), so none is routed by default
+_GEMM_DW_EXTRA = {(256, 512): (54, 64), (768, 219): (54, 64), (128, 705): (48, 64), (128, 256): (54, 128),
+                  (128, 128): (46, 128)}
+_sel = os.environ.get("HG_WGRAD_TR", "1")
+if _sel not in ("0", "1"):
+    for _shape, _route_tr in _GEMM_DW_EXTRA.items():
+        if _sel == "all" or "%dx%d" % _shape in _sel.split(","):
+            _GEMM_DW[_shape] = [(8191, 0), (_BIG_ROWS, _route_tr)]
 
 
 def _weight_grad(gh, x, red=None):
