@@ -39,8 +39,18 @@ __device__ inline void store_obs<float>(float* dst, float v) { *dst = v; }
 template <>
 __device__ inline void store_obs<__half>(__half* dst, float v) { *dst = __float2half(v); }
 
-template <typename OT>
-__global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, const float* __restrict__ std,
+// the fused output layer (hg_rollout_act_head): HEAD_N outputs over HEAD_K = 128 inputs, lane j of
+// an env's 16-lane group holding inputs 8j .. 8j + 7 (k_skinny_fwd's layout and arithmetic)
+constexpr int HEAD_N = 12, HEAD_K = 128;
+struct ActHead {
+  const float* h;
+  int64_t ld;
+  const float* W;
+  const float* b;
+};
+
+template <typename OT, bool HEAD>
+__global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, ActHead hd, const float* __restrict__ std,
                                             const float* __restrict__ value, const float* __restrict__ obs,
                                             const float* __restrict__ cobs, int n, int A, int64_t obs_w,
                                             int64_t cobs_w, int64_t obs_ld, int64_t obs_c0, int64_t cobs_ld,
@@ -59,11 +69,36 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, con
       const int j = threadIdx.x % ACT_LANES;
       if (e >= n) return;  // whole groups leave together
       float term = 0.f;
+      float mh = 0.f;
+      if (HEAD) {
+        // mean of row e = W h_e + b, as k_skinny_fwd<12> computes it (same fma chain, the same
+        // xor-shuffle tree, the bias added last), so bitwise the two-launch result
+        const int k0 = 8 * j;
+        const float4 xa = *reinterpret_cast<const float4*>(hd.h + (int64_t)e * hd.ld + k0);
+        const float4 xb = *reinterpret_cast<const float4*>(hd.h + (int64_t)e * hd.ld + k0 + 4);
+        const float v[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+        float out = 0.f;
+#pragma unroll
+        for (int q = 0; q < HEAD_N; q++) {
+          const float4 wa = *reinterpret_cast<const float4*>(hd.W + q * HEAD_K + k0);
+          const float4 wb = *reinterpret_cast<const float4*>(hd.W + q * HEAD_K + k0 + 4);
+          const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; i++) s = fmaf(v[i], w[i], s);
+          s += __shfl_xor(s, 8, 16);
+          s += __shfl_xor(s, 4, 16);
+          s += __shfl_xor(s, 2, 16);
+          s += __shfl_xor(s, 1, 16);
+          out = (j == q) ? s : out;
+        }
+        mh = out + (j < HEAD_N ? hd.b[j] : 0.f);
+      }
       if (j < A) {
         float z4[4];
         normals4(philox_key(seed, (uint32_t)(e + row_offset), counter, (uint32_t)(j >> 2)), z4);
         const float z = (j & 3) == 0 ? z4[0] : (j & 3) == 1 ? z4[1] : (j & 3) == 2 ? z4[2] : z4[3];
-        const float m = mean[(size_t)e * A + j], s = std[j];
+        const float m = HEAD ? mh : mean[(size_t)e * A + j], s = std[j];
         const float a = m + s * z;
         const float d = a - m;
         term = -(d * d) / (2.0f * (s * s)) - logf(s) - c;
@@ -135,13 +170,13 @@ __global__ void __launch_bounds__(TPB) k_env(const float* __restrict__ rew, cons
 
 }  // namespace
 
-extern "C" int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
-                              const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
-                              int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
-                              float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
-                              void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
-                              uint64_t seed, uint64_t counter, void* stream) {
-  if (!mean || !std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out ||
+namespace {
+int launch_act(const float* mean, ActHead hd, const float* std, const float* value, const float* obs,
+               const float* critic_obs, int num_envs, int num_actions, int64_t obs_width, int64_t critic_obs_width,
+               int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld, float* actions_out, float* logp_out,
+               float* mu_out, float* sigma_out, float* value_out, void* obs_out, int64_t obs_out_ld,
+               void* critic_obs_out, int obs_fp16, int row_offset, uint64_t seed, uint64_t counter, void* stream) {
+  if ((!mean && !hd.h) || !std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out ||
       !obs_out || num_envs <= 0 || num_actions <= 0 || num_actions > 64 || obs_width <= 0 || obs_col0 < 0 ||
       (obs_out_ld != 0 && obs_out_ld < obs_width) ||
       obs_ld < obs_col0 + obs_width || (critic_obs_width > 0 && (!critic_obs || !critic_obs_out ||
@@ -154,17 +189,49 @@ extern "C" int hg_rollout_act(const float* mean, const float* std, const float* 
   const int64_t cw = critic_obs_width > 0 ? critic_obs_width : 0;
   const int64_t old = obs_out_ld ? obs_out_ld : obs_width;
   hipStream_t s = (hipStream_t)stream;
-  if (obs_fp16)
-    hipLaunchKernelGGL(k_act<__half>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
-                       critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, critic_obs_ld,
-                       actions_out, logp_out, mu_out, sigma_out, value_out, old, (__half*)obs_out,
-                       (__half*)critic_obs_out, row_offset, seed, counter, env_blocks);
-  else
-    hipLaunchKernelGGL(k_act<float>, dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, std, value, obs,
-                       critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, critic_obs_ld,
-                       actions_out, logp_out, mu_out, sigma_out, value_out, old, (float*)obs_out, (float*)critic_obs_out,
-                       row_offset, seed, counter, env_blocks);
+#define HG_ACT(OT, H) hipLaunchKernelGGL((k_act<OT, H>), dim3(env_blocks + copy_blocks), dim3(TPB), 0, s, mean, hd, std,  \
+                                         value, obs, critic_obs, num_envs, num_actions, obs_width, cw, obs_ld, obs_col0, \
+                                         critic_obs_ld, actions_out, logp_out, mu_out, sigma_out, value_out, old,       \
+                                         (OT*)obs_out, (OT*)critic_obs_out, row_offset, seed, counter, env_blocks)
+  const bool head = hd.h != nullptr;
+  if (obs_fp16) {
+    if (head) HG_ACT(__half, true);
+    else HG_ACT(__half, false);
+  } else {
+    if (head) HG_ACT(float, true);
+    else HG_ACT(float, false);
+  }
+#undef HG_ACT
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+}  // namespace
+
+extern "C" int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
+                              const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
+                              int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
+                              float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
+                              void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
+                              uint64_t seed, uint64_t counter, void* stream) {
+  if (!mean) return HG_ERR_ARG;
+  return launch_act(mean, ActHead{nullptr, 0, nullptr, nullptr}, std, value, obs, critic_obs, num_envs, num_actions,
+                    obs_width, critic_obs_width, obs_ld, obs_col0, critic_obs_ld, actions_out, logp_out, mu_out,
+                    sigma_out, value_out, obs_out, obs_out_ld, critic_obs_out, obs_fp16, row_offset, seed, counter,
+                    stream);
+}
+
+extern "C" int hg_rollout_act_head(const float* h, int64_t h_ld, const float* W, const float* b, int head_k,
+                                   const float* std, const float* value, const float* obs, const float* critic_obs,
+                                   int num_envs, int num_actions, int64_t obs_width, int64_t critic_obs_width,
+                                   int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld, float* actions_out,
+                                   float* logp_out, float* mu_out, float* sigma_out, float* value_out, void* obs_out,
+                                   int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
+                                   uint64_t seed, uint64_t counter, void* stream) {
+  if (!h || !W || !b || num_actions != HEAD_N || head_k != HEAD_K || h_ld < HEAD_K || h_ld % 4 != 0 ||
+      (uintptr_t)h % 16 != 0 || (uintptr_t)W % 16 != 0)
+    return HG_ERR_ARG;
+  return launch_act(nullptr, ActHead{h, h_ld, W, b}, std, value, obs, critic_obs, num_envs, num_actions, obs_width,
+                    critic_obs_width, obs_ld, obs_col0, critic_obs_ld, actions_out, logp_out, mu_out, sigma_out,
+                    value_out, obs_out, obs_out_ld, critic_obs_out, obs_fp16, row_offset, seed, counter, stream);
 }
 
 extern "C" int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs,

@@ -563,6 +563,31 @@ def mlp_forward(net, x):
     return _MLP.apply(x, *_params(net))
 
 
+def mlp_infer_hidden(net, x):
+    """mlp_infer's hidden layers only: the last hidden activation, for callers that fuse the output
+    layer into their own launch (hg_rollout_act_head); None when ``net`` is not fusable."""
+    if not fusable(net):
+        return None
+    mods = list(net)
+    params = _params(net)
+    fimg = _forward_images(params, len(params) // 2, x.shape[0], x.device, False)[0]
+    h = x
+    for j in range(0, len(mods) - 1, 2):
+        lin = mods[j]
+        if isinstance(mods[j + 1], nn.ELU) and mods[j + 1].alpha == 1.0 and not mods[j + 1].inplace:
+            h = _hidden_forward(h, lin.weight, lin.bias, fimg, j // 2)
+        else:
+            h = mods[j + 1](lin(h))
+    return h
+
+
+def head_fusable(h, W):
+    """The output layer W applied to h can run inside hg_rollout_act_head (12 x 128, aligned rows)."""
+    return (h is not None and tuple(W.shape) == (12, 128) and W.is_contiguous() and h.dim() == 2
+            and h.dtype == torch.float32 and h.stride(1) == 1 and h.stride(0) % 4 == 0 and h.data_ptr() % 16 == 0
+            and W.data_ptr() % 16 == 0)
+
+
 def mlp_infer(net, x, out=None):
     """net(x) without autograd (rollout inference): hidden layers on the LDS-staged GEMM or the
     register-operand fused kernel where ``_GEMM_FWD`` / ``_FUSED_FWD_ROWS`` route them, torch's

@@ -32,6 +32,9 @@ from . import hg_mlp
 from .hg_loss import ppo_loss
 from .rollout_storage import RolloutStorage, gather_rows
 
+# the actor's 12 x 128 output layer fused into the rollout's sampling launch (hg_rollout_act_head)
+HEAD_FUSED = os.environ.get("HG_HEAD_FUSED", "1") != "0"
+
 
 def _world():
     if dist.is_available() and dist.is_initialized():
@@ -209,14 +212,29 @@ class PPO:
         from humanoid import _native as N
         st, ac, tr = self.storage, self.actor_critic, self.transition
         t = st.step
-        mean = ac._mlp(ac.actor, obs).contiguous()
+        # the actor's output layer runs inside the sampling launch when it is the 12 x 128 head
+        # (hg_rollout_act_head: bitwise the separate output-layer launch); the mean lands in mu
+        mean = head = None
+        last = ac.actor[-1]
+        if (HEAD_FUSED and ac.policy_dtype == "fp32" and ac.fused_mlp and not torch.is_grad_enabled()
+                and isinstance(last, torch.nn.Linear) and tuple(last.weight.shape) == (12, 128)
+                and last.bias is not None and last.bias.is_contiguous() and hg_mlp.fusable(ac.actor)):
+            h = hg_mlp.mlp_infer_hidden(ac.actor, obs)
+            if hg_mlp.head_fusable(h, last.weight):
+                head = (h, last.weight, last.bias)
+            else:
+                mean = last(h).contiguous()
+        else:
+            mean = ac._mlp(ac.actor, obs).contiguous()
         defer = self._defer_values()
         value = None if defer else ac._mlp(ac.critic, critic_obs).contiguous()
         std = ac.std.detach().contiguous()
-        ac.distribution = _DiagGaussian(mean, std.expand_as(mean))
         p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
         priv = st.privileged_observations
         sl = _slot_views(st, t)
+        if head is not None:
+            mean = sl["mu"]  # written by the launch below
+        ac.distribution = _DiagGaussian(mean, std.expand_as(mean))
         s = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
         if st.obs_frames is not None:
             # frame-only storage: the newest frame of the stack per slot, slot 0's whole stack
@@ -225,8 +243,15 @@ class PPO:
             w, c0 = st.frame_width, obs.shape[1] - st.frame_width
         else:
             w, c0 = obs.shape[1], 0
-        N.check(N.lib().hg_rollout_act(
-            p(mean), p(std), p(value) if value is not None else None, p(obs),
+        if head is not None:
+            h, W, b = head
+            fn = N.lib().hg_rollout_act_head
+            lead = (p(h), ctypes.c_int64(h.stride(0)), p(W), p(b), W.shape[1], p(std))
+        else:
+            fn = N.lib().hg_rollout_act
+            lead = (p(mean), p(std))
+        N.check(fn(
+            *lead, p(value) if value is not None else None, p(obs),
             p(critic_obs) if priv is not None else None, obs.shape[0],
             mean.shape[1], ctypes.c_int64(w), ctypes.c_int64(critic_obs.shape[1] if priv is not None else 0),
             ctypes.c_int64(obs.stride(0)), ctypes.c_int64(c0), ctypes.c_int64(critic_obs.stride(0)),

@@ -281,6 +281,17 @@ int hg_rollout_act(const float* mean, const float* std, const float* value, cons
                    float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
                    void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
                    uint64_t seed, uint64_t counter, void* stream);
+/* hg_rollout_act with the policy's output layer fused in (the skinny 12 x 128 head of the actor,
+ * replacing hg_linear_skinny_forward + the mean round trip): mean[r] = W h[r] + b computed by each
+ * env's 16 sampling lanes with hg_linear_skinny_forward's arithmetic (bitwise its result), h [N,
+ * head_k] rows h_ld apart (16-byte aligned, h_ld % 4 == 0), W [A, head_k], b [A]; the mean goes to
+ * mu_out.  Supported: A == 12, head_k == 128 (else HG_ERR_ARG: run the two launches). */
+int hg_rollout_act_head(const float* h, int64_t h_ld, const float* W, const float* b, int head_k, const float* std,
+                        const float* value, const float* obs, const float* critic_obs, int num_envs, int num_actions,
+                        int64_t obs_width, int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0,
+                        int64_t critic_obs_ld, float* actions_out, float* logp_out, float* mu_out, float* sigma_out,
+                        float* value_out, void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16,
+                        int row_offset, uint64_t seed, uint64_t counter, void* stream);
 int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
                    int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
                    void* stream);

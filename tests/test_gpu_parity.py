@@ -957,6 +957,40 @@ def test_fused_rollout_writes(obs_dtype):
     torch.testing.assert_close(st.dones[0, :, 0], dones, rtol=0, atol=0)
 
 
+def test_fused_head_matches_two_launches():
+    """hg_rollout_act_head (the actor's 12 x 128 output layer inside the sampling launch) writes
+    bitwise the actions, log-probs, mu, sigma and observation rows of the two-launch form
+    (hg_linear_skinny_forward, then hg_rollout_act) on the same seed and counter, on a strided
+    observation view like the env's history windows."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    from humanoid.algo.ppo import ppo as ppo_mod
+    torch.manual_seed(3)
+    n = 4096
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     init_noise_std=0.8)
+    big = torch.randn(n, 705 + 47, device="cuda:0")
+    obs, cobs = big[:, 47:], torch.randn(n, 219, device="cuda:0")  # row stride 752
+    out = {}
+    try:
+        for fused in (False, True):
+            ppo_mod.HEAD_FUSED = fused
+            ppo = PPO(ac, device="cuda:0")
+            ppo._rollout_seed = 12345  # the same action noise in both runs
+            ppo.init_storage(n, 2, [705], [219], [12])
+            with torch.inference_mode():
+                ppo.act(obs, cobs)
+            st = ppo.storage
+            out[fused] = {k: getattr(st, k)[0].clone() for k in
+                          ("actions", "actions_log_prob", "mu", "sigma", "observations", "privileged_observations")}
+    finally:
+        ppo_mod.HEAD_FUSED = True
+    for k in out[True]:
+        assert torch.equal(out[True][k], out[False][k]), k
+    with torch.inference_mode():
+        torch.testing.assert_close(out[True]["mu"], ac.actor(obs), rtol=1e-5, atol=1e-5)
+
+
 def test_set_root_state_and_env_props(env):
     """hg_set_root_state (all envs, clears contact warm-starts) and hg_set_env_props (DR
     friction / base mass) through the C ABI."""
