@@ -311,14 +311,12 @@ constexpr int SK_WROWS = SK_ROWS / SK_WAVES;
 // dx * elu'(h) (h = this layer's input = the layer below's ELU output; elu' = 1 for h > 0, h + 1
 // otherwise) and the block's column sums of it (that layer's bias-gradient partials, one row per
 // 64-row tile: each wave sums its 16 rows in order, then waves 0 + 1 + 2 + 3).
-template <int N, typename TD, bool ACT = false>
-__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
-                                                             TD* __restrict__ dx, int64_t rows,
-                                                             const float* __restrict__ h = nullptr, int64_t ldh = 0,
-                                                             float* __restrict__ colpart = nullptr) {
-  __shared__ float g_s[SK_ROWS * N];
-  __shared__ float2 red[ACT ? SK_WAVES - 1 : 1][64];
-  const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
+template <int N, typename TD, bool ACT>
+__device__ __forceinline__ void skinny_dx_body(int bx, float* __restrict__ g_s, float2 (*red)[64],
+                                               const float* __restrict__ gh, const float* __restrict__ W,
+                                               TD* __restrict__ dx, int64_t rows, const float* __restrict__ h,
+                                               int64_t ldh, float* __restrict__ colpart) {
+  const int64_t r0 = (int64_t)bx * SK_ROWS;
   const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
   for (int i = threadIdx.x; i < nr * N; i += 64 * SK_WAVES) g_s[i] = gh[r0 * N + i];
   const int c = 2 * (threadIdx.x & 63);
@@ -360,17 +358,26 @@ __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __rest
         s0 += t.x;
         s1 += t.y;
       }
-      *reinterpret_cast<float2*>(colpart + (int64_t)blockIdx.x * SK_K + c) = make_float2(s0, s1);
+      *reinterpret_cast<float2*>(colpart + (int64_t)bx * SK_K + c) = make_float2(s0, s1);
     }
   }
 }
 
-template <int N, typename TH>
-__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dw(const float* __restrict__ gh, const TH* __restrict__ h,
-                                                             int64_t ldh, float* __restrict__ partial, int64_t rows) {
+template <int N, typename TD, bool ACT = false>
+__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dx(const float* __restrict__ gh, const float* __restrict__ W,
+                                                             TD* __restrict__ dx, int64_t rows,
+                                                             const float* __restrict__ h = nullptr, int64_t ldh = 0,
+                                                             float* __restrict__ colpart = nullptr) {
   __shared__ float g_s[SK_ROWS * N];
-  __shared__ float2 red[SK_WAVES - 1][N][64];
-  const int64_t r0 = (int64_t)blockIdx.x * SK_ROWS;
+  __shared__ float2 red[ACT ? SK_WAVES - 1 : 1][64];
+  skinny_dx_body<N, TD, ACT>(blockIdx.x, g_s, red, gh, W, dx, rows, h, ldh, colpart);
+}
+
+template <int N, typename TH>
+__device__ __forceinline__ void skinny_dw_body(int bx, float* __restrict__ g_s, float2 (*red)[N][64],
+                                               const float* __restrict__ gh, const TH* __restrict__ h, int64_t ldh,
+                                               float* __restrict__ partial, int64_t rows) {
+  const int64_t r0 = (int64_t)bx * SK_ROWS;
   const int nr = (int)min<int64_t>(SK_ROWS, rows - r0);
   for (int i = threadIdx.x; i < nr * N; i += 64 * SK_WAVES) g_s[i] = gh[r0 * N + i];
   __syncthreads();
@@ -422,7 +429,7 @@ __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dw(const float* __rest
       a1[n] += t.y;
     }
   }
-  float* out = partial + (int64_t)blockIdx.x * (N * SK_K + N);
+  float* out = partial + (int64_t)bx * (N * SK_K + N);
 #pragma unroll
   for (int n = 0; n < N; n++) *reinterpret_cast<float2*>(out + n * SK_K + c) = make_float2(a0[n], a1[n]);
   if (lane < N) {
@@ -430,6 +437,30 @@ __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dw(const float* __rest
     for (int rr = 0; rr < nr; rr++) gb += g_s[rr * N + lane];
     out[N * SK_K + lane] = gb;
   }
+}
+
+template <int N, typename TH>
+__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_dw(const float* __restrict__ gh, const TH* __restrict__ h,
+                                                             int64_t ldh, float* __restrict__ partial, int64_t rows) {
+  __shared__ float g_s[SK_ROWS * N];
+  __shared__ float2 red[SK_WAVES - 1][N][64];
+  skinny_dw_body<N, TH>(blockIdx.x, g_s, red, gh, h, ldh, partial, rows);
+}
+
+// dW / db partials (blocks [0, tiles)) and the ELU-fused input gradient (blocks [tiles, 2 tiles))
+// of hg_linear_skinny_backward_act in ONE launch: the two bodies unchanged (the same bits), one
+// launch ramp / tail instead of two
+template <int N>
+__global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_bwd_act(const float* __restrict__ gh, const float* __restrict__ h,
+                                                                  int64_t ldh, const float* __restrict__ W,
+                                                                  float* __restrict__ partial, float* __restrict__ dx,
+                                                                  float* __restrict__ colpart, int64_t rows, int tiles) {
+  __shared__ float g_s[SK_ROWS * N];
+  __shared__ float2 red[SK_WAVES - 1][N][64];
+  if ((int)blockIdx.x < tiles)
+    skinny_dw_body<N, float>(blockIdx.x, g_s, red, gh, h, ldh, partial, rows);
+  else
+    skinny_dx_body<N, float, true>(blockIdx.x - tiles, g_s, red[0], gh, W, dx, rows, h, ldh, colpart);
 }
 }  // namespace
 
@@ -525,14 +556,16 @@ extern "C" int hg_linear_skinny_backward_act(const float* gh, const float* h, in
   if (!gh_prev || !colpart || ldh % 2 != 0 || (uintptr_t)h % 8 != 0 || (uintptr_t)gh_prev % 8 != 0 ||
       (uintptr_t)colpart % 8 != 0)
     return HG_ERR_ARG;
-  const int rc = skinny_backward<float>(gh, h, ldh, W, nullptr, nullptr, rows, n, k, scratch, stream);
-  if (rc != HG_OK) return rc;
+  if (!gh || !h || !W || !scratch || rows <= 0 || !hg_linear_skinny_supported(n, k) || ldh < k ||
+      (uintptr_t)W % 8 != 0 || rows > ((int64_t)1 << 36))
+    return HG_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((rows + SK_ROWS - 1) / SK_ROWS));
-#define HG_SK_DXA(NN) \
-  hipLaunchKernelGGL((k_skinny_dx<NN, float, true>), grid, dim3(64 * SK_WAVES), 0, s, gh, W, gh_prev, rows, h, ldh, colpart)
-  HG_SKINNY_SWITCH(n, HG_SK_DXA)
-#undef HG_SK_DXA
+  const int tiles = (int)((rows + SK_ROWS - 1) / SK_ROWS);
+  const dim3 grid((unsigned)(2 * tiles));
+#define HG_SK_BWDA(NN) \
+  hipLaunchKernelGGL((k_skinny_bwd_act<NN>), grid, dim3(64 * SK_WAVES), 0, s, gh, h, ldh, W, scratch, gh_prev, colpart, rows, tiles)
+  HG_SKINNY_SWITCH(n, HG_SK_BWDA)
+#undef HG_SK_BWDA
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
