@@ -88,6 +88,10 @@ class _PPOLoss(torch.autograd.Function):
     def backward(ctx, g_loss, g_stats=None):
         g_mu, g_std, g_v, g_p = ctx.saved_tensors
         rows, A = g_mu.shape
+        if g_loss.data_ptr() in UNIT_SEEDS:
+            # seeded by a registered constant 1.0 (PPO's graphed update): scaling by exactly 1.0 is
+            # the identity on every float, so the scaling launch is left out
+            return g_mu, g_std, g_v, g_p, None, None
         g_loss = g_loss.contiguous()
         s = ctypes.c_void_p(torch.cuda.current_stream(g_mu.device).cuda_stream)
         rc = _lib().hg_ppo_loss_backward(g_loss.data_ptr(), rows, A, g_mu.data_ptr(), g_std.data_ptr(),
@@ -95,6 +99,11 @@ class _PPOLoss(torch.autograd.Function):
         if rc != 0:
             raise RuntimeError(f"hg_ppo_loss_backward failed ({rc})")
         return g_mu, g_std, g_v, g_p, None, None
+
+
+# persistent device scalars holding exactly 1.0 that seed loss.backward(), by data pointer (their
+# owners never write them again; kept referenced here so the address is never reused)
+UNIT_SEEDS = {}
 
 
 def ppo_loss(mu, std, value, lin_vel, data, clip_param, value_loss_coef, entropy_coef, lin_vel_coef,

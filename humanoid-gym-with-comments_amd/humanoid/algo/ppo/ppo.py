@@ -29,6 +29,7 @@ import torch.optim as optim
 from .actor_critic import ActorCritic, _DiagGaussian
 from .hg_adam import HgAdam
 from . import hg_mlp
+from . import hg_loss
 from .hg_loss import ppo_loss
 from .rollout_storage import RolloutStorage, gather_rows
 
@@ -580,6 +581,7 @@ class PPO:
                                    device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
         self._one_grad = torch.ones((), dtype=torch.float32, device=dev)
+        hg_loss.UNIT_SEEDS[self._one_grad.data_ptr()] = self._one_grad
         # [value, surrogate, lin-vel loss sums, KL mean of the current minibatch]: the fused loss
         # accumulates into it directly
         self._stats4 = torch.zeros(4, dtype=torch.float32, device=dev)
