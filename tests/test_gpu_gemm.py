@@ -359,3 +359,41 @@ def test_skinny_backward_act_matches_fp64(rows, n):
     dw_bound = REL * (g.double().abs().t() @ h.double().abs()).reshape(-1) * 2 + 1e-9
     assert ((wb[: n * k] - dw_ref).abs() <= dw_bound).all()
     assert ((wb[n * k:] - db_ref).abs() <= REL * g.double().abs().sum(0) * 2 + 1e-9).all()
+
+
+@pytest.mark.parametrize("parts,width", [(8, 90240), (32, 360960), (64, 196608), (5, 4100), (40, 768)])
+def test_colsum_jobs_wide_and_narrow_orders(parts, width):
+    """hg_colsum_jobs in one launch over several jobs: wide split-K jobs (width >= 4096, a multiple
+    of 4) sum part p into accumulator p % 8 and combine the eight as a fixed tree above 16 parts,
+    in part order up to 16 — both reproduced bitwise here in float32 numpy; narrow jobs (bias-tile
+    partials) keep the 16-column blocks' order, checked against float64 within rounding."""
+    _need_gpu()
+    import numpy as np
+    from humanoid import _native as N
+    g = torch.Generator(device="cuda:0").manual_seed(parts * 7 + 1)
+    src = torch.randn(parts, width, device="cuda:0", generator=g) * 3.0
+    nar = torch.randn(37, 768, device="cuda:0", generator=g)
+    dst, dst_n = torch.empty(width, device="cuda:0"), torch.empty(768, device="cuda:0")
+    vp = ctypes.c_void_p
+    rc = N.lib().hg_colsum_jobs((vp * 2)(src.data_ptr(), nar.data_ptr()), (vp * 2)(dst.data_ptr(), dst_n.data_ptr()),
+                                (ctypes.c_int64 * 2)(width, 768), (ctypes.c_int * 2)(parts, 37), 2,
+                                vp(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    a = src.cpu().numpy()
+    if width >= 4096 and width % 4 == 0 and parts > 16:
+        acc = [np.zeros(width, np.float32) for _ in range(8)]
+        for p in range(parts):
+            acc[p % 8] = (acc[p % 8] + a[p]).astype(np.float32)
+        want = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]))
+    elif parts <= 16:
+        want = a[0].copy()
+        for p in range(1, parts):
+            want = (want + a[p]).astype(np.float32)
+    else:  # narrow job with many parts: the bias-partial blocks' order
+        want = None
+        assert torch.allclose(dst.double(), src.double().sum(0), rtol=1e-5, atol=1e-4)
+    if want is not None:
+        assert np.array_equal(dst.cpu().numpy(), want)
+    ref = nar.double().sum(0)
+    assert torch.allclose(dst_n.double(), ref, rtol=1e-5, atol=1e-4)
