@@ -546,7 +546,10 @@ struct X6Op {
 // exactly the LDS fragment order, so a block's BM (BN) rows of a chunk are copied by LDS-DMA
 // (global_load_lds, 1 KB per wave instruction, lane-linear) with no register staging, split or LDS
 // write pass.  The image's plane pitch (16-byte slots) rides in lda / ldb.
-template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, int IMG = 0>
+// APF (B from its image, A staged from k-contiguous rows): A's global loads run two chunks ahead
+// in two register sets, so the activations' HBM latency has two chunks of MFMAs to hide behind
+// (the B image comes from L2 by LDS-DMA one chunk ahead as before); same products, same bits
+template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, int IMG = 0, bool APF = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
@@ -592,6 +595,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
 
   X6Op<BM, KG, NT, AKC, VEC> sa;
   X6Op<BN, KG, NT, BKC, VEC> sb;
+  constexpr bool AP = APF && IMG == 1 && AKC;
+  X6Op<BM, KG, NT, AKC, VEC> sa2;  // AP: A's second register set
   float* scA = reinterpret_cast<float*>(lds + 2 * STAGE);
   float* scB = scA + SCA;
   const int64_t nk = kend - kbeg;
@@ -634,6 +639,56 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
       if (!BKC && !BIMG) sb.rt.to_planes(S + 3 * PA, scB, tid);
     }
   };
+  auto mfma_chunk = [&](const bf16x8* cur) {
+#pragma unroll
+    for (int kg = 0; kg < KG; kg++) {
+      bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+#pragma unroll
+        for (int m = 0; m < TM; m++) a[p][m] = cur[p * PA + x6_slot(BM, kg, wm0 + 32 * m + i, h)];
+#pragma unroll
+        for (int n = 0; n < TN; n++) b[p][n] = cur[3 * PA + p * PB + x6_slot(BN, kg, wn0 + 32 * n + i, h)];
+      }
+#pragma unroll
+      for (int m = 0; m < TM; m++)
+#pragma unroll
+        for (int n = 0; n < TN; n++) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][m], b[0][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[1][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[2][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][m], b[0][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[1][n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][m], b[0][n], acc[m][n], 0, 0, 0);
+        }
+    }
+  };
+  if (AP) {
+    // chunk j's A in set j & 1: chunk c + 2 loads into the set chunk c left at the top of
+    // iteration c, chunk c + 1 (loaded one iteration earlier) is split into LDS at its bottom
+    auto loadA = [&](auto& S, int64_t kc) { S.load(g.A, g.lda, m0, mmax, kc, kend, kc + BK > kfull, tid); };
+    if (nchunks > 0) {
+      dma_all(0, lds);
+      loadA(sa, kbeg);
+      sa.kc.store(lds, tid);
+      if (nchunks > 1) loadA(sa2, kbeg + BK);
+    }
+    __syncthreads();
+    auto body = [&](int c, auto& L, auto& H) {
+      const bf16x8* cur = lds + (c & 1) * STAGE;
+      bf16x8* nxt = lds + ((c + 1) & 1) * STAGE;
+      const bool more = c + 1 < nchunks;
+      if (more) dma_all(c + 1, nxt);
+      if (c + 2 < nchunks) loadA(L, kbeg + (int64_t)(c + 2) * BK);
+      mfma_chunk(cur);
+      if (more) H.kc.store(nxt, tid);
+      __syncthreads();
+    };
+    for (int c = 0; c < nchunks; c += 2) {
+      body(c, sa, sa2);
+      if (c + 1 < nchunks) body(c + 1, sa2, sa);
+    }
+  } else {
   if (nchunks > 0) {
     if (IMG) dma_all(0, lds);
     if (IMG != 3) {
@@ -674,6 +729,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
     }
     if (more && IMG != 3) store(nxt);
     __syncthreads();
+  }
   }
 
   // epilogue.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2) + 4h, column i.
@@ -793,7 +849,7 @@ __global__ void __launch_bounds__(256) k_x6_image_jobs(ImageJobs J) {
   base[2 * pitch] = x2;
 }
 
-template <int BM, int BN, int WGM, int WGN, int KG>
+template <int BM, int BN, int WGM, int WGN, int KG, bool APF = false>
 int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
   GemmArgs& g = xa.g;
   g.tiles_n = (g.N + BN - 1) / BN;
@@ -802,7 +858,7 @@ int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStrea
   if (mode != 2) xa.slices = 1;
   if (g.tiles * xa.slices > 0x7fffffff) return HG_ERR_ARG;
   const dim3 grid((unsigned)(g.tiles * xa.slices)), block(64 * WGM * WGN);
-#define HG_X6I(V, MD, E, I) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, I>), grid, block, 0, s, xa)
+#define HG_X6I(V, MD, E, I) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, I, APF>), grid, block, 0, s, xa)
   if (mode == 2) {
     HG_X6I(false, 2, false, 3);
   } else if (img == 3) {
@@ -839,6 +895,9 @@ int x6_img_dispatch(int tile, int mode, int img, GemmX6Args xa, bool vec, bool e
     case 26: return launch_x6_img<128, 128, 2, 4, 2>(mode, img, xa, vec, elu, s);
     case 27: return launch_x6_img<128, 256, 2, 4, 1>(mode, img, xa, vec, elu, s);
     case 28: return launch_x6_img<64, 256, 2, 4, 1>(mode, img, xa, vec, elu, s);
+    // 29: tile 23 with A two chunks ahead (APF; B-image form only).  The same variant of tiles 20,
+    // 21, 22 and 28 measured slower on every routed shape (profiles/r4_gemm/x6_apf_probe.jsonl)
+    case 29: return launch_x6_img<64, 64, 2, 2, 1, true>(mode, img, xa, vec, elu, s);
     default: return launch_x6_img<64, 128, 2, 2, 1>(mode, img, xa, vec, elu, s);  // 19
   }
 }
@@ -878,7 +937,7 @@ int launch_x6(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-constexpr int NTILES = 28;
+constexpr int NTILES = 29;  // 29: tile 23 with A two chunks ahead (image entry)
 // block rows of a tile id (the column-partial row count of mode 1)
 int tile_bm(int tile) {
   if (tile == 25) return 256;
@@ -1245,6 +1304,7 @@ extern "C" int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B
     case 20: return launch_x6<128, 128, 2, 2, 1>(mode, xa, vec, elu, s);
     case 21: return launch_x6<128, 128, 2, 4, 1>(mode, xa, vec, elu, s);
     case 22: return launch_x6<128, 64, 2, 2, 1>(mode, xa, vec, elu, s);
+    case 29:
     case 23: return launch_x6<64, 64, 2, 2, 1>(mode, xa, vec, elu, s);
     case 24: return launch_x6<128, 128, 2, 2, 2>(mode, xa, vec, elu, s);
     case 25: return launch_x6<256, 128, 4, 2, 1>(mode, xa, vec, elu, s);
@@ -1259,7 +1319,7 @@ extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, in
                                  int64_t cstride, int64_t M, int N, int64_t K, int slices, int kmajor, int tile,
                                  void* stream) {
   const bool tr = tile >= WGRAD_TR0 && tile <= WGRAD_TR1;
-  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || slices < 1 || (!tr && (tile < 19 || tile > NTILES)) ||
+  if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || slices < 1 || (!tr && (tile < 19 || tile > 28)) ||
       K > 0x7fffffff || (kmajor != 0 && kmajor != 1) || (tr && (kmajor != 0 || M > 0x7fffffff)))
     return HG_ERR_ARG;
   if (kmajor == 0 && (lda < M || ldb < N)) return HG_ERR_ARG;

@@ -263,7 +263,7 @@ def linear_act(h, W, b, elu=True, out=None, tile=0):
 _BIG = 1 << 40
 X6_TILE0 = 19  # tiles >= 19: the bf16-split (6-term) kernels of hg_gemm_f32
 _GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG, 22)],
-             (256, 128): [(8192, 0), (32768, 5), (_BIG, 20)], (705, 128): [(8192, 5), (_BIG, 23)],
+             (256, 128): [(8192, 0), (32768, 5), (_BIG, 20)], (705, 128): [(8192, 5), (_BIG, 29)],
              (128, 128): [(8192, 0), (_BIG, 5)], (219, 768): [(32768, 21), (_BIG, 20)],
              (768, 256): [(32768, 22), (_BIG, 20)]}
 # input gradients (24576 rows, torch mm + ELU-backward pass -> fused; gemm_probe_x6.jsonl): 256->512
@@ -274,6 +274,11 @@ _GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG,
 # split-K slices (LDS-transposed staging of the row-major gh and x, or explicit transposes) was
 # 0.57-0.94x of its tuned TN kernels on every shape.
 # The 64x256 tile on 8 waves (28) with the W^T image: 256->512 72.9 -> 67.5 us (x6_image_probe_wide.jsonl).
+# lin-vel's first layer 705 -> 128 on tile 29 (tile 23 with A's loads two chunks ahead): 54.3 ->
+# 50.9 us at 24576 rows; the same variant of the other tiles was slower on every routed shape
+# (scripts/x6_apf_probe.py, profiles/r4_gemm/x6_apf_probe.jsonl)
+if os.environ.get("HG_X6_APF", "1") == "0":
+    _GEMM_FWD[(705, 128)] = [(8192, 5), (_BIG, 23)]
 _GEMM_DX = {(256, 512): [(_BIG, 28)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 22)], (128, 128): [(_BIG, 5)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
 # The bf16-split tiles read B (the weight) from an image split once per MLP call

@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 pytestmark = pytest.mark.gpu
 
 REL = 1e-6
-TILES = list(range(1, 29))  # 1..18 f32 MFMA, 19..28 bf16-split (6-term)
+TILES = list(range(1, 30))  # 1..18 f32 MFMA, 19..29 bf16-split (6-term; 29 = 23 with A two chunks ahead)
 
 
 def _need_gpu():
@@ -184,7 +184,7 @@ def test_gemm_images_bitwise_equal(rows, k, n):
     aimg = _image(L, x, 0, rows, k)
     for mode, B, trans in ((0, W, 0), (1, Wd, 1)):
         bimg = _image(L, B, trans, n, k)
-        for tile in range(19, 29):
+        for tile in range(19, 30):
             parts = int(L.hg_gemm_colpart_rows(rows, tile))
             outs = []
             for form in ("staged", "b_image", "ab_image"):
@@ -224,7 +224,7 @@ def test_gemm_images_bitwise_equal(rows, k, n):
     assert L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), None, bimg.data_ptr(), None, None, 0, out.data_ptr(),
                              out.stride(0), None, rows, n, k + 40, 0, 20, 0, nb, _stream()) != 0
     assert L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), None, bimg.data_ptr(), None, None, 0, out.data_ptr(),
-                             out.stride(0), None, rows, n, k, 0, 29, 0, nb, _stream()) != 0
+                             out.stride(0), None, rows, n, k, 0, 30, 0, nb, _stream()) != 0
     torch.cuda.synchronize()
 
 
