@@ -6,7 +6,8 @@
 // Two launches over a list of up to HG_MAX_TENSORS parameter tensors, passed by value:
 //   k_sqnorm: per-block partial sums of g^2 (fixed chunk -> block map, deterministic), and each
 //             tensor's first block increments that tensor's step counter;
-//   k_adam:   every block reduces the partials in a fixed order (deterministic total norm),
+//   k_adam:   every block reduces the partials in one fixed order (deterministic total norm; its
+//             own chunk's loads issued before that reduction),
 //             clip_coef = min(max_norm / (||g|| + 1e-6), 1) as clip_grad_norm_, then Adam:
 //               m = b1 m + (1 - b1) g';  v = b2 v + (1 - b2) g'^2
 //               p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
@@ -60,33 +61,13 @@ __global__ void __launch_bounds__(TPB) k_sqnorm(hg_tensor_list T, float* __restr
 __global__ void __launch_bounds__(TPB) k_adam(hg_tensor_list T, const float* __restrict__ partial, int nblocks,
                                              const float* __restrict__ lr_ptr, float beta1, float beta2, float eps,
                                              float max_norm) {
-  __shared__ float s_coef;
-  if (threadIdx.x < 64) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < nblocks; i += 64) s += partial[i];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (threadIdx.x == 0) {
-      float c = 1.0f;
-      if (max_norm > 0.f) {
-        const float total = sqrtf(s);
-        c = fminf(max_norm / (total + 1e-6f), 1.0f);
-      }
-      s_coef = c;
-    }
-  }
-  __syncthreads();
-  const float coef = s_coef;
+  // the chunk's parameter / gradient / moment loads go out first, so their latency overlaps the
+  // norm reduction (a barrier would otherwise hold them back)
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < T.count && T.chunk_start[t + 1] <= b) t++;
   const int64_t off = (int64_t)(b - T.chunk_start[t]) * CHUNK;
   const int64_t n = T.numel[t];
-  const float step = T.step[t] ? *T.step[t] : 1.0f;
-  const float lr = *lr_ptr;
-  const float bc1 = 1.0f - powf(beta1, step);
-  const float bc2 = 1.0f - powf(beta2, step);
-  const float step_size = lr / bc1;
-  const float bc2_sqrt = sqrtf(bc2);
   float* __restrict__ p = T.param[t];
   const float* __restrict__ g = T.grad[t];
   float* __restrict__ m = T.exp_avg[t];
@@ -97,6 +78,26 @@ __global__ void __launch_bounds__(TPB) k_adam(hg_tensor_list T, const float* __r
     const int64_t i = off + threadIdx.x + k * TPB;
     if (i < n) { gk[k] = g[i]; mk[k] = m[i]; vk[k] = v[i]; pk[k] = p[i]; }
   }
+  // total squared norm from the k_sqnorm partials, the same fixed order in every block: thread t
+  // sums partials t, t + 256, ... (independent loads), then the wave and the four waves in order
+  __shared__ float ws[TPB / 64];
+  float s = 0.f;
+#pragma unroll 4
+  for (int i = threadIdx.x; i < nblocks; i += TPB) s += partial[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  float coef = 1.0f;
+  if (max_norm > 0.f) {
+    const float total = sqrtf((ws[0] + ws[1]) + (ws[2] + ws[3]));
+    coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+  }
+  const float step = T.step[t] ? *T.step[t] : 1.0f;
+  const float lr = *lr_ptr;
+  const float bc1 = 1.0f - powf(beta1, step);
+  const float bc2 = 1.0f - powf(beta2, step);
+  const float step_size = lr / bc1;
+  const float bc2_sqrt = sqrtf(bc2);
 #pragma unroll
   for (int k = 0; k < PER; k++) {
     const int64_t i = off + threadIdx.x + k * TPB;
