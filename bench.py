@@ -409,6 +409,8 @@ def main():
                                 "XBot-L heightfield terrain 2100x2100, 4096 envs/GPU, PPO 24-step rollout (config 3)"),
                    "envs_per_gpu": args.envs, "num_steps_per_env": args.T, "parallelism": f"dp{world}",
                    "ppo": "2 epochs x 4 minibatches, actor 705-512-256-128-12, critic 219-768-256-128-1",
+                   "update_graph": runner.alg.update_graph,
+                   "collectives_per_iteration": runner.alg.collectives_per_update(),
                    "gemm_table": "tuning/tunableop_mi355x_f32.csv" if tuned else None,
                    "gemm": ("f32 operands and accumulation; the large hidden-layer forwards run on the bf16 matrix "
                             "cores as exact three-way bf16 splits of each f32 operand (six partial products, f32 "

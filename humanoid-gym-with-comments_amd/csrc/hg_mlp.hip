@@ -457,10 +457,14 @@ __global__ void __launch_bounds__(64 * SK_WAVES) k_skinny_bwd_act(const float* _
                                                                   float* __restrict__ colpart, int64_t rows, int tiles) {
   __shared__ float g_s[SK_ROWS * N];
   __shared__ float2 red[SK_WAVES - 1][N][64];
-  if ((int)blockIdx.x < tiles)
+  if ((int)blockIdx.x < tiles) {
     skinny_dw_body<N, float>(blockIdx.x, g_s, red, gh, h, ldh, partial, rows);
-  else
-    skinny_dx_body<N, float, true>(blockIdx.x - tiles, g_s, red[0], gh, W, dx, rows, h, ldh, colpart);
+  } else {
+    // the dx body's [SK_WAVES - 1][64] view over the whole buffer (>= that size for every N >= 1),
+    // not red[0], whose [N][64] bound is one row for the critic head
+    float2 (*red_dx)[64] = reinterpret_cast<float2 (*)[64]>(&red[0][0][0]);
+    skinny_dx_body<N, float, true>(blockIdx.x - tiles, g_s, red_dx, gh, W, dx, rows, h, ldh, colpart);
+  }
 }
 }  // namespace
 

@@ -12,6 +12,7 @@ for ``max`` and ``clamp``); reductions run in float64 in a fixed order, so the r
 deterministic.  Device tensors only.
 """
 import ctypes
+import os
 
 import torch
 
@@ -101,9 +102,26 @@ class _PPOLoss(torch.autograd.Function):
         return g_mu, g_std, g_v, g_p, None, None
 
 
-# persistent device scalars holding exactly 1.0 that seed loss.backward(), by data pointer (their
-# owners never write them again; kept referenced here so the address is never reused)
+# persistent device scalars holding exactly 1.0 that seed loss.backward(), by data pointer.  The
+# contract (register_unit_seed): the owner never writes the tensor after registering it, and
+# releases it (release_unit_seed) before dropping it; the registry keeps it referenced meanwhile,
+# so its address cannot be reused by another tensor while registered.
 UNIT_SEEDS = {}
+
+
+def register_unit_seed(t):
+    """Register a [] float32 device tensor holding 1.0 as a backward seed whose scaling launch may
+    be skipped; returns it.  HG_DEBUG_UNIT_SEEDS=1 checks the value (a host read: not under capture)."""
+    if t.numel() != 1 or t.dtype != torch.float32:
+        raise ValueError("a unit seed is a float32 scalar")
+    if os.environ.get("HG_DEBUG_UNIT_SEEDS") == "1" and float(t) != 1.0:
+        raise ValueError("a unit seed must hold exactly 1.0")
+    UNIT_SEEDS[t.data_ptr()] = t
+    return t
+
+
+def release_unit_seed(t):
+    UNIT_SEEDS.pop(t.data_ptr(), None)
 
 
 def ppo_loss(mu, std, value, lin_vel, data, clip_param, value_loss_coef, entropy_coef, lin_vel_coef,

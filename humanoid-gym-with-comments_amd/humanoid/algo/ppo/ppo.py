@@ -19,6 +19,7 @@ CPU the reference's host-side arithmetic is kept verbatim (this is what the gold
 import contextlib
 import ctypes
 import os
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -52,6 +53,21 @@ def _data_parallel():
         return True
     return (os.environ.get("HG_DP_FORCE") == "1" and dist.is_available() and dist.is_initialized())
 
+
+
+@contextlib.contextmanager
+def _capturing(g, mode, pool=None):
+    """torch.cuda.graph without its one failure mode that matters here: when the body raises and
+    capture_end raises too, torch.cuda.graph leaves the side stream current.  The stream context is
+    the outer one, so it is restored whatever happens inside."""
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    with torch.cuda.stream(torch.cuda.Stream()):
+        g.capture_begin(*(() if pool is None else (pool,)), capture_error_mode=mode)
+        try:
+            yield
+        finally:
+            g.capture_end()
 
 
 def _slot_views(st, t):
@@ -103,6 +119,8 @@ class PPO:
         self.use_graphs = self._on_device
         self._graphs = None
         self._graph_warm = False
+        self.update_graph = "eager"   # the update form last run: "eager" | "one" | "two" graphs
+        self.capture_error = None     # why the in-graph collective fell back, if it did
         self._flat_grad = None
         if self._dp:
             with torch.no_grad():
@@ -284,10 +302,12 @@ class PPO:
         t.action_sigma = self.actor_critic.action_std.detach()
         # the reference keeps the obs tensors and copies them into the storage after env.step
         # (ppo.py:123-125, rollout_storage.py:90-91), relying on the env allocating new ones per
-        # step; hg_sim's window views are rewritten in place by the next step (a reset zeroes the
-        # older frames), so a device tensor is copied here, before the step
-        t.observations = obs.clone() if obs.is_cuda else obs
-        t.critic_observations = critic_obs.clone() if critic_obs.is_cuda else critic_obs
+        # step — as hg_sim does by default (stable_observations); its live window views (the
+        # runner's mode, tagged hg_live_view) are rewritten in place by the next step (a reset
+        # zeroes the older frames), so those are copied here, before the step
+        t.observations = obs.clone() if getattr(obs, "hg_live_view", False) else obs
+        t.critic_observations = (critic_obs.clone() if getattr(critic_obs, "hg_live_view", False)
+                                 else critic_obs)
         return t.actions
 
     def process_env_step(self, rewards, dones, infos):
@@ -580,8 +600,9 @@ class PPO:
         self._packed = torch.empty(st.num_transitions_per_env * st.num_envs, sum(widths), dtype=torch.float32,
                                    device=dev)
         self._idx = torch.zeros(mb, dtype=torch.int64, device=dev)
-        self._one_grad = torch.ones((), dtype=torch.float32, device=dev)
-        hg_loss.UNIT_SEEDS[self._one_grad.data_ptr()] = self._one_grad
+        if getattr(self, "_one_grad", None) is not None:
+            hg_loss.release_unit_seed(self._one_grad)  # the graphs that read it are replaced below
+        self._one_grad = hg_loss.register_unit_seed(torch.ones((), dtype=torch.float32, device=dev))
         # [value, surrogate, lin-vel loss sums, KL mean of the current minibatch]: the fused loss
         # accumulates into it directly
         self._stats4 = torch.zeros(4, dtype=torch.float32, device=dev)
@@ -613,29 +634,62 @@ class PPO:
             nmb = self.num_mini_batches
             self._perm = torch.zeros(nmb * mb, dtype=torch.int64, device=dev)
             g = torch.cuda.CUDAGraph()
-            # thread_local: the process group's watchdog thread may query its events meanwhile
-            with torch.cuda.graph(g, capture_error_mode="thread_local" if self._dp else "global"):
-                for _ in range(self.num_learning_epochs):
-                    for i in range(nmb):
-                        if self._flat_grad is None:
-                            self.optimizer.zero_grad(set_to_none=True)  # fresh gradients from each backward
-                        self._mb_backward(self._perm[i * mb:(i + 1) * mb])  # zeroes the flat buffer (dp)
-                        if self._dp:
-                            dist.all_reduce(self._flat_grad)  # gradients + the KL slot, in the graph
-                        self._mb_step()
-            self._graphs = (g, None, mb, self._storage_key())
-            return
-        with torch.cuda.graph(ga):
+            ok = True
+            try:
+                # thread_local: the process group's watchdog thread may query its events meanwhile
+                with _capturing(g, "thread_local" if self._dp else "global"):
+                    for _ in range(self.num_learning_epochs):
+                        for i in range(nmb):
+                            if self._flat_grad is None:
+                                self.optimizer.zero_grad(set_to_none=True)  # fresh gradients from each backward
+                            self._mb_backward(self._perm[i * mb:(i + 1) * mb])  # zeroes the flat buffer (dp)
+                            if self._dp:
+                                dist.all_reduce(self._flat_grad)  # gradients + the KL slot, in the graph
+                            self._mb_step()
+            except Exception as e:  # noqa: BLE001 — the collective's capture is the known risk
+                if not self._dp:
+                    raise
+                ok = False
+                self.capture_error = f"{type(e).__name__}: {e}"
+            if self._dp:
+                # every rank takes the same form: a rank whose capture failed pulls all to two graphs
+                flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                ok = bool(flag.item())
+            if ok:
+                self._graphs = (g, None, mb, self._storage_key())
+                self.update_graph = "one"
+                return
+            # fall back in this process (never a re-exec): the two-graph form, all-reduce between
+            del g
+            torch.cuda.synchronize(dev)
+            self._whole = False
+            if self.capture_error is None:
+                self.capture_error = "another rank's capture failed"
+            warnings.warn(f"PPO: the in-graph all-reduce could not be captured ({self.capture_error}); "
+                          "using two graphs per minibatch with the all-reduce between them")
+        with _capturing(ga, "global"):
             self._mb_backward(self._idx)
-        with torch.cuda.graph(gb, pool=ga.pool()):
+        with _capturing(gb, "global", pool=ga.pool()):
             self._mb_step()
         self._graphs = (ga, gb, mb, self._storage_key())
+        self.update_graph = "two"
 
     def _collective_in_graph(self):
-        """RCCL ("nccl" backend): the per-minibatch gradient all-reduce is captured in the update
-        graph (HG_DP_GRAPH_COLLECTIVE=0 keeps the two-graph form with an eager all-reduce)."""
+        """Whether the per-minibatch gradient all-reduce is captured inside the one update graph.
+        Only on RCCL ("nccl" backend; gloo collectives cannot be captured) and only on request
+        (HG_DP_GRAPH_COLLECTIVE=1): the in-graph collective is verified at world size 1 only, so
+        the default data-parallel form is the two-graph one with the eager all-reduce between the
+        replays.  A failed capture falls back to that form on every rank (`update_graph`)."""
         return (self._dp and dist.is_initialized() and dist.get_backend() == "nccl"
-                and os.environ.get("HG_DP_GRAPH_COLLECTIVE", "1") != "0")
+                and os.environ.get("HG_DP_GRAPH_COLLECTIVE", "0") == "1")
+
+    def collectives_per_update(self):
+        """Collectives one update() issues: per minibatch the flat-gradient (+ KL slot) all-reduce,
+        plus the advantage-statistics all-reduce of compute_returns; 0 on one process."""
+        if not self._dp:
+            return 0
+        return self.num_learning_epochs * self.num_mini_batches + 1
 
     def _mb_backward(self, idx):
         """Captured minibatch body: gather rows -> losses -> backward (+ KL mean, loss sums)."""

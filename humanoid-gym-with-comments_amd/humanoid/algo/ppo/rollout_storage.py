@@ -88,7 +88,6 @@ class RolloutStorage:
         self.saved_hidden_states_c = None
         self.step = 0
         self.writes = 0          # bumped by every write of a slot (add_transitions, PPO's fused act)
-        self._obs_cache = None   # frame-only storage: (key, rebuilt [T, N, obs])
         self.gae_fn = None  # optional override (tests); default: HIP kernel
         self.time_outs = None  # [T, N, 1] u8, only when PPO defers the value pass (device path)
         self.values_deferred = False
@@ -99,19 +98,16 @@ class RolloutStorage:
     def observations(self):
         """[T, N, obs] actor observations.  Frame-only storage: a READ-ONLY reconstruction (writing
         into it does not reach the storage — write through add_transitions), rebuilt from the
-        frames + dones once per change of the storage (``writes``) and cached until the next."""
+        frames + dones on every access and not kept: a cached copy would hold T x N x 705 floats
+        through the next rollout and go stale under any direct write of the frames or dones.  The
+        update itself never reads it (its minibatch rows come from gather_stacked)."""
         if self.obs_frames is None:
             return self._observations
-        key = (self.writes, self.step)
-        if self._obs_cache is not None and self._obs_cache[0] == key:
-            return self._obs_cache[1]
         T, N = self.num_transitions_per_env, self.num_envs
         idx = torch.arange(T * N, device=self.device, dtype=torch.int64)
         out = torch.empty(T * N, self.obs_shape[0], dtype=self.obs_dtype, device=self.device)
         self.gather_stacked(idx, out)
-        out = out.view(T, N, -1)
-        self._obs_cache = (key, out)
-        return out
+        return out.view(T, N, -1)
 
     def prepare_gather(self):
         """Env-major copy of the dones ([N, T]: a row's reset scan reads one run) for the

@@ -133,6 +133,13 @@ def build_hg_cfg(cfg, num_envs, sim_dt, seed, model_js, heightfield=None, hf_sha
     return c, aux
 
 
+
+def _live(view):
+    """Tag a window view handed out in place of a copy (stable_observations False): the next step
+    rewrites it, so a consumer that keeps it past env.step must copy it (PPO.act does)."""
+    view.hg_live_view = True
+    return view
+
 class XBotLFreeEnv(BaseTask):
     """Drop-in for the reference XBotLFreeEnv (humanoid_env.py:63)."""
 
@@ -527,10 +534,10 @@ class XBotLFreeEnv(BaseTask):
         return self.get_observations(), self.get_privileged_observations(), self.rew_buf, self.reset_buf, self.extras
 
     def get_observations(self):
-        return self.obs_buf.clone() if self.stable_observations else self.obs_buf
+        return self.obs_buf.clone() if self.stable_observations else _live(self.obs_buf)
 
     def get_privileged_observations(self):
-        return self.privileged_obs_buf.clone() if self.stable_observations else self.privileged_obs_buf
+        return self.privileged_obs_buf.clone() if self.stable_observations else _live(self.privileged_obs_buf)
 
     def reset_idx(self, env_ids):
         """reset_idx (humanoid_env.py:1109-1163) for the given env ids, as a device mask; also

@@ -67,6 +67,50 @@ class RefSim:
                 _p(self.contact), _p(self.rigid), _p(self.nonfinite), _p(self.dropped))
 
 
+def ground(cfg, hf, x, y):
+    """(height, unit normal[..., 3]) of the terrain under world points (x, y), numpy float64: the
+    plane z = 0, or the int16 heightfield triangulated along the (i, j)-(i+1, j+1) diagonal —
+    physics_ref.c:179-196 (`ground`) element for element.  For tests that classify contacts by
+    the triangle they sit on."""
+    x, y = np.asarray(x, np.float64), np.asarray(y, np.float64)
+    if cfg.terrain_type == 0 or hf is None:
+        n = np.zeros(x.shape + (3,))
+        n[..., 2] = 1.0
+        return np.zeros(x.shape), n
+    hs, vs = float(cfg.hf_horizontal_scale), float(cfg.hf_vertical_scale)
+    rows, cols = int(cfg.hf_rows), int(cfg.hf_cols)
+    fx, fy = (x + cfg.hf_border) / hs, (y + cfg.hf_border) / hs
+    i = np.clip(np.floor(fx).astype(np.int64), 0, rows - 2)
+    j = np.clip(np.floor(fy).astype(np.int64), 0, cols - 2)
+    u, v = np.clip(fx - i, 0, 1), np.clip(fy - j, 0, 1)
+    H = np.asarray(hf).reshape(rows, cols).astype(np.float64) * vs
+    h00, h10, h01, h11 = H[i, j], H[i + 1, j], H[i, j + 1], H[i + 1, j + 1]
+    lower = u >= v
+    h = np.where(lower, h00 + u * (h10 - h00) + v * (h11 - h10), h00 + v * (h01 - h00) + u * (h11 - h01))
+    dx = np.where(lower, (h10 - h00) / hs, (h11 - h01) / hs)
+    dy = np.where(lower, (h11 - h10) / hs, (h01 - h00) / hs)
+    inv = 1 / np.sqrt(dx * dx + dy * dy + 1)
+    return h, np.stack([-dx * inv, -dy * inv, inv], axis=-1)
+
+
+def quat_rotate(q, v):
+    """Rotate v[..., 3] by unit quaternions q[..., 4] (x, y, z, w), numpy."""
+    u, w = q[..., :3], q[..., 3:4]
+    t = 2 * np.cross(u, v)
+    return v + w * t + np.cross(u, t)
+
+
+def ground_candidates(model, rigid):
+    """World centres [n, nc, 3] of the model's ground-contact spheres from rigid states
+    [n, bodies, 13] (position, quaternion xyzw, ...): x = o_b + R_b cpos_c, the point whose
+    (x, y) physics_ref.c:472-477 looks the terrain up under."""
+    nc = len(model.contact_body)
+    cb = np.array([model.contact_body[c] for c in range(nc)])
+    cp = np.array([list(model.contact_pos[c]) for c in range(nc)], np.float64)
+    rb = np.asarray(rigid, np.float64)[:, cb]
+    return rb[..., 0:3] + quat_rotate(rb[..., 3:7], cp[None])
+
+
 def dynamics(model, root, q, qd, mass0=None, gz=-9.81):
     """(M[18,18], h[18]) at a state, float64."""
     M = np.zeros((18, 18))

@@ -39,6 +39,7 @@ class Cfg:
         self.c = c
         self.seed = int(c.seed)
         self.n = int(c.num_envs)
+        self.offset = int(getattr(c, "env_offset", 0))   # the shard's first global env id
         self.P = E.Params(dt=c.dt, cycle_time=c.cycle_time, target_joint_pos_scale=c.target_joint_pos_scale,
                           target_feet_height=c.target_feet_height, base_height_target=c.base_height_target,
                           min_dist=c.min_dist, max_dist=c.max_dist, tracking_sigma=c.tracking_sigma,
@@ -59,38 +60,44 @@ class Cfg:
 class PhiloxDraws:
     """The kernels' draw schedule (csrc/hg_common.h rng4 + csrc/hg_envlogic.hip / hg_physics.hip)."""
 
-    def __init__(self, seed, n):
-        self.seed, self.n = seed, n
+    def __init__(self, seed, n, offset=0):
+        # offset: the shard's first GLOBAL env id (data parallel, SURVEY 8e): every stream is keyed
+        # by the global id, as the kernels key theirs (cfg.env_offset + local index)
+        self.seed, self.n, self.off = seed, n, int(offset)
+
+    def _all(self):
+        return np.arange(self.n) + self.off
 
     def act_delay(self, step):                       # torch.rand((N, 1))           :624
-        return R.u01(R.rng4(self.seed, np.arange(self.n), step, 0, R.ACT_DELAY)[0])[:, None]
+        return R.u01(R.rng4(self.seed, self._all(), step, 0, R.ACT_DELAY)[0])[:, None]
 
     def act_noise(self, step, D):                    # torch.randn_like(actions)     :631
-        return R.normals(self.seed, np.arange(self.n), step, R.ACT_NOISE, D)
+        return R.normals(self.seed, self._all(), step, R.ACT_NOISE, D)
 
     def cmd(self, ids, step, salt):                  # 3 x torch_rand_float         :1024-1030
-        r = R.rng4(self.seed, ids, step, salt, R.CMD)
+        r = R.rng4(self.seed, np.asarray(ids) + self.off, step, salt, R.CMD)
         return R.u01(r[0]), R.u01(r[1]), R.u01(r[2])
 
     def push(self, step):                            # torch_rand_float (N,2), (N,3) :672-677
-        r0, r1 = R.rng4(self.seed, np.arange(self.n), step, 0, R.PUSH), R.rng4(self.seed, np.arange(self.n), step, 1, R.PUSH)
+        r0, r1 = R.rng4(self.seed, self._all(), step, 0, R.PUSH), R.rng4(self.seed, self._all(), step, 1, R.PUSH)
         return np.stack([R.u01(r0[0]), R.u01(r0[1])], 1), np.stack([R.u01(r0[2]), R.u01(r0[3]), R.u01(r1[0])], 1)
 
     def reset_dof(self, rid, counter, D):            # torch_rand_float (n, D)       :1044
         blocks = (D + 3) // 4
-        u = np.concatenate([np.stack(R.rng4(self.seed, rid, counter, b, R.RESET_DOF), 1) for b in range(blocks)], 1)
+        g = np.asarray(rid) + self.off
+        u = np.concatenate([np.stack(R.rng4(self.seed, g, counter, b, R.RESET_DOF), 1) for b in range(blocks)], 1)
         return R.u01(u[:, :D])
 
     def reset_root(self, rid, counter):              # torch_rand_float (n, 2)       :1062
-        rr = R.rng4(self.seed, rid, counter, 0, R.RESET_ROOT)
+        rr = R.rng4(self.seed, np.asarray(rid) + self.off, counter, 0, R.RESET_ROOT)
         return np.stack([R.u01(rr[0]), R.u01(rr[1])], 1)
 
     def terrain_level(self, rid, counter, maxl):     # torch.randint_like(levels, maxl) :1091
-        u = R.u01(R.rng4(self.seed, rid, counter, 0, R.TERRAIN)[0])
+        u = R.u01(R.rng4(self.seed, np.asarray(rid) + self.off, counter, 0, R.TERRAIN)[0])
         return np.minimum((u * f32(maxl)).astype(np.int64), maxl - 1)
 
     def obs_noise(self, step, width):                # torch.randn_like(obs_now)     :868
-        return R.normals(self.seed, np.arange(self.n), step, R.OBS_NOISE, width)
+        return R.normals(self.seed, self._all(), step, R.OBS_NOISE, width)
 
 
 class InjectedDraws:
@@ -141,7 +148,7 @@ class InjectedDraws:
 
 
 def _draws(cfg, draws):
-    return PhiloxDraws(cfg.seed, cfg.n) if draws is None else draws
+    return PhiloxDraws(cfg.seed, cfg.n, cfg.offset) if draws is None else draws
 
 
 def _rand_float(lo, hi, u):
@@ -290,7 +297,7 @@ def initial_state(cfg, env_origins, body_mass, frictions):
     S["episode_sums"] = {name: np.zeros(n, f32) for name in E.REWARD_NAMES}
     reset_envs(cfg, S, np.arange(n), 0)
     S["base_euler_xyz"] = E.euler_xyz(S["root_states"][:, 3:7])
-    noise = PhiloxDraws(cfg.seed, n).obs_noise(0, 47) if c.add_noise else None
+    noise = PhiloxDraws(cfg.seed, n, cfg.offset).obs_noise(0, 47) if c.add_noise else None
     o, p, ref = E.obs_frames(S, cfg.L, cfg.P, noise=noise)
     clip = f32(c.clip_observations)
     S["ref_dof_pos"] = ref

@@ -1,0 +1,152 @@
+"""The stated fp32 tolerance of one K_step against the f64 C reference physics.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ (the GPU parity tests), __graft_entry__.smoke() and
+scripts/ (calibration); never by the product package.
+
+A candidate step (the GPU's, or a CPU f32 stand-in) is compared with the f64 oracle element by
+element: |x - f64| <= K * yard + 2^-20 (1 + |f64|), where the fp32 yardstick `yard` is the larger
+of
+  * the f32 gap: max over an ensemble of CPU f32 steps (the state as given, and members - 1
+    copies with root / q / qd perturbed by a few ulp) of |f32 - f64|, and
+  * the conditioning spread: max over perturbations of the f64 inputs by ~1e-6 relative of the
+    change of the f64 output;
+the reported torque (the last substep's PD torque) also inherits the final q / qd tolerances
+through kp, kd.
+
+Contact steps at thousands of envs add rare DISCRETE events to this picture: a joint-friction
+row switching between stick and slip at its bound f dt, a contact candidate crossing the contact
+offset, a friction cone switching between inside and on the cone.  Any fp32 build flips a few of
+them somewhere among thousands of envs, each in different envs; the ensemble above cannot predict
+which.  `flip_null_rate` measures how often an independent fp32 build (a perturbed CPU f32
+member, judged against a yardstick built WITHOUT it) lands outside the element tolerance, so the
+GPU's count of such envs can be held to the fp32 rate instead of to zero (tests/test_gpu_parity.py).
+"""
+import numpy as np
+
+import physics_ref as P
+
+FIELDS = ("q", "qd", "root", "torques", "rigid")
+
+
+def ref_sim(hgcfg, model, S, precision, hf=None):
+    sim = P.RefSim(hgcfg, model, int(np.asarray(S["dof_pos"]).shape[0]), precision, heightfield=hf)
+    sim.root[:] = S["root_states"]
+    sim.q[:] = S["dof_pos"]
+    sim.qd[:] = S["dof_vel"]
+    sim.lam[:] = S["lambda"]
+    sim.mass0[:] = np.asarray(S["body_mass"])[:, 0]
+    sim.fric[:] = np.asarray(S["env_frictions"])[:, 0]
+    return sim
+
+
+def outputs(sim):
+    return {"q": sim.q, "qd": sim.qd, "root": sim.root, "torques": sim.torques, "rigid": sim.rigid}
+
+
+def f64_spread(hgcfg, model, S, a_ref, r64, fields, hf=None, trials=2, rel=1e-6, seed=1234):
+    """Local conditioning of the f64 step: max |f64(state perturbed by ~rel) - f64(state)|."""
+    rng = np.random.default_rng(seed)
+    base = outputs(r64)
+    spread = {f: np.zeros_like(base[f]) for f in fields}
+    for _ in range(trials):
+        Sp = dict(S)
+        for k in ("root_states", "dof_pos", "dof_vel"):
+            x = np.asarray(S[k]).astype(np.float64)
+            Sp[k] = x * (1 + rel * rng.standard_normal(x.shape)) + rel * 1e-3 * rng.standard_normal(x.shape)
+        rp = ref_sim(hgcfg, model, Sp, "f64", hf)
+        rp.step(a_ref)
+        o = outputs(rp)
+        for f in fields:
+            spread[f] = np.maximum(spread[f], np.abs(o[f] - base[f]))
+    return spread
+
+
+def f32_members(hgcfg, model, S, a_ref, fields, hf=None, members=3, rel=2.0 ** -22, seed=4321, first=0):
+    """Outputs of `members` CPU f32 steps: member 0 on the state as given, member m > 0 with
+    root / q / qd scaled by (1 + rel * N(0, 1)) from one seeded stream (`first` skips members of
+    the same stream, so members [first, first + members) of a longer ensemble come out equal)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for m in range(first + members):
+        Sp = dict(S)
+        if m:
+            for k in ("root_states", "dof_pos", "dof_vel"):
+                x = np.asarray(S[k])
+                Sp[k] = (x * (1 + rel * rng.standard_normal(x.shape))).astype(np.float32)
+        if m < first:
+            continue
+        r32 = ref_sim(hgcfg, model, Sp, "f32", hf)
+        r32.step(a_ref)
+        o = outputs(r32)
+        d = {f: o[f].copy() for f in fields}
+        d["dropped"] = r32.dropped.copy()
+        out.append(d)
+    return out
+
+
+def gap(members, r64, fields):
+    base = outputs(r64)
+    g = {f: np.zeros_like(base[f]) for f in fields}
+    for m in members:
+        for f in fields:
+            g[f] = np.maximum(g[f], np.abs(m[f] - base[f]))
+    return g
+
+
+def compare(cand, r64, gap32, spread, fields, kp, kd, K):
+    """Element tolerance and verdict of candidate outputs `cand` (dict of arrays).  Returns
+    (bad: field -> bool mask, headroom: field -> achieved max multiple of the yardstick beyond the
+    rounding term, tol: field -> tolerance)."""
+    base = outputs(r64)
+    tols, yards, rnds, headroom, bad = {}, {}, {}, {}, {}
+    for name in fields:
+        a64, x = base[name], np.asarray(cand[name], np.float64)
+        yard = np.maximum(gap32[name], spread[name])
+        rnd = 2.0 ** -20 * (1 + np.abs(a64))
+        tol = K * yard + rnd
+        if name == "torques" and "q" in tols and "qd" in tols:
+            # the reported torque is the LAST substep's, kp (target - q) - kd qd from the state after
+            # substep 9: it inherits that state's deviation, which the q / qd tolerances bound
+            tol = np.maximum(tol, kp * tols["q"] + kd * tols["qd"])
+            yard = np.maximum(yard, kp * yards["q"] + kd * yards["qd"])
+            rnd = np.maximum(rnd, kp * rnds["q"] + kd * rnds["qd"])
+        tols[name], yards[name], rnds[name] = tol, yard, rnd
+        excess = np.maximum(np.abs(x - a64) - rnd, 0.0)
+        ratio = np.where(yard > 0, excess / np.where(yard > 0, yard, 1.0), np.where(excess > 0, np.inf, 0.0))
+        headroom[name] = float(ratio.max())
+        bad[name] = np.abs(x - a64) > tol
+    return bad, headroom, tols
+
+
+def bad_envs(bad):
+    """Per-env flag: any element of any field outside its tolerance."""
+    flags = None
+    for m in bad.values():
+        f = m.reshape(m.shape[0], -1).any(axis=1)
+        flags = f if flags is None else (flags | f)
+    return flags
+
+
+def flip_null_rate(hgcfg, model, S, a_ref, r64, spread, fields, kp, kd, K, hf=None, members=3, candidates=4,
+                   seed=4321):
+    """How many envs an independent fp32 build puts outside the element tolerance: candidates
+    c = 0 .. candidates-1 are further perturbed CPU f32 members (the same seeded stream, past the
+    `members` the yardstick uses), each judged against the yardstick of the first `members`
+    (which excludes it) — the test's own yardstick, so the count is the fp32 rate the GPU is held
+    to.  Returns {"bad_envs": per-candidate counts, "max_err": field -> the largest |f32 - f64| in
+    those envs, "dropped_mismatch_envs": per-candidate count of envs whose dropped-row count
+    differs from the f64 step's}."""
+    ens = f32_members(hgcfg, model, S, a_ref, fields, hf, members=members, seed=seed)
+    g32 = gap(ens, r64, fields)
+    extra = f32_members(hgcfg, model, S, a_ref, fields, hf, members=candidates, seed=seed, first=members)
+    base = outputs(r64)
+    res = {"bad_envs": [], "max_err": {f: 0.0 for f in fields}, "dropped_mismatch_envs": []}
+    for cand in extra:
+        b, _, _ = compare(cand, r64, g32, spread, fields, kp, kd, K)
+        be = bad_envs(b)
+        res["bad_envs"].append(int(be.sum()))
+        res["dropped_mismatch_envs"].append(int((cand["dropped"] != r64.dropped).sum()))
+        for f in fields:
+            if be.any():
+                res["max_err"][f] = max(res["max_err"][f], float(np.abs(cand[f][be] - base[f][be]).max()))
+    return res

@@ -74,6 +74,64 @@ def test_sharded_envs_equal_single_instance(terrain):
 
 
 # ------------------------------------------------------------------------------------------------
+# config 4 (BASELINE configs[3]: 32768 envs = 8 x 4096 on the heightfield with DR, one rank per GPU)
+# at its per-rank workload on one GPU
+
+C4_RANKS, C4_ENVS = 8, 4096
+
+
+def test_config4_rank7_shard_contact_parity():
+    """Rank 7 of config 4: envs [28672, 32768) of a 32768-env job, heightfield + creation-time DR,
+    every draw keyed by the global env id.  After touchdown, one K_step against the C reference
+    physics at the stated tolerance on a contact step (>= 95 % of envs on the ground, >= 10 % on a
+    sloped triangle, rows dropped equal), then K_post against the pipeline oracle keyed by the same
+    global ids (forced resets, timeouts, command resample and a push)."""
+    _need_gpu()
+    from test_gpu_parity import TOUCHDOWN_STEPS, _assert_contact_step, _post_parity, _step_parity
+    r = C4_RANKS - 1
+    env = _env(C4_ENVS, r * C4_ENVS, C4_RANKS * C4_ENVS, terrain__mesh_type="heightfield")
+    assert env._hgcfg.env_offset == r * C4_ENVS and env._hgcfg.terrain_type == 1
+    torch.manual_seed(7)
+    for _ in range(TOUCHDOWN_STEPS):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    fr = env.env_frictions.cpu().numpy()
+    assert fr.min() >= 0.1 and fr.max() <= 2.0 and fr.std() > 0.3   # DR on: frictions drawn per env
+    r64 = _step_parity(env, 173)
+    _assert_contact_step(env, r64, sloped_min=0.10)
+    _post_parity(env, steps=0)
+
+
+def test_config4_eight_shards_equal_one_instance():
+    """The config-4 split on one GPU: eight shard instances of 4096 envs (env_offset 4096 r,
+    num_envs_total 32768) step bit-identically to ONE 32768-env instance, env for env, over 40
+    policy steps with resets (2 s episodes cut to 0.3 s), command resamples and pushes every 0.2 s,
+    on the heightfield with DR and observation noise: observations, privileged observations,
+    rewards, dones and the full state after every step."""
+    _need_gpu()
+    over = dict(terrain__mesh_type="heightfield", env__episode_length_s=0.3, commands__resampling_time=0.1,
+                domain_rand__push_interval_s=0.2)
+    n, R = C4_ENVS, C4_RANKS
+    whole = _env(R * n, 0, R * n, **over)
+    shards = [_env(n, r * n, R * n, **over) for r in range(R)]
+    g = torch.Generator(device="cpu").manual_seed(4)
+    resets = 0
+    for step in range(40):
+        a = (torch.randn(R * n, 12, generator=g) * 0.5).to("cuda:0")
+        ow, pw, rw, dw, _ = whole.step(a)
+        outs = [s.step(a[r * n:(r + 1) * n].contiguous()) for r, s in enumerate(shards)]
+        resets += int(dw.sum().item())
+        for name, x_w, xs in (("obs", ow, [o[0] for o in outs]), ("priv", pw, [o[1] for o in outs]),
+                              ("rew", rw, [o[2] for o in outs]), ("reset", dw, [o[3] for o in outs])):
+            assert torch.equal(x_w, torch.cat(xs)), f"{name} differs at step {step}"
+        for k in _STATE:
+            assert torch.equal(getattr(whole, k), torch.cat([getattr(s, k) for s in shards])), f"{k} at step {step}"
+    assert resets >= R * n, resets  # every env went through at least one reset on average
+    dim = list(whole._sums.shape).index(R * n)
+    assert torch.equal(whole._sums, torch.cat([s._sums for s in shards], dim=dim))
+    assert torch.equal(whole.rows_dropped, torch.cat([s.rows_dropped for s in shards]))
+
+
+# ------------------------------------------------------------------------------------------------
 # world_size 2 update vs the single process on the concatenated batch
 
 T_STEPS, N_LOCAL, WORLD = 24, 64, 2
@@ -119,10 +177,20 @@ def _worker(rank, world, port, out_path, rccl=False):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     elif rccl:
         os.environ["HG_DP_FORCE"] = "1"
-        if rccl == "eager":  # the two-graph form with the eager all-reduce between the replays
-            os.environ["HG_DP_GRAPH_COLLECTIVE"] = "0"
+        # "eager": the default two-graph form with the eager all-reduce between the replays;
+        # "graph": the opt-in one-graph form with the collective captured; "capture_fails": the
+        # opt-in form whose capture of the collective raises -> the in-process fallback
+        os.environ["HG_DP_GRAPH_COLLECTIVE"] = "0" if rccl == "eager" else "1"
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         assert dist.get_backend() == "nccl"
+        if rccl == "capture_fails":
+            real_all_reduce = dist.all_reduce
+
+            def all_reduce(t, *a, **k):
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("injected: the collective refuses stream capture")
+                return real_all_reduce(t, *a, **k)
+            dist.all_reduce = all_reduce
     import bench
     from humanoid.algo.ppo import ActorCritic, PPO
     dev = "cuda:0"
@@ -175,6 +243,8 @@ def _worker(rank, world, port, out_path, rccl=False):
     flat = torch.cat([p.detach().reshape(-1) for p in ac.parameters()]).cpu()
     torch.save({"flat": flat, "lr": float(ppo.learning_rate), "losses": losses, "graphed": ppo._graphs is not None,
                 "whole": bool(getattr(ppo, "_whole", False)), "calls": calls[0], "dp": bool(ppo._dp),
+                "update_graph": ppo.update_graph, "capture_error": ppo.capture_error,
+                "collectives": ppo.collectives_per_update(),
                 "backend": dist.get_backend() if dist.is_initialized() else None,
                 "accumulate_grad_warnings": sum("AccumulateGrad" in str(w.message) for w in caught)}, out_path)
     if dist.is_initialized():
@@ -232,15 +302,17 @@ def test_dp_graphed_update_matches_single_process(tmp_path):
         assert abs(a - float(b)) <= 1e-5 * max(1.0, abs(float(b)))
 
 
-@pytest.mark.parametrize("mode", ["graph", "eager"])
+@pytest.mark.parametrize("mode", ["graph", "eager", "capture_fails"])
 def test_rccl_update_matches_single_process(tmp_path, mode):
     """The RCCL code path executed: a world-size-1 "nccl" group with the multi-rank update forced
     (HG_DP_FORCE=1) — parameter broadcast, the flat gradient buffer with the KL slot, the
     advantage-statistics all-reduce, and per minibatch backward -> all_reduce on RCCL -> step:
-    mode "graph" (the default) captures the collective inside the ONE update
-    graph; mode "eager" is the two-graph form with the all-reduce between the replays.  At world
+    mode "eager" is the default two-graph form with the all-reduce between the replays; mode
+    "graph" (HG_DP_GRAPH_COLLECTIVE=1) captures the collective inside the ONE update graph; mode
+    "capture_fails" is that opt-in with the collective raising under capture:
+    the update must fall back in the same process to the two-graph form and say so.  At world
     size 1 the all-reduce is the identity, so the parameters must equal the single-process
-    update bit for bit."""
+    update bit for bit in every mode."""
     _need_gpu()
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -253,6 +325,9 @@ def test_rccl_update_matches_single_process(tmp_path, mode):
         runs[name] = torch.load(tmp_path / f"{name}.pt", weights_only=True)
     R, S = runs["rccl"], runs["single"]
     assert R["backend"] == "nccl" and R["dp"] and R["graphed"] and R["whole"] == (mode == "graph")
+    assert R["update_graph"] == ("one" if mode == "graph" else "two")
+    assert (R["capture_error"] is not None) == (mode == "capture_fails"), R["capture_error"]
+    assert R["collectives"] == 2 * 4 + 1 and S["collectives"] == 0 and S["update_graph"] == "one"
     assert S["backend"] is None and not S["dp"] and S["whole"]
     assert R["calls"] == S["calls"] == 3
     assert R["lr"] == S["lr"]

@@ -206,64 +206,22 @@ def _post_parity(env, steps=3):
         np.testing.assert_allclose(gpu(env._sums[k]), S["episode_sums"][n], rtol=2e-4, atol=1e-6, err_msg=n)
 
 
+def _hf(env):
+    return env.height_samples.cpu().numpy() if getattr(env, "height_samples", None) is not None else None
+
+
 def _ref_sim(env, S, precision):
-    import physics_ref as P
-    hf = env.height_samples.cpu().numpy() if getattr(env, "height_samples", None) is not None else None
-    sim = P.RefSim(env._hgcfg, env._model, env.num_envs, precision, heightfield=hf)
-    sim.root[:] = S["root_states"]
-    sim.q[:] = S["dof_pos"]
-    sim.qd[:] = S["dof_vel"]
-    sim.lam[:] = S["lambda"]
-    sim.mass0[:] = S["body_mass"][:, 0]
-    sim.fric[:] = S["env_frictions"][:, 0]
-    return sim
+    import step_tolerance as ST
+    return ST.ref_sim(env._hgcfg, env._model, S, precision, _hf(env))
 
 
-def _ref_spread(env, S, a_ref, fields, trials=2, rel=1e-6):
-    """Local conditioning of the reference step: max |f64(state perturbed by ~rel) - f64(state)|
-    per output element over a few seeded perturbations of root / q / qd.  Contact dynamics are
-    stiff where a foot is at zero separation, so fp32-rounding-sized input differences can move
-    an output far more than the CPU-f32-vs-f64 gap alone predicts; the parity tolerance scales
-    with this spread as well."""
-    base = _ref_sim(env, S, "f64")
-    base.step(a_ref)
-    rng = np.random.default_rng(1234)
-    spread = {f: np.zeros_like(getattr(base, f)) for f in fields}
-    for _ in range(trials):
-        Sp = dict(S)
-        for k in ("root_states", "dof_pos", "dof_vel"):
-            x = S[k].astype(np.float64)
-            Sp[k] = x * (1 + rel * rng.standard_normal(x.shape)) + rel * 1e-3 * rng.standard_normal(x.shape)
-        rp = _ref_sim(env, Sp, "f64")
-        rp.step(a_ref)
-        for f in fields:
-            spread[f] = np.maximum(spread[f], np.abs(getattr(rp, f) - getattr(base, f)))
-    return spread
-
-
+# members of the CPU f32 ensemble behind the yardstick (oracle/step_tolerance.py: the state as
+# given + members - 1 copies perturbed by a few ulp); at 4096 envs a single CPU draw under-estimates
+# the tail (13 of 49152 torque elements in the first 4096-env run)
 F32_STEP_ENSEMBLE = 3
-
-
-def _f32_ensemble_gap(env, S, a_ref, r64, fields, members=F32_STEP_ENSEMBLE, rel=2.0 ** -22):
-    """The fp32 yardstick of one step: max over an ensemble of CPU f32 steps (the state as given,
-    and members - 1 copies with root / q / qd perturbed by a few ulp) of |f32 - f64| per element.
-    One CPU f32 run is a single draw of how fp32 rounding inside the solve (PGS sweeps, the
-    friction-row clamps of the ankle joints) lands; the GPU, rounding in other orders (FMA
-    contraction, MFMA accumulation, v_rsq), is another draw — at 4096 envs a single CPU draw
-    under-estimates the tail (13 of 49152 torque elements in the first 4096-env run)."""
-    rng = np.random.default_rng(4321)
-    gap = {f: np.zeros_like(getattr(r64, f)) for f in fields}
-    for m in range(members):
-        Sp = dict(S)
-        if m:
-            for k in ("root_states", "dof_pos", "dof_vel"):
-                x = S[k]
-                Sp[k] = (x * (1 + rel * rng.standard_normal(x.shape))).astype(np.float32)
-        r32 = _ref_sim(env, Sp, "f32")
-        r32.step(a_ref)
-        for f in fields:
-            gap[f] = np.maximum(gap[f], np.abs(getattr(r32, f) - getattr(r64, f)))
-    return gap
+# independent f32 builds judged against that yardstick (excluded from it): their count of envs
+# outside the element tolerance is the fp32 discrete-event rate the GPU's count is held to
+F32_NULL_CANDIDATES = 4
 
 
 def _step_only(env, actions, counter):
@@ -281,7 +239,7 @@ def _step_only(env, actions, counter):
 STEP_TOL_K = 12.0
 
 
-def _report_headroom(env, headroom):
+def _report_headroom(env, headroom, key="ratio"):
     """Append the achieved max |gpu - f64| / max(gap32, spread) per field (beyond the rounding
     term) of one _step_parity call to $HG_TOL_REPORT (JSON lines), when set."""
     path = os.environ.get("HG_TOL_REPORT")
@@ -290,17 +248,24 @@ def _report_headroom(env, headroom):
     import json
     test = os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0]
     with open(path, "a") as f:
-        f.write(json.dumps({"test": test, "envs": env.num_envs, "k": STEP_TOL_K, "ratio": headroom}) + "\n")
+        f.write(json.dumps({"test": test, "envs": env.num_envs, "k": STEP_TOL_K, key: headroom}) + "\n")
 
 
 def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), scale=0.5, actions=None):
     """One K_step (prologue + 10 substeps + rigid states) from the env's current state vs the C
     reference simulator (f64, f32) on the identical state and preprocessed actions.  Stated fp32
-    tolerance: STEP_TOL_K (12) x the larger of the CPU f32-vs-f64 gap and the local conditioning
-    spread of the f64 step, plus fp32 rounding (2^-20 relative, ~8 ulp); no absolute floor
-    (DESIGN.md section 4).  The achieved multiple per field goes to $HG_TOL_REPORT.
-    Returns the reference f64 sim."""
+    tolerance (oracle/step_tolerance.py): per element, STEP_TOL_K (12) x the
+    larger of the CPU f32-vs-f64 gap and the local conditioning spread of the f64 step, plus fp32
+    rounding (2^-20 relative, ~8 ulp), no absolute floor.  On contact steps at thousands of envs,
+    rare discrete events (a joint-friction row between stick and slip, a contact crossing the
+    offset) put any fp32 build outside that bound in a few envs; the count of envs with an element
+    outside is therefore held to the fp32 rate measured on the same state — at most twice the mean
+    count of F32_NULL_CANDIDATES independent CPU f32 builds judged against the same yardstick — and
+    their deviations to 4 x the largest such a build shows there (zero envs whenever those builds
+    have none).  Rows dropped over the budget: equal env for env.  The achieved multiples and the
+    counts go to $HG_TOL_REPORT.  Returns the reference f64 sim."""
     import pipeline_ref as PR
+    import step_tolerance as ST
     S, _, _ = snapshot(env)
     cfg = _oracle_cfg(env)
     if actions is None:
@@ -310,45 +275,82 @@ def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), s
     _step_only(env, actions, counter)
     g = lambda t: t.detach().cpu().numpy()  # noqa: E731
     np.testing.assert_allclose(g(env.actions), a_ref, rtol=1e-5, atol=1e-6)
-    r64 = _ref_sim(env, S, "f64")
+    hc, model, hf = env._hgcfg, env._model, _hf(env)
+    r64 = ST.ref_sim(hc, model, S, "f64", hf)
     r64.step(a_ref)
-    gap32 = _f32_ensemble_gap(env, S, a_ref, r64, fields)
-    sp = _ref_spread(env, S, a_ref, fields)
+    gap32 = ST.gap(ST.f32_members(hc, model, S, a_ref, fields, hf, members=F32_STEP_ENSEMBLE), r64, fields)
+    sp = ST.f64_spread(hc, model, S, a_ref, r64, fields, hf)
     gpu = {"q": g(env.dof_pos), "qd": g(env.dof_vel), "root": g(env.root_states), "torques": g(env.torques),
            "rigid": g(env.rigid_state)}
-    tols, yards, rnds, headroom, fails = {}, {}, {}, {}, []
-    kp = np.array([env._hgcfg.kp[j] for j in range(12)])
-    kd = np.array([env._hgcfg.kd[j] for j in range(12)])
-    for name in fields:
-        a64, a32, x = getattr(r64, name), gap32[name], gpu[name]
-        yard = np.maximum(a32, sp[name])       # the fp32 yardstick: max(f32 gap, conditioning spread)
-        rnd = 2.0 ** -20 * (1 + np.abs(a64))   # fp32 rounding, ~8 ulp
-        tol = STEP_TOL_K * yard + rnd
-        if name == "torques" and "q" in tols and "qd" in tols:
-            # the reported torque is the LAST substep's, kp (target - q) - kd qd from the state
-            # after substep 9: it inherits that state's deviation, which the final-state tolerances
-            # of q / qd bound (the CPU f32 draws share the oracle's summation structure, so their
-            # own torque gap under-states the GPU's, whose solve rounds in other orders)
-            tol = np.maximum(tol, kp * tols["q"] + kd * tols["qd"])
-            yard = np.maximum(yard, kp * yards["q"] + kd * yards["qd"])
-            rnd = np.maximum(rnd, kp * rnds["q"] + kd * rnds["qd"])
-        tols[name], yards[name], rnds[name] = tol, yard, rnd
-        # achieved multiple of the yardstick: the error beyond the rounding term over the yardstick
-        excess = np.maximum(np.abs(x - a64) - rnd, 0.0)
-        ratio = np.where(yard > 0, excess / np.where(yard > 0, yard, 1.0), np.where(excess > 0, np.inf, 0.0))
-        headroom[name] = float(ratio.max())
-        bad = np.abs(x - a64) > tol
-        detail = "; ".join(f"{tuple(int(i) for i in ix)} gpu {x[tuple(ix)]:+.6f} f64 {a64[tuple(ix)]:+.6f} "
-                           f"f32 gap {a32[tuple(ix)]:.2e} spread {sp[name][tuple(ix)]:.2e}"
-                           for ix in np.argwhere(bad)[:6])
-        if bad.any():
-            fails.append(f"{name}: {bad.sum()} mismatches, max err {np.abs(x - a64).max()}: {detail}")
-    _report_headroom(env, headroom)
+    kp = np.array([hc.kp[j] for j in range(12)])
+    kd = np.array([hc.kd[j] for j in range(12)])
+    bad, headroom, tols = ST.compare(gpu, r64, gap32, sp, fields, kp, kd, STEP_TOL_K)
+    outl = ST.bad_envs(bad)
+    base = ST.outputs(r64)
+    report = {"ratio": headroom, "outlier_envs": int(outl.sum())}
+    fails = []
+    if outl.any():
+        null = ST.flip_null_rate(hc, model, S, a_ref, r64, sp, fields, kp, kd, STEP_TOL_K, hf=hf,
+                                 members=F32_STEP_ENSEMBLE, candidates=F32_NULL_CANDIDATES)
+        allowed = int(np.ceil(2.0 * np.mean(null["bad_envs"])))
+        err = {f: float(np.abs(gpu[f][outl] - base[f][outl]).max()) for f in fields}
+        report.update(null_outlier_envs=null["bad_envs"], allowed_outlier_envs=allowed, outlier_max_err=err,
+                      null_outlier_max_err=null["max_err"])
+        if outl.sum() > allowed:
+            fails.append(f"{int(outl.sum())} envs outside the element tolerance, fp32 rate allows {allowed} "
+                         f"(independent CPU f32 builds: {null['bad_envs']})")
+        for f in fields:
+            if err[f] > 4.0 * null["max_err"][f]:
+                fails.append(f"{f}: outlier deviation {err[f]:.3e} > 4 x the f32 builds' {null['max_err'][f]:.3e}")
+        if fails:
+            for name in fields:
+                x, a64 = gpu[name], base[name]
+                detail = "; ".join(f"{tuple(int(i) for i in ix)} gpu {x[tuple(ix)]:+.6f} f64 {a64[tuple(ix)]:+.6f} "
+                                   f"f32 gap {gap32[name][tuple(ix)]:.2e} spread {sp[name][tuple(ix)]:.2e}"
+                                   for ix in np.argwhere(bad[name])[:6])
+                if bad[name].any():
+                    fails.append(f"{name}: {bad[name].sum()} mismatches, max err {np.abs(x - a64).max()}: {detail}")
+    _report_headroom(env, report, key="step")
     assert not fails, " | ".join(fails)
     assert not r64.nonfinite.any() and not g(env.nonfinite_count).any()
     # rows / contact points over the budget: the same count per env
     np.testing.assert_array_equal(g(env.rows_dropped - dropped0), r64.dropped)
     return r64
+
+
+# policy steps before a compared contact step: from the 0.95 m spawn the first foot lands at step 9
+# and every env is on the ground by step 12 (oracle, 0.3 randn actions)
+TOUCHDOWN_STEPS = 24
+
+
+def _assert_contact_step(env, r64, sloped_min=None):
+    """The compared K_step is a contact step: >= 95 % of envs hold a ground
+    contact with a positive normal impulse after the step, on the GPU and in the oracle (warm-start
+    slots 3c of the ground candidates, the last substep's impulses); with `sloped_min`, at least
+    that fraction of envs has such a contact on a heightfield triangle whose normal has z < 0.995
+    (the terrain, not a flat patch, is in the compared step).  Returns the per-env statistics."""
+    N = _hg()
+    import physics_ref as P
+    nc = N.HG_MAX_CONTACTS
+    lam_gpu = env._view(N.T["CONTACT_LAMBDA"]).cpu().numpy()[:, 0:3 * nc:3]
+    lam_ref = r64.lam[:, 0:3 * nc:3]
+    on_gpu, on_ref = (lam_gpu > 0).any(axis=1), (lam_ref > 0).any(axis=1)
+    stats = {"envs": env.num_envs, "ground_contact_gpu": float(on_gpu.mean()),
+             "ground_contact_oracle": float(on_ref.mean()),
+             "contacts_per_env_gpu": float((lam_gpu > 0).sum(axis=1).mean())}
+    if sloped_min is not None:
+        hf = env.height_samples.cpu().numpy()
+        x = P.ground_candidates(env._model, env.rigid_state.cpu().numpy())
+        _, nrm = P.ground(env._hgcfg, hf, x[..., 0], x[..., 1])
+        steep = nrm[..., 2] < 0.995
+        stats["sloped_contact_gpu"] = float(((lam_gpu > 0) & steep).any(axis=1).mean())
+        stats["sloped_contact_oracle"] = float(((lam_ref > 0) & steep).any(axis=1).mean())
+    print("contact step:", stats)
+    _report_headroom(env, stats, key="contact")
+    assert stats["ground_contact_gpu"] >= 0.95 and stats["ground_contact_oracle"] >= 0.95, stats
+    if sloped_min is not None:
+        assert stats["sloped_contact_gpu"] >= sloped_min and stats["sloped_contact_oracle"] >= sloped_min, stats
+    return stats
 
 
 def test_step_physics_parity(physics_env):
@@ -376,11 +378,14 @@ def bench_terrain_env():
 @pytest.mark.parametrize("which", ["plane", "heightfield"])
 def test_step_and_post_parity_4096_envs(which, request):
     """K_step and K_post against the oracle at the bench's 4096 envs (config 2 plane, config 3
-    heightfield): the same stated tolerances as the 64-env tests, every env checked."""
+    heightfield): the same stated tolerances as the 64-env tests, every env checked, on a contact
+    step (>= 95 % of envs on the ground, >= 10 % on a sloped heightfield triangle; rows dropped
+    equal env for env)."""
     env = request.getfixturevalue("bench_env" if which == "plane" else "bench_terrain_env")
-    for _ in range(4):
+    for _ in range(TOUCHDOWN_STEPS):  # past touchdown: the compared step resolves ground contact
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
-    _step_parity(env, 131)
+    r64 = _step_parity(env, 131)
+    _assert_contact_step(env, r64, sloped_min=0.10 if which == "heightfield" else None)
     _post_parity(env, steps=0)
 
 
@@ -861,7 +866,8 @@ def test_config5_bf16_policy_fp16_storage_push_curriculum():
 
 def test_config5_8192_envs_per_rank():
     """Config 5 at its per-rank size (65536 envs on 8 GPUs = 8192 per rank):
-    one K_step + K_post against the oracle at the stated tolerances with the push curriculum
+    one K_step (a contact step, after touchdown) + K_post against the oracle at the stated
+    tolerances with the push curriculum
     ramped to its final bounds, then two runner iterations of the bf16 policy with fp16
     observation storage: finite losses, finite parameters that moved."""
     _need_gpu()
@@ -869,9 +875,10 @@ def test_config5_8192_envs_per_rank():
     import bench
     env = _make_env(8192, domain_rand__push_curriculum=True)
     env.update_push_curriculum(10 ** 6)
-    for _ in range(4):
+    for _ in range(TOUCHDOWN_STEPS):
         env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
-    _step_parity(env, 211)
+    r64 = _step_parity(env, 211)
+    _assert_contact_step(env, r64)
     _post_parity(env, steps=0)
     runner = OnPolicyRunner(env, bench.train_cfg(24, "bf16", "fp16"), log_dir=None, device="cuda:0")
     assert runner.alg.storage.privileged_observations.dtype == torch.float16
