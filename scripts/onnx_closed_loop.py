@@ -40,10 +40,38 @@ def cause_slots(js, model):
     return {"base_ground": corners, "hand_leg": hand, "box_thigh": box}
 
 
+DOF_NAMES = ("l_roll", "l_yaw", "l_pitch", "l_knee", "l_ankle", "l_ankle_roll",
+             "r_roll", "r_yaw", "r_pitch", "r_knee", "r_ankle", "r_ankle_roll")
+
+
+def signed_policy(net, sign):
+    """The actor with joint sign conventions (oracle/sim2sim_ref.Sim2SimRef joint_sign, identity
+    permutation): the policy's joint j is the robot's joint j times sign[j] — its q, qd and last
+    action observation columns of every stacked 47-wide frame and its action."""
+    import torch
+    s = torch.as_tensor(np.asarray(sign, np.float32))
+    col = torch.ones(47)
+    for off in (5, 17, 29):
+        col[off:off + 12] = s
+    col = col.repeat(15)
+
+    class Signed(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.net = net
+            self.register_buffer("col", col)
+            self.register_buffer("sign", s)
+
+        def forward(self, x):
+            return self.net(x * self.col) * self.sign
+    return Signed()
+
+
 def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0, ensemble=3, device="cuda:0",
-            self_collisions=True):
+            self_collisions=True, joint_sign=None):
     """GPU sim2sim and the CPU oracle (f64, plus an fp32 ensemble as the divergence yardstick)
-    from the GPU env's initial state.  Returns a dict of numpy arrays / numbers."""
+    from the GPU env's initial state; ``joint_sign`` (12 x +-1): the actor's joint sign convention
+    (scripts/onnx_fixed_base.py derives one).  Returns a dict of numpy arrays / numbers."""
     import torch
     import sim2sim_ref as SR
     from humanoid import _native as N
@@ -60,7 +88,10 @@ def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0,
     hc, model = env._hgcfg, env._model
     cyc = env.cfg.rewards.cycle_time
     slots = cause_slots(env._model_js, model)
-    summary, traces = S2.run(S2.mlp_from_weights(W).to(device).eval(), profile, cmds, duration, envs_per_command,
+    policy = S2.mlp_from_weights(W)
+    if joint_sign is not None:
+        policy = signed_policy(policy, joint_sign)
+    summary, traces = S2.run(policy.to(device).eval(), profile, cmds, duration, envs_per_command,
                              device, env=env, record_q=True)
     q_gpu = traces["q_all"]
     per_cmd = np.repeat(cmds, envs_per_command, axis=0)
@@ -73,7 +104,7 @@ def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0,
             qd = qd * (1 + pert * rng.standard_normal(qd.shape))
         dt = np.float64 if prec == "f64" else np.float32
         sim = SR.Sim2SimRef(hc, model, SR.mlp(W, dt), root, q, qd, init["mass"], init["fric"], per_cmd,
-                            precision=prec, cycle_time=cyc, lam=init["lam"], cause_slots=slots)
+                            precision=prec, cycle_time=cyc, lam=init["lam"], cause_slots=slots, joint_sign=joint_sign)
         qs = []
         for _ in range(steps):
             sim.step()
@@ -109,6 +140,7 @@ def compare(profile="urdf", commands=COMMANDS, envs_per_command=8, duration=3.0,
     gpu_lin = np.array([c["lin_vel_error"] for c in summary["commands"] for _ in range(envs_per_command)])
     gpu_yaw = np.array([c["yaw_rate_error"] for c in summary["commands"] for _ in range(envs_per_command)])
     return dict(profile=profile, self_collisions=bool(self_collisions), envs=n, steps=steps, duration_s=duration,
+                joint_sign=None if joint_sign is None else [float(x) for x in joint_sign],
                 gpu=stats(alive_gpu, gpu_lin, gpu_yaw),
                 oracle_f64=stats(ref64["fall_step"], ref64["lin_vel_error"], ref64["yaw_rate_error"]),
                 oracle_f32=[stats(e[0]["fall_step"], e[0]["lin_vel_error"], e[0]["yaw_rate_error"]) for e in ens],
@@ -126,14 +158,22 @@ def main():
     ap.add_argument("--envs_per_command", type=int, default=16)
     ap.add_argument("--ensemble", type=int, default=2)
     ap.add_argument("--no-self-collisions", action="store_true", help="ablation: no self-collision pairs")
+    ap.add_argument("--flip", default="", help="comma-separated joints the actor drives with the opposite sign "
+                                                  "(scripts/onnx_fixed_base.py), e.g. l_yaw,l_knee,r_yaw,r_pitch,r_ankle")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r3_onnx"))
     a = ap.parse_args()
+    sign = None
+    if a.flip:
+        sign = np.ones(12)
+        for nm in a.flip.split(","):
+            sign[DOF_NAMES.index(nm)] = -1.0
     import physics_ref as P
     P.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
     r = compare(a.profile, COMMANDS, a.envs_per_command, a.duration, a.ensemble,
-                self_collisions=not a.no_self_collisions)
+                self_collisions=not a.no_self_collisions, joint_sign=sign)
     os.makedirs(a.out, exist_ok=True)
-    path = os.path.join(a.out, f"onnx_closed_loop_{a.profile}{'_noself' if a.no_self_collisions else ''}.json")
+    path = os.path.join(a.out, f"onnx_closed_loop_{a.profile}{'_noself' if a.no_self_collisions else ''}"
+                               f"{'_signs' if sign is not None else ''}.json")
     with open(path, "w") as f:
         json.dump(r, f, indent=1)
     for name in ("gpu", "oracle_f64"):

@@ -85,13 +85,17 @@ def variants():
     return V
 
 
-def build(v, n):
+def build(v, n, fixed_base=False):
     """(hc, model, default pose [12]) of a variant: the sim2sim URDF profile (humanoid.scripts.
-    sim2sim.make_cfg) with the variant's physics changes, compiled as XBotLFreeEnv.create_sim does."""
+    sim2sim.make_cfg) with the variant's physics changes, compiled as XBotLFreeEnv.create_sim does.
+    fixed_base: the base link held in place (asset.fix_base_link; no ground contact is generated
+    for a fixed base) and every self-collision pair dropped — the robot suspended in free space
+    (scripts/onnx_fixed_base.py)."""
     from humanoid import _native as N
     from humanoid.envs.custom.humanoid_env import build_hg_cfg
     from humanoid.scripts.sim2sim import make_cfg
-    cfg = make_cfg("urdf", n, 30.0, self_collisions=v.get("self_collisions", True))
+    cfg = make_cfg("urdf", n, 30.0, self_collisions=v.get("self_collisions", True) and not fixed_base)
+    cfg.asset.fix_base_link = bool(fixed_base)
     if "default" in v:
         names = N.model_names(N.load_model()[1])[1]
         angles = dict(cfg.init_state.default_joint_angles)  # a class-level dict: never mutate it

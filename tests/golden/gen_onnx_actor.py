@@ -8,6 +8,10 @@ into tests/golden/onnx_actor.npz as W0, b0, ..., W3, b3 (nn.Linear layout [out, 
 activation between layers.  The GPU box never reads the reference; the tests load the npz.
 
 Usage (build container only):  python tests/golden/gen_onnx_actor.py
+       python tests/golden/gen_onnx_actor.py <policy.onnx> <out.npz> "<source note>"
+The second form makes the same fixture from a policy exported by THIS build (humanoid.utils.onnx_io,
+scripts/train_eval.sh -> gpurun_out/train_eval/policy.onnx): tests/golden/hg_trained_actor.npz, the
+positive control of scripts/onnx_fixed_base.py.
 """
 import os
 import sys
@@ -20,9 +24,9 @@ sys.path.insert(0, os.path.join(REPO, "humanoid-gym-with-comments_amd"))
 SRC = "/root/reference/humanoid/OnnxTest.onnx"
 
 
-def main():
+def main(src=SRC, dst=os.path.join(HERE, "onnx_actor.npz"), note=None):
     from humanoid.utils.onnx_io import read_onnx_graph
-    g = read_onnx_graph(SRC)
+    g = read_onnx_graph(src)
     out, cur, k, acts = {}, g["inputs"][0], 0, []
     for nd in g["nodes"]:
         assert nd["input"][0] == cur, "single chain"
@@ -41,10 +45,13 @@ def main():
         cur = nd["output"][0]
     assert cur == g["outputs"][0] and k == 4 and acts == ["elu"] * 3
     out["activations"] = np.array(acts)
-    out["source"] = np.array("humanoid/OnnxTest.onnx (reference), opset %d" % g["opset"])
-    np.savez_compressed(os.path.join(HERE, "onnx_actor.npz"), **out)
+    out["source"] = np.array(note or "humanoid/OnnxTest.onnx (reference), opset %d" % g["opset"])
+    np.savez_compressed(dst, **out)
     print({k: v.shape for k, v in out.items()})
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    else:
+        main()

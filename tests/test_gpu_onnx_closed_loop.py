@@ -42,3 +42,35 @@ def test_onnx_actor_closed_loop_gpu_vs_oracle(profile):
         assert cg["falls"] == co["falls"], (cg, co)
         tol = max(0.25, 0.15 * co["mean_fall_time_s"])
         assert abs(cg["mean_fall_time_s"] - co["mean_fall_time_s"]) <= tol, (cg, co)
+
+
+def test_onnx_actor_under_derived_signs_gpu_vs_oracle():
+    """The actor with the joint signs the suspended-robot probe derives (scripts/onnx_fixed_base.py:
+    left / right hip yaw, left knee, right hip pitch, right ankle pitch driven with the opposite
+    sign) stands and walks on hg_sim as on the CPU oracle: the same falls per command (at most one of
+    8 envs in 3 s), and the GPU's closed-loop joint trajectory within 2 x the fp32 ensemble's
+    divergence from f64 (+1e-4 rad) while the envs stand."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import onnx_closed_loop as OC
+    sign = np.ones(12)
+    for n in ("l_yaw", "l_knee", "r_yaw", "r_pitch", "r_ankle"):
+        sign[OC.DOF_NAMES.index(n)] = -1.0
+    r = OC.compare("urdf", envs_per_command=2, duration=3.0, ensemble=2, joint_sign=sign)
+    falls = 0
+    for cg, co in zip(r["gpu"], r["oracle_f64"]):
+        print("cmd", cg["command"][0], "GPU falls", cg["falls"], "|v - cmd|", round(cg["lin_vel_error"], 3),
+              "oracle falls", co["falls"], "|v - cmd|", round(co["lin_vel_error"], 3))
+        assert cg["falls"] == co["falls"], (cg, co)
+        tol = max(0.25, 0.15 * co["mean_fall_time_s"])
+        assert abs(cg["mean_fall_time_s"] - co["mean_fall_time_s"]) <= tol, (cg, co)
+        falls += cg["falls"]
+    # under the trained conventions every env falls within 0.5 s (the test above); here at most one
+    # of the 8 within 3 s (the 20 s run: profiles/r5_onnx_fixed_base/onnx_closed_loop_urdf_signs.json)
+    assert falls <= 1, falls
+    div_gpu, div_f32 = np.array(r["div_gpu"]), np.array(r["div_f32"])
+    ok = ~np.isnan(div_gpu)
+    run_gpu = np.maximum.accumulate(div_gpu[ok])
+    run_f32 = np.maximum.accumulate(div_f32[ok])
+    bad = run_gpu > 2.0 * run_f32 + 1e-4
+    assert not bad.any(), f"first excess at step {int(np.argmax(bad))}: {run_gpu[bad][0]:.3e} vs {run_f32[bad][0]:.3e}"
