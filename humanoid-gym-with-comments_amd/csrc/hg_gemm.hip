@@ -171,6 +171,78 @@ __device__ __forceinline__ void mma_chunk(const float* __restrict__ As, const fl
 
 // MODE 0: forward (B k-contiguous [N, K]; + bias, ELU if ELU).  MODE 1: input grad (B n-contiguous
 // [K, N]; ELU backward from Y when ELU; column partials when colpart is non-null).
+// Epilogues shared by the MFMA GEMMs.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2) +
+// 4h, column i.  Round 5: every global load an epilogue needs is issued up front and
+// unconditionally (clamped addresses) — the bias once per column, Y sixteen rows at a time — so no
+// wait on a load lands between two stores.  Written as before (load inside the store guard), the
+// compiler waited for each Y load right before its store (32-64 dependent HBM round trips per wave
+// in the input-gradient kernels) and re-waited vmcnt(0) for the bias before every store of the
+// forward (stores count on that counter too).  Values, stores and the column-sum order unchanged.
+template <int TM, int TN, bool ELU, bool BIAS>
+__device__ __forceinline__ void epi_forward(const f32x16 (&acc)[TM][TN], const GemmArgs& g, float* __restrict__ C,
+                                            int64_t row0, int col0, int i, int h) {
+  const int64_t mmax = g.M - 1;
+  const int nmax = g.N - 1;
+#pragma unroll
+  for (int n = 0; n < TN; n++) {
+    const int cidx = col0 + 32 * n + i;
+    float bc = 0.f;
+    if (BIAS) bc = g.bias[min(cidx, nmax)];
+    asm volatile("" : "+v"(bc));  // the bias load retires here, once
+    if (cidx > nmax) continue;
+#pragma unroll
+    for (int m = 0; m < TM; m++) {
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int64_t r = row0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (r <= mmax) {
+          float v = acc[m][n][q] + bc;
+          if (ELU) v = v > 0.f ? v : expm1f(v);
+          C[r * g.ldc + cidx] = v;
+        }
+      }
+    }
+  }
+}
+
+// input gradient: C = acc * elu'(Y) (ELU) and the wave's column sums of the stored values (0 past
+// the edges), per column n in cs[n]
+template <int TM, int TN, bool ELU>
+__device__ __forceinline__ void epi_input_grad(const f32x16 (&acc)[TM][TN], const GemmArgs& g, int64_t row0, int col0,
+                                               int i, int h, float (&cs)[TN]) {
+  const int64_t mmax = g.M - 1;
+  const int nmax = g.N - 1;
+#pragma unroll
+  for (int n = 0; n < TN; n++) {
+    const int cidx = col0 + 32 * n + i;
+    const int cc = min(cidx, nmax);
+    cs[n] = 0.f;
+#pragma unroll
+    for (int m = 0; m < TM; m++) {
+      float yv[16];
+      if (ELU) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int64_t r = row0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
+          yv[q] = g.Y[min(r, mmax) * g.ldY + cc];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int64_t r = row0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
+        float v = acc[m][n][q];
+        if (r <= mmax && cidx <= nmax) {
+          if (ELU) v = yv[q] > 0.f ? v : v * (yv[q] + 1.f);
+          g.C[r * g.ldc + cidx] = v;
+        } else {
+          v = 0.f;
+        }
+        cs[n] += v;
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN, int BK, int LAY, int PIPE, bool VEC, int MODE, bool ELU>
 __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm(GemmArgs g) {
   constexpr int NT = 64 * WGM * WGN;
@@ -264,53 +336,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm(GemmArgs g) {
 #undef HG_STAGE_LOAD
 #undef HG_STAGE_STORE
 
-  // epilogue.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2) + 4h, column i.
+  // epilogue (epi_forward / epi_input_grad)
   if (MODE == 0) {
-#pragma unroll
-    for (int n = 0; n < TN; n++) {
-      const int cidx = n0 + wn0 + 32 * n + i;
-      if (cidx > nmax) continue;
-      const float bc = g.bias ? g.bias[cidx] : 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; m++) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
-          if (r <= mmax) {
-            float v = acc[m][n][q] + bc;
-            if (ELU) v = v > 0.f ? v : expm1f(v);
-            g.C[r * g.ldc + cidx] = v;
-          }
-        }
-      }
-    }
+    if (g.bias) epi_forward<TM, TN, ELU, true>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h);
+    else epi_forward<TM, TN, ELU, false>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h);
   } else {
     float* red = lds;  // [WGM][BN] column partials of the waves along M (staging buffers are free)
+    float cs[TN];
+    epi_input_grad<TM, TN, ELU>(acc, g, m0 + wm0, n0 + wn0, i, h, cs);
 #pragma unroll
     for (int n = 0; n < TN; n++) {
       const int cl = wn0 + 32 * n + i;
-      const int cidx = n0 + cl;
-      float cs = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; m++) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
-          float v = acc[m][n][q];
-          if (r <= mmax && cidx <= nmax) {
-            if (ELU) {
-              const float yv = g.Y[r * g.ldY + cidx];
-              v = yv > 0.f ? v : v * (yv + 1.f);
-            }
-            g.C[r * g.ldc + cidx] = v;
-          } else {
-            v = 0.f;
-          }
-          cs += v;
-        }
-      }
-      cs += __shfl_xor(cs, 32);
-      if (h == 0) red[(wave % WGM) * BN + cl] = cs;
+      cs[n] += __shfl_xor(cs[n], 32);
+      if (h == 0) red[(wave % WGM) * BN + cl] = cs[n];
     }
     if (g.colpart) {
       __syncthreads();
@@ -732,54 +770,20 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   }
   }
 
-  // epilogue.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2) + 4h, column i.
+  // epilogue (epi_forward / epi_input_grad)
   if (MODE == 0 || SPLITK) {
     float* Cs = g.C + (SPLITK ? (int64_t)slice * xa.cstride : 0);  // mode 3 takes the input-grad epilogue
-#pragma unroll
-    for (int n = 0; n < TN; n++) {
-      const int cidx = n0 + wn0 + 32 * n + i;
-      if (cidx > nmax) continue;
-      const float bc = (MODE == 0 && g.bias) ? g.bias[cidx] : 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; m++) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
-          if (r <= mmax) {
-            float v = acc[m][n][q] + bc;
-            if (MODE == 0 && ELU) v = v > 0.f ? v : expm1f(v);
-            Cs[r * g.ldc + cidx] = v;
-          }
-        }
-      }
-    }
+    if (MODE == 0 && g.bias) epi_forward<TM, TN, MODE == 0 && ELU, true>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h);
+    else epi_forward<TM, TN, MODE == 0 && ELU, false>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h);
   } else {
     float* red = reinterpret_cast<float*>(lds);  // [WGM][BN] column partials of the waves along M
+    float cs[TN];
+    epi_input_grad<TM, TN, ELU>(acc, g, m0 + wm0, n0 + wn0, i, h, cs);
 #pragma unroll
     for (int n = 0; n < TN; n++) {
       const int cl = wn0 + 32 * n + i;
-      const int cidx = n0 + cl;
-      float cs = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; m++) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int64_t r = m0 + wm0 + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * h;
-          float v = acc[m][n][q];
-          if (r <= mmax && cidx <= nmax) {
-            if (ELU) {
-              const float yv = g.Y[r * g.ldY + cidx];
-              v = yv > 0.f ? v : v * (yv + 1.f);
-            }
-            g.C[r * g.ldc + cidx] = v;
-          } else {
-            v = 0.f;
-          }
-          cs += v;
-        }
-      }
-      cs += __shfl_xor(cs, 32);
-      if (h == 0) red[(wave % WGM) * BN + cl] = cs;
+      cs[n] += __shfl_xor(cs[n], 32);
+      if (h == 0) red[(wave % WGM) * BN + cl] = cs[n];
     }
     if (g.colpart) {
       __syncthreads();

@@ -149,12 +149,15 @@ __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act(const float* __re
   }
 
   // epilogue: + bias, ELU, one store.  acc register q of a 32x32 tile: row (q & 3) + 8 (q >> 2)
-  // + 4h, column i.
+  // + 4h, column i.  The bias is read once per column, unconditionally (clamped column) and
+  // retired before the stores (round 5): read inside the column guard, the compiler waited vmcnt(0)
+  // for it in front of every store, and stores count on that counter — 16-64 serialized stores
 #pragma unroll
   for (int n = 0; n < TN; n++) {
     const int c = c0 + 32 * n + i;
+    float bc = b ? b[min(c, N - 1)] : 0.f;
+    asm volatile("" : "+v"(bc));
     if (c >= N) continue;
-    const float bc = b ? b[c] : 0.f;
 #pragma unroll
     for (int m = 0; m < TM; m++) {
 #pragma unroll
