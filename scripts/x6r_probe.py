@@ -40,6 +40,19 @@ CASES = [
 ]
 
 
+# (name, rows, n, k, [(tile, slices)]): tile 0 = torch.mm; 40-48 PF = 1, 49-54 PF = 2 (hg_gemm.hip)
+WGRAD = [
+    ("dW actor0 512x705", 24576, 512, 705, [(0, 1), (49, 32), (40, 32)]),
+    ("dW critic0 256x768", 24576, 256, 768, [(0, 1), (49, 64), (40, 64)]),
+    ("dW actor1 256x512", 24576, 256, 512, [(0, 1), (54, 64), (45, 64)]),
+    ("dW critic1 768x219", 24576, 768, 219, [(0, 1), (54, 64), (45, 64)]),
+    ("dW linvel0 128x705", 24576, 128, 705, [(0, 1), (48, 64)]),
+    ("dW actor2 128x256", 24576, 128, 256, [(0, 1), (54, 128)]),
+    ("dW critic2 128x256", 24576, 128, 256, [(0, 1), (54, 128)]),
+    ("dW 128x128", 24576, 128, 128, [(0, 1), (46, 128), (52, 128)]),
+]
+
+
 def run(tag):
     import torch
     from humanoid import _native as N
@@ -102,6 +115,40 @@ def run(tag):
             tf = 2.0 * rows * k * n / (us * 1e-6) / 1e12
             res[f"{name} t{tile}"] = {"us": round(us, 2), "tflops_f32": round(tf, 1), "sha": h}
             print(f"{tag:5s} {name:22s} tile {tile:2d}: {us:8.2f} us {tf:6.1f} TF/s  {h}", flush=True)
+    # weight gradients dW [n, k] = gh^T x on k_wgrad_tr (split-K slices, not summed here) and on
+    # torch.mm (hipBLASLt, the committed TunableOp table)
+    from humanoid.utils.blas_tuning import use_tuned_gemms
+    use_tuned_gemms()
+    for name, rows, n, k, tiles in WGRAD:
+        g = torch.Generator(device=dev).manual_seed(zlib.crc32(name.encode()) % 100000)
+        gh = torch.randn(rows, n, device=dev, generator=g)
+        x = torch.randn(rows, k, device=dev, generator=g)
+        for tile, S in tiles:
+            if tile == 0:
+                fn = lambda: torch.mm(gh.t(), x)  # noqa: E731
+                outp = None
+            else:
+                outp = torch.empty(S, n, k, device=dev)
+                fn = lambda: L.hg_gemm_f32_wgrad(gh.data_ptr(), gh.stride(0), x.data_ptr(), x.stride(0), outp.data_ptr(),  # noqa: E731
+                                                 k, n * k, n, k, rows, S, 0, tile, s)
+            r = fn()
+            if outp is not None and r != 0:
+                res[f"{name} t{tile}/S{S}"] = {"rc": int(r)}
+                continue
+            torch.cuda.synchronize()
+            h = hashlib.sha256((outp if outp is not None else r).cpu().numpy().tobytes()).hexdigest()[:16]
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(ITERS):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / ITERS
+            res[f"{name} t{tile}/S{S}"] = {"us": round(us, 2), "sha": h}
+            print(f"{tag:5s} {name:22s} tile {tile:2d} S{S:3d}: {us:8.2f} us  {h}", flush=True)
     os.makedirs(OUT, exist_ok=True)
     with open(os.path.join(OUT, f"x6r_{tag}.json"), "w") as f:
         json.dump(res, f, indent=1)
@@ -113,10 +160,11 @@ def compare():
     ref_sha = {}
     for key, r in base.items():
         if "sha" in r:
-            ref_sha.setdefault(key.rsplit(" t", 1)[0], r["sha"])
+            if " t0/" not in key:
+                ref_sha.setdefault(key.rsplit(" t", 1)[0] + ("/" + key.rsplit("/", 1)[1] if "/S" in key else ""), r["sha"])
     for key, r in new.items():
         b = base.get(key, {})
-        name = key.rsplit(" t", 1)[0]
+        name = key.rsplit(" t", 1)[0] + ("/" + key.rsplit("/", 1)[1] if "/S" in key else "")
         same = "sha" in r and r["sha"] == ref_sha.get(name)
         print(f"{key:30s} base {b.get('us', '-'):>8} us  new {r.get('us', '-'):>8} us  "
               f"{'bitwise = base routed tile' if same else 'DIFFERS' if 'sha' in r else r}")
