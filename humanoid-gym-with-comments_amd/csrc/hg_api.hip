@@ -9,7 +9,7 @@
 
 #include "hg_common.h"
 
-extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
+extern "C" int hg_launch_step(const HgState* S, const hg_cfg* hcfg, const float* actions, uint64_t step_counter,
                                hipStream_t stream);
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
                               float* frame_obs, float* frame_priv, HgWindow obs, HgWindow priv, float inv_len_s,
@@ -315,7 +315,7 @@ int hg_tensor(void* sim, int id, hg_desc* d) {
 int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream) {
   Sim* s = (Sim*)sim;
   if (!s || !actions) return fail(s, HG_ERR_ARG, "null argument");
-  const int rc = hg_launch_step(&s->S, actions, step_counter, s->cfg.fix_base_link, (hipStream_t)stream);
+  const int rc = hg_launch_step(&s->S, &s->cfg, actions, step_counter, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_step launch failed");
   return HG_OK;
 }
@@ -374,7 +374,8 @@ int hg_update_cfg(void* sim, const hg_cfg* cfg, void* stream) {
   if (cfg->pgs_iterations < 0 || cfg->pgs_iterations > 1000 || !(cfg->sim_dt > 0.f))
     return fail(s, HG_ERR_ARG, "hg_update_cfg: bad solver parameters");
   s->cfg = *cfg;
-  // the device copy is read by every launch; the host source stays valid (it is the handle's)
+  // the device copy is read by the env-logic launches, the host copy by K_step's launch (its
+  // physics scalars go by value); the host source stays valid (it is the handle's)
   if (hipMemcpyAsync((void*)s->S.cfg, &s->cfg, sizeof(hg_cfg), hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess)
     return fail(s, HG_ERR_HIP, "hg_update_cfg: copy failed");
   return HG_OK;

@@ -42,7 +42,7 @@ struct __align__(16) GroupC {  // PGS constants of one 3-slot group (a, b, c): f
   float Wba, Wca, Wcb;     // W[b][a], W[c][a], W[c][b]
   float tgt[3], lo[3], hi[3];
   float mu;                // >= 0: (a, b, c) = a contact's normal and tangent pair (friction
-                           // coefficient); -1: single rows (the group kind rides in the same read)
+                           // coefficient); +inf: single rows (the disc test never scales them)
 };
 static_assert(sizeof(GroupC) == 64, "GroupC is four 16-byte LDS reads");
 
@@ -57,7 +57,7 @@ struct ContactC {  // one active contact: points on the two bodies (base-centred
 struct __align__(16) EnvSh {
   float root[16];
   float q[12], qd[12], act[12], tau[12];
-  float pd_kp[12], pd_kd[12], pd_lim[12], pd_tgt[12], madd[12];
+  float pd_kp[12], pd_kd[12], pd_lim[12], pd_tgt[12], pd_arm[12], madd[12];
   alignas(16) float nu[20];
   alignas(16) float h[20];
   alignas(16) float gv[20];  // g = L^-1 (tau - h), legs-first order
@@ -128,16 +128,28 @@ __device__ __forceinline__ f3 symv(const float* S, f3 v) {
             S[4] * v.x + S[5] * v.y + S[2] * v.z);
 }
 
-__device__ void ground(const hg_cfg* cfg, float x, float y, float* h, f3* n) {
-  if (cfg->terrain_type == 0 || cfg->heightfield == nullptr) { *h = 0; *n = mk(0, 0, 1); return; }
-  const float hs = cfg->hf_horizontal_scale, vs = cfg->hf_vertical_scale;
-  float fx = (x + cfg->hf_border) / hs, fy = (y + cfg->hf_border) / hs;
+// The launch's physics scalars, passed by value as a kernel argument: the substep loop reads them
+// with scalar loads from the kernarg segment (invariant) instead of vector loads of hg_cfg, which
+// the compiler cannot keep across the kernel's stores and reloads through the vector cache on the
+// chain of every substep (detection, PGS bounds).  Filled from the host hg_cfg by hg_launch_step.
+struct StepParams {
+  float dt, gz, contact_offset, vmax, beta, ground_friction;
+  int decimation, pgs_iterations, heightfield_on;  // heightfield_on: terrain_type != 0 and a heightfield
+  int hf_rows, hf_cols;
+  float hs, vs, border;
+  const int16_t* hf;
+};
+
+__device__ void ground(const StepParams& P, float x, float y, float* h, f3* n) {
+  if (!P.heightfield_on) { *h = 0; *n = mk(0, 0, 1); return; }
+  const float hs = P.hs, vs = P.vs;
+  float fx = (x + P.border) / hs, fy = (y + P.border) / hs;
   int i = (int)floorf(fx), j = (int)floorf(fy);
-  i = max(0, min(i, cfg->hf_rows - 2));
-  j = max(0, min(j, cfg->hf_cols - 2));
+  i = max(0, min(i, P.hf_rows - 2));
+  j = max(0, min(j, P.hf_cols - 2));
   float u = fminf(fmaxf(fx - i, 0.f), 1.f), v = fminf(fmaxf(fy - j, 0.f), 1.f);
-  const int16_t* hf = cfg->heightfield;
-  const int C = cfg->hf_cols;
+  const int16_t* hf = P.hf;
+  const int C = P.hf_cols;
   float h00 = vs * hf[i * C + j], h10 = vs * hf[(i + 1) * C + j];
   float h01 = vs * hf[i * C + j + 1], h11 = vs * hf[(i + 1) * C + j + 1];
   float dhdx, dhdy;
@@ -205,12 +217,37 @@ __device__ __forceinline__ f3 shr1_or(f3 v, int k, f3 base) {  // parent's value
   return k == 0 ? base : u;
 }
 
+// One lane's model constants for kin_scan (body bk: the lane's joint body, lanes outside 1..12 on
+// body 1) and rnea_scan (body br: lanes 0..12, others on the base).  Issued at the head of the
+// substep, ahead of A1 and its barrier, so their global round trip overlaps that phase instead of
+// sitting on the chain inside kin_scan / rnea_scan; the body indices go through an empty asm so the
+// loads stay in the loop (not hoisted out and then re-read next to their uses under the loop's
+// register pressure).
+struct ModelLane {
+  f3 ax, jp, com;
+  float jr[9], I[6], m;
+};
+__device__ __forceinline__ ModelLane load_model_lane(const hg_model* M, int l) {
+  int bk = l >= 1 && l <= 12 ? l : 1, br = l < 13 ? l : 0;
+  asm volatile("" : "+v"(bk), "+v"(br));
+  ModelLane ML;
+  ML.ax = ld3(M->axis[bk]);
+  ML.jp = ld3(M->joint_pos[bk]);
+#pragma unroll
+  for (int i = 0; i < 9; i++) ML.jr[i] = M->joint_rot[bk][i];
+  ML.com = ld3(M->com[br]);
+#pragma unroll
+  for (int i = 0; i < 6; i++) ML.I[i] = M->inertia[br][i];
+  ML.m = M->mass[br];
+  return ML;
+}
+
 struct KinLane {  // one lane's body after kin_scan (lane 0: the base; lanes 13..31: don't-care)
   float R[9];
   f3 o, w, al, ac;
 };
 
-__device__ KinLane kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool bias) {
+__device__ KinLane kin_scan(EnvSh& E, const ModelLane& ML, int l, float gz, bool bias) {
   const bool body = l >= 1 && l <= 12;
   const int b = body ? l : 1;
   const int k = (b - 1) % 6;  // link index within the leg
@@ -224,7 +261,7 @@ __device__ KinLane kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool b
   }
   const f3 v0 = mk(E.nu[0], E.nu[1], E.nu[2]), w0 = mk(E.nu[3], E.nu[4], E.nu[5]);
   // local transform of body b: Lr = jrot * rot(axis, q), origin jp (parent frame)
-  const f3 ax = ld3(M->axis[b]);
+  const f3 ax = ML.ax;
   float P[9];
   {
     float Rq[9], s, c;
@@ -233,9 +270,9 @@ __device__ KinLane kin_scan(EnvSh& E, const hg_model* M, int l, float gz, bool b
     Rq[0] = c + ax.x * ax.x * vv;        Rq[1] = ax.x * ax.y * vv - ax.z * s; Rq[2] = ax.x * ax.z * vv + ax.y * s;
     Rq[3] = ax.y * ax.x * vv + ax.z * s; Rq[4] = c + ax.y * ax.y * vv;        Rq[5] = ax.y * ax.z * vv - ax.x * s;
     Rq[6] = ax.z * ax.x * vv - ax.y * s; Rq[7] = ax.z * ax.y * vv + ax.x * s; Rq[8] = c + ax.z * ax.z * vv;
-    mm3(M->joint_rot[b], Rq, P);
+    mm3(ML.jr, Rq, P);
   }
-  f3 t = ld3(M->joint_pos[b]);
+  f3 t = ML.jp;
   tf_step<1>(P, t, k);
   tf_step<2>(P, t, k);
   tf_step<4>(P, t, k);
@@ -304,15 +341,15 @@ __device__ __forceinline__ void sfx_step(float* v, int n, int k) {
   }
 }
 
-__device__ void rnea_scan(EnvSh& E, const hg_model* M, int l, const KinLane& K, float scale0) {
+__device__ void rnea_scan(EnvSh& E, const ModelLane& ML, int l, const KinLane& K, float scale0) {
   const int b = l < 13 ? l : 0;
   const bool leg = l >= 1 && l <= 12;
   const int k = leg ? (l - 1) % 6 : 6;  // lanes outside the legs take no partner
   const f3 o = K.o;
-  const f3 cb = o + mv3(K.R, ld3(M->com[b]));
+  const f3 cb = o + mv3(K.R, ML.com);
   float Iw[6];
   {
-    const float* I = M->inertia[b];
+    const float* I = ML.I;
     const float* Rm = K.R;
     float Im[9] = {I[0], I[3], I[4], I[3], I[1], I[5], I[4], I[5], I[2]};
     float T9[9];
@@ -324,7 +361,7 @@ __device__ void rnea_scan(EnvSh& E, const hg_model* M, int l, const KinLane& K, 
       for (int j = 0; j < 3; j++) W9[i * 3 + j] = T9[i * 3] * Rm[j * 3] + T9[i * 3 + 1] * Rm[j * 3 + 1] + T9[i * 3 + 2] * Rm[j * 3 + 2];
     Iw[0] = W9[0]; Iw[1] = W9[4]; Iw[2] = W9[8]; Iw[3] = W9[1]; Iw[4] = W9[2]; Iw[5] = W9[5];
   }
-  float mb = M->mass[b];
+  float mb = ML.m;
   if (b == 0) {
     mb = E.mass0;
 #pragma unroll
@@ -410,16 +447,20 @@ __device__ __forceinline__ int lane_opaque(int l) {
 }
 
 
-// closest points of the segments [p1,q1], [p2,q2] (Ericson 5.1.9; as oracle/physics_ref.c seg_seg)
+// closest points of the segments [p1,q1], [p2,q2] (Ericson 5.1.9; as oracle/physics_ref.c seg_seg).
+// The quotients are products with v_rcp_f32 reciprocals (1 ulp) instead of correctly rounded
+// divisions (about nine instructions each): a and e are squared segment lengths of the model's
+// capsules (> 0), and denom is used only above 1e-6 a e
 __device__ __forceinline__ void seg_seg(f3 p1, f3 q1, f3 p2, f3 q2, f3& c1, f3& c2) {
   const f3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
   const float a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r);
   const float c = dot(d1, r), b = dot(d1, d2);
   const float denom = a * e - b * b;
-  float s = denom > 1e-6f * a * e ? fminf(fmaxf((b * f - c * e) / denom, 0.f), 1.f) : 0.f;
-  float t = (b * s + f) / e;
-  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-c / a, 0.f), 1.f); }
-  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((b - c) / a, 0.f), 1.f); }
+  const float ra = __builtin_amdgcn_rcpf(a), re = __builtin_amdgcn_rcpf(e);
+  float s = denom > 1e-6f * a * e ? fminf(fmaxf((b * f - c * e) * __builtin_amdgcn_rcpf(denom), 0.f), 1.f) : 0.f;
+  float t = (b * s + f) * re;
+  if (t < 0.f) { t = 0.f; s = fminf(fmaxf(-c * ra, 0.f), 1.f); }
+  else if (t > 1.f) { t = 1.f; s = fminf(fmaxf((b - c) * ra, 0.f), 1.f); }
   c1 = p1 + s * d1;
   c2 = p2 + t * d2;
 }
@@ -465,7 +506,7 @@ __device__ __forceinline__ bool load_item(const hg_model* M, int item, int nleg,
   return pr;
 }
 
-__device__ __forceinline__ Cand detect(const EnvSh& E, const hg_cfg* cfg, bool is_pair, int c, int p, int b0, int b1,
+__device__ __forceinline__ Cand detect(const EnvSh& E, const StepParams& P, bool is_pair, int c, int p, int b0, int b1,
                                        const float* k, bool fixed) {
   Cand C;
   C.cn = mk(0, 0, 1); C.xP = mk(0, 0, 0); C.xN = mk(0, 0, 0);
@@ -473,14 +514,14 @@ __device__ __forceinline__ Cand detect(const EnvSh& E, const hg_cfg* cfg, bool i
   if (!is_pair) {
     const f3 x = ld3(E.o[b0]) + mv3(E.R[b0], mk(k[0], k[1], k[2]));
     float hg;
-    ground(cfg, x.x + E.root[0], x.y + E.root[1], &hg, &C.cn);
+    ground(P, x.x + E.root[0], x.y + E.root[1], &hg, &C.cn);
     const float r = k[3];
     C.phi = (x.z + E.root[2] - hg) * C.cn.z - r;
     C.xP = x - r * C.cn;
     C.bP = b0;
-    C.mu = 0.5f * (E.fric + cfg->ground_friction);
+    C.mu = 0.5f * (E.fric + P.ground_friction);
     C.lam_base = 3 * c;
-    C.act = !fixed && C.phi < cfg->contact_offset;
+    C.act = !fixed && C.phi < P.contact_offset;
     return C;
   }
   const f3 ob = ld3(E.o[b1]);
@@ -508,8 +549,9 @@ __device__ __forceinline__ Cand detect(const EnvSh& E, const hg_cfg* cfg, bool i
     const f3 oa = ld3(E.o[b0]);
     seg_seg(oa + mv3(E.R[b0], mk(k[0], k[1], k[2])), oa + mv3(E.R[b0], mk(k[3], k[4], k[5])), q0, q1, pa, pb);
     const f3 dv = pb - pa;
-    dist = sqrtf(dot(dv, dv));
-    C.cn = dist > 1e-9f ? (1.0f / dist) * dv : mk(0.f, -1.f, 0.f);
+    // v_sqrt_f32 / v_rcp_f32 (1 ulp) instead of the correctly rounded sequences
+    dist = __builtin_amdgcn_sqrtf(dot(dv, dv));
+    C.cn = dist > 1e-9f ? __builtin_amdgcn_rcpf(dist) * dv : mk(0.f, -1.f, 0.f);
     ra = k[12];
   }
   C.phi = dist - ra - rb;
@@ -519,7 +561,7 @@ __device__ __forceinline__ Cand detect(const EnvSh& E, const hg_cfg* cfg, bool i
   C.bN = b0;
   C.mu = E.fric;
   C.lam_base = LAM_PAIR + 3 * p;
-  C.act = C.phi < cfg->contact_offset;
+  C.act = C.phi < P.contact_offset;
   return C;
 }
 
@@ -553,7 +595,7 @@ __device__ __forceinline__ void place_contact(EnvSh& E, const Cand& C, bool act,
 // FIXED = asset.fix_base_link, a compile-time constant so the factorised size and every
 // floating-base branch resolve at compile time
 template <bool FIXED>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_step(HgState S, const float* __restrict__ actions_in, uint64_t step_counter) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) k_step(HgState S, const float* __restrict__ actions_in, uint64_t step_counter, const StepParams P) {
   __shared__ EnvSh shm[2];
   const int half = threadIdx.x >> 5;
   int l = threadIdx.x & 31;
@@ -570,11 +612,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const hg_cfg* cfg = S.cfg;
   const hg_model* M = S.model;
   const int np = S.np;
-  const float dt = cfg->sim_dt;
+  const float dt = P.dt;
   const float inv_dt = 1.0f / dt;
   constexpr bool fixed = FIXED;
   constexpr int nf = fixed ? 12 : 18;  // factorised size (legs-first order: left leg, right leg, base)
-  const float gz = cfg->gravity_z;
+  const float gz = P.gz;
 
   // ---------------- prologue: actions (humanoid_env.py:624-635) + state load
   if (l < 12) {
@@ -608,10 +650,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     E.pd_kp[l] = cfg->kp[l];
     E.pd_kd[l] = cfg->kd[l];
     E.pd_lim[l] = cfg->torque_limit[l];
+    E.pd_arm[l] = M->armature[l + 1];
     E.pd_tgt[l] = E.act[l] * cfg->action_scale + cfg->default_dof_pos[l];
   }
   for (int i = l; i < 18 * 20; i += 32) (&E.L[0][0])[i] = 0.f;  // the left-right cross block stays zero
-  const int decimation = cfg->decimation;
+  const int decimation = P.decimation;
   // per-lane model constants of the detection phase, in registers for the whole launch (they
   // were global loads at the head of every substep's detection): this lane's ground candidate
   // (body, sole point / sphere centre, radius) or capsule pair (bodies, segment ends, radii),
@@ -620,6 +663,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   int det_c, det_p, det_b0, det_b1;
   float det_k[14];
   const bool det_pair = load_item(M, min(l, nitems - 1), nleg, npair, det_c, det_p, det_b0, det_b1, det_k);
+  // the round-2 items' plane early-out (A9) from two per-lane constants (body, reach = the point's
+  // distance from the body origin + its radius), so the skipped round reads no model constants
+  int r2_b0 = 0;
+  float r2_reach = 0.f;
+  if (nitems > 32) {
+    int cc2, pp2, b02, b12;
+    float k2[14];
+    const bool pr2 = load_item(M, min(32 + l, nitems - 1), nleg, npair, cc2, pp2, b02, b12, k2);
+    r2_b0 = b02;
+    r2_reach = pr2 ? 0.f : sqrtf(k2[0] * k2[0] + k2[1] * k2[1] + k2[2] * k2[2]) + k2[3];
+  }
   const int lj = l < 12 ? l + 1 : 1;
   const float lim_lo = M->lower[lj], lim_hi = M->upper[lj], jfric = M->joint_friction[lj];
   // this joint's slot among the friction rows: larger friction bounds first, then the joint
@@ -635,6 +689,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   for (int sub = 0; sub < decimation; sub++) {
     // lane masks are rebuilt per substep (v_cmp) instead of living across the loop in SGPR pairs
     asm volatile("" : "+v"(l));
+    const ModelLane ML = load_model_lane(M, l);
     // ---- A1: torques (_compute_torques, humanoid_env.py:910-925); implicit damping on the
     // joints whose torque is not clipped: dt*kd joins M's diagonal (with the model armature)
     if (l < 12) {
@@ -642,14 +697,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       const float lim = E.pd_lim[l];
       E.tau[l] = clampf(t, -lim, lim);
       const bool sat = t < -lim || t > lim;
-      E.madd[l] = M->armature[l + 1] + (sat ? 0.f : dt * E.pd_kd[l]);
+      E.madd[l] = E.pd_arm[l] + (sat ? 0.f : dt * E.pd_kd[l]);
       E.nu[6 + l] = E.qd[l];
     }
     if (l < 6) E.nu[l] = fixed ? 0.f : E.root[7 + l];
     __syncthreads();
     // ---- A2..A5: kinematics (prefix scans), per-body forces, backward recursions (suffix scans)
-    const KinLane K = kin_scan(E, M, l, gz, true);
-    rnea_scan(E, M, l, K, scale0);
+    const KinLane K = kin_scan(E, ML, l, gz, true);
+    rnea_scan(E, ML, l, K, scale0);
     __syncthreads();
     // base totals (lane 0) — read the kinematics scratch before M overwrites it.  One total per
     // lane (16 lanes: h 0..5, base_cm, base_cs 0..2, base_cJ 0..5), each with the operations and
@@ -801,7 +856,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     // rest dropped and counted)
     {
       const uint32_t lt = (1u << l) - 1u;
-      const float beta = cfg->baumgarte, vmax = cfg->max_depenetration_vel;
+      const float beta = P.beta, vmax = P.vmax;
       // single rows unless a contact claims the group below (mu = +inf: the PGS disc projection
       // never scales a single-row group, see A13)
       if (l < NGRP) E.grp[l].mu = __builtin_huge_valf();
@@ -821,24 +876,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int i = 0; i < 14; i++) k[i] = det_k[i];
         if (rnd) {
-          pr = load_item(M, min(item, nitems - 1), nleg, npair, cc, pp, b0, b1, k);
           // round 2 holds ground candidates (the base-box corners): on a plane, a candidate whose
           // body origin is higher than contact_offset + the point's distance from it + its radius
           // cannot be active.  When no round-2 item of the wave's two envs can be, the round is
           // skipped (bitwise the same result: its warm-start slots are cleared as an inactive
-          // candidate's are, and no contact is placed)
+          // candidate's are, and no contact is placed); the test is from the launch-time constants
+          // with a 1e-4 margin (conservative: a borderline round runs in full)
           // (a fixed base never activates ground candidates)
+          const bool pr2 = item >= nleg && item < nleg + npair;
           const bool can = item < nitems &&
-                           (pr || (!fixed && (cfg->terrain_type != 0 ||
-                                              E.o[b0][2] + E.root[2] - sqrtf(k[0] * k[0] + k[1] * k[1] + k[2] * k[2]) -
-                                                      k[3] < cfg->contact_offset)));
+                           (pr2 || (!fixed && (P.heightfield_on ||
+                                               E.o[r2_b0][2] + E.root[2] - r2_reach < P.contact_offset + 1e-4f)));
           if (__ballot(can) == 0) {
-            if (item < nitems) E.lamst[3 * cc + 0] = E.lamst[3 * cc + 1] = E.lamst[3 * cc + 2] = 0.f;
+            const int cs = min(item < nleg ? item : item - npair, HG_MAX_CONTACTS - 1);  // load_item's c
+            if (item < nitems) E.lamst[3 * cs + 0] = E.lamst[3 * cs + 1] = E.lamst[3 * cs + 2] = 0.f;
             continue;
           }
+          pr = load_item(M, min(item, nitems - 1), nleg, npair, cc, pp, b0, b1, k);
         }
         Cand c;
-        if (item < nitems) c = detect(E, cfg, pr, cc, pp, b0, b1, k, fixed);
+        if (item < nitems) c = detect(E, P, pr, cc, pp, b0, b1, k, fixed);
         const bool act = item < nitems && c.act;
         const uint32_t mc = (uint32_t)(__ballot(act) >> (32 * half));
         const int n = __popc(mc);
@@ -1039,46 +1096,51 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     // ---- A13: projected Gauss-Seidel over the 3-slot groups.  The impulses are replicated: every
     // lane of an env holds all 32 of its env's impulses (uniform per half-wave); the row velocity
-    // v_r lives in lane r and is read with scalar v_readlane pairs.  Per group (a, b, c):
+    // v_r lives in lane r and is read with one ds_swizzle broadcast (swz).  Per group (a, b, c):
     //   a: lambda_a <- clamp(lambda_a + (tgt_a - v_a) / W_aa, lo_a, hi_a)   (normal / single row)
     //   b: lambda_b' <- clamp(lambda_b + (tgt_b - v_b - W_ba dl_a) / W_bb, lo_b, hi_b)
     //   c: lambda_c' <- clamp(lambda_c + (tgt_c - v_c - W_ca dl_a - W_cb dl_b') / W_cc, lo_c, hi_c)
     //   (b, c) <- (b', c') scaled onto the disc |.| <= mu lambda_a
     // One instruction stream for both group kinds, through the group constants: a contact's
     // tangent pair has tgt 0, bounds -+BIG (no clamp) and W_cb = 0 (both steps from the same nu,
-    // as the oracle); a single-row group has mu = +inf, so the disc test never scales it (lim =
-    // +-inf or NaN: nn2 > lim^2 is false).  Then every row velocity takes the group's three
-    // updates (one FMA each).  Groups empty in both envs of the wave are skipped (scalar branch).
+    // as the oracle); a single-row group has mu = +inf, so the disc never scales it.  Then every
+    // row velocity takes the group's three updates (one FMA each).  Groups empty in both envs of
+    // the wave are skipped (scalar branch).  Separate contact / single-row streams behind scalar
+    // branches (round 5) cut VALU per wave 45.1 k -> 41.8 k but were slower per launch (their
+    // extra SALU and taken branches sit on the chain; profiles/r5_kstep/README.md).
     {
       float vrow = v0;
       const int ng = (max(shm[0].nrows, shm[1].nrows) + 2) / 3;
-      const int npgs = cfg->pgs_iterations;
+      const int npgs = P.pgs_iterations;
       for (int it = 0; it < npgs; it++) {
 #pragma unroll
         for (int g = 0; g < NGRP; g++) {
           if (g < ng) {
             const int ra = 3 * g, rb = 3 * g + 1, rc = 3 * g + 2;
+            const bool has_c = rc < RMAX;  // slot 32 of group 10 is virtual
+            const int rcc = has_c ? rc : 0;
             const GroupC& G = E.grp[g];
             const float va = swz(vrow, ra), vb = swz(vrow, rb);
-            const float vc = rc < RMAX ? swz(vrow, rc < RMAX ? rc : 0) : 0.f;
-            const float la = lam[ra], lb = lam[rb], lc = rc < RMAX ? lam[rc < RMAX ? rc : 0] : 0.f;
+            const float vc = has_c ? swz(vrow, rcc) : 0.f;
+            const float la = lam[ra], lb = lam[rb], lc = has_c ? lam[rcc] : 0.f;
             const float na = clampf(la + (G.tgt[0] - va) * G.invD[0], G.lo[0], G.hi[0]);
             const float da = na - la;
             const float vb1 = vb + G.Wba * da, vc1 = vc + G.Wca * da;
-            const float nb = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
-            const float vc2 = vc1 + G.Wcb * (nb - lb);
-            const float nc = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
-            const float lim = G.mu * na, nn2 = __builtin_fmaf(nc, nc, nb * nb);  // the order of the oracle's l1^2 + l2^2
-            const float sc = nn2 > lim * lim ? lim * __builtin_amdgcn_rsqf(nn2) : 1.f;
-            const float db = nb * sc - lb, dc = nc * sc - lc;
-            if (rc < RMAX) {
-              vrow += wrow[ra] * da + wrow[rb] * db + wrow[rc < RMAX ? rc : 0] * dc;
-              lam[rc < RMAX ? rc : 0] += dc;
-            } else {
-              vrow += wrow[ra] * da + wrow[rb] * db;
-            }
+            const float tb = clampf(lb + (G.tgt[1] - vb1) * G.invD[1], G.lo[1], G.hi[1]);
+            const float vc2 = vc1 + G.Wcb * (tb - lb);
+            const float tc = clampf(lc + (G.tgt[2] - vc2) * G.invD[2], G.lo[2], G.hi[2]);
+            // the oracle's "if (|l| > lim) l *= lim / |l|" as the scale min(1, |lim| / |l|): |l| = 0
+            // gives lim * inf (inf or NaN) and min returns 1; a single-row group's lim = mu lambda_a
+            // is +-inf or NaN (mu = +inf), so its scale is 1; |.| is a free source modifier
+            const float lim = G.mu * na, nn2 = __builtin_fmaf(tc, tc, tb * tb);  // the order of the oracle's l1^2 + l2^2
+            const float sc = fminf(1.f, fabsf(lim) * __builtin_amdgcn_rsqf(nn2));
+            const float db = __builtin_fmaf(tb, sc, -lb), dc = __builtin_fmaf(tc, sc, -lc);
+            vrow = __builtin_fmaf(wrow[ra], da, vrow);
+            vrow = __builtin_fmaf(wrow[rb], db, vrow);
+            if (has_c) vrow = __builtin_fmaf(wrow[rcc], dc, vrow);
             lam[ra] += da;
             lam[rb] += db;
+            if (has_c) lam[rcc] += dc;
           }
         }
       }
@@ -1200,7 +1262,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   if (l < 6) E.nu[l] = E.root[7 + l];
   if (l < 12) E.nu[6 + l] = E.qd[l];
   __syncthreads();
-  kin_scan(E, M, l, gz, false);
+  kin_scan(E, load_model_lane(M, l), l, gz, false);
   __syncthreads();
   // stage the [13][13] rigid states and [13][3] contact forces in LDS, then store them as SoA rows
   if (l < 13) {
@@ -1243,12 +1305,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   for (int i = l; i < HG_LAMW; i += 32) S.lambda[i * np + e] = E.lamst[i];
 }
 
-extern "C" int hg_launch_step(const HgState* S, const float* actions, uint64_t step_counter, int fixed_base,
+extern "C" int hg_launch_step(const HgState* S, const hg_cfg* hcfg, const float* actions, uint64_t step_counter,
                               hipStream_t stream) {
   const int grid = (S->n + 1) / 2;
-  if (fixed_base)
-    hipLaunchKernelGGL(k_step<true>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);
+  StepParams P;
+  P.dt = hcfg->sim_dt;
+  P.gz = hcfg->gravity_z;
+  P.contact_offset = hcfg->contact_offset;
+  P.vmax = hcfg->max_depenetration_vel;
+  P.beta = hcfg->baumgarte;
+  P.ground_friction = hcfg->ground_friction;
+  P.decimation = hcfg->decimation;
+  P.pgs_iterations = hcfg->pgs_iterations;
+  P.heightfield_on = hcfg->terrain_type != 0 && hcfg->heightfield != nullptr;
+  P.hf_rows = hcfg->hf_rows;
+  P.hf_cols = hcfg->hf_cols;
+  P.hs = hcfg->hf_horizontal_scale;
+  P.vs = hcfg->hf_vertical_scale;
+  P.border = hcfg->hf_border;
+  P.hf = hcfg->heightfield;
+  if (hcfg->fix_base_link)
+    hipLaunchKernelGGL(k_step<true>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter, P);
   else
-    hipLaunchKernelGGL(k_step<false>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter);
+    hipLaunchKernelGGL(k_step<false>, dim3(grid), dim3(64), 0, stream, *S, actions, step_counter, P);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -292,7 +292,7 @@ def _step_parity(env, counter, fields=("q", "qd", "root", "torques", "rigid"), s
     if outl.any():
         null = ST.flip_null_rate(hc, model, S, a_ref, r64, sp, fields, kp, kd, STEP_TOL_K, hf=hf,
                                  members=F32_STEP_ENSEMBLE, candidates=F32_NULL_CANDIDATES)
-        allowed = int(np.ceil(2.0 * np.mean(null["bad_envs"])))
+        allowed = ST.allowed_outliers(null["bad_envs"], len(outl))
         err = {f: float(np.abs(gpu[f][outl] - base[f][outl]).max()) for f in fields}
         report.update(null_outlier_envs=null["bad_envs"], allowed_outlier_envs=allowed, outlier_max_err=err,
                       null_outlier_max_err=null["max_err"])

@@ -67,3 +67,11 @@ def test_fp32_builds_have_rare_contact_outliers(contact_step):
     assert frac.max() < 0.05          # a small fraction ...
     assert sum(null["bad_envs"]) > 0  # ... but not zero: the allowance is needed on contact steps
     assert null["dropped_mismatch_envs"] == [0, 0, 0]
+
+
+def test_allowance_is_twice_the_rate_with_a_floor():
+    # large checks: twice the null builds' mean; small checks: twice the 1 % floor rate
+    assert ST.allowed_outliers([39, 36, 43, 36], 4096) == 82
+    assert ST.allowed_outliers([0, 0, 0, 0], 64) == 2
+    assert ST.allowed_outliers([0, 0, 0, 0], 4096) == 82
+    assert ST.allowed_outliers([3, 0, 1, 0], 64) == 2
