@@ -53,6 +53,11 @@ struct GemmArgs {
   int N, K;
   int tiles_n;
   int64_t tiles;
+  // forward (mode 0) column split: columns >= nsplit (> 0, a multiple of every tile's BN) go to C2
+  // (ldc2) at column - nsplit, so one GEMM writes two contiguous outputs (zero: no split)
+  float* C2;
+  int64_t ldc2;
+  int nsplit;
 };
 
 template <int LAY>
@@ -180,7 +185,7 @@ __device__ __forceinline__ void mma_chunk(const float* __restrict__ As, const fl
 // forward (stores count on that counter too).  Values, stores and the column-sum order unchanged.
 template <int TM, int TN, bool ELU, bool BIAS>
 __device__ __forceinline__ void epi_forward(const f32x16 (&acc)[TM][TN], const GemmArgs& g, float* __restrict__ C,
-                                            int64_t row0, int col0, int i, int h) {
+                                            int64_t row0, int col0, int i, int h, int64_t ldc, int cshift) {
   const int64_t mmax = g.M - 1;
   const int nmax = g.N - 1;
 #pragma unroll
@@ -198,7 +203,7 @@ __device__ __forceinline__ void epi_forward(const f32x16 (&acc)[TM][TN], const G
         if (r <= mmax) {
           float v = acc[m][n][q] + bc;
           if (ELU) v = v > 0.f ? v : expm1f(v);
-          C[r * g.ldc + cidx] = v;
+          C[r * ldc + cidx - cshift] = v;
         }
       }
     }
@@ -338,8 +343,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm(GemmArgs g) {
 
   // epilogue (epi_forward / epi_input_grad)
   if (MODE == 0) {
-    if (g.bias) epi_forward<TM, TN, ELU, true>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h);
-    else epi_forward<TM, TN, ELU, false>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h);
+    if (g.bias) epi_forward<TM, TN, ELU, true>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h, g.ldc, 0);
+    else epi_forward<TM, TN, ELU, false>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h, g.ldc, 0);
   } else {
     float* red = lds;  // [WGM][BN] column partials of the waves along M (staging buffers are free)
     float cs[TN];
@@ -773,8 +778,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   // epilogue (epi_forward / epi_input_grad)
   if (MODE == 0 || SPLITK) {
     float* Cs = g.C + (SPLITK ? (int64_t)slice * xa.cstride : 0);  // mode 3 takes the input-grad epilogue
-    if (MODE == 0 && g.bias) epi_forward<TM, TN, MODE == 0 && ELU, true>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h);
-    else epi_forward<TM, TN, MODE == 0 && ELU, false>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h);
+    int64_t ldcs = g.ldc;
+    int cshift = 0;
+    if (MODE == 0 && g.nsplit > 0 && n0 >= g.nsplit) {  // block-uniform: the split is a multiple of BN
+      Cs = g.C2;
+      ldcs = g.ldc2;
+      cshift = g.nsplit;
+    }
+    if (MODE == 0 && g.bias) epi_forward<TM, TN, MODE == 0 && ELU, true>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h, ldcs, cshift);
+    else epi_forward<TM, TN, MODE == 0 && ELU, false>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h, ldcs, cshift);
   } else {
     float* red = reinterpret_cast<float*>(lds);  // [WGM][BN] column partials of the waves along M
     float cs[TN];
@@ -1181,8 +1193,22 @@ extern "C" int64_t hg_gemm_x6_image_bytes(int64_t rows, int64_t K) {
   return img_chunks(K) * 3 * img_rows(rows) * 2 * 16;
 }
 
+extern "C" int hg_gemm_x6_image_jobs_pitched(const float* const* P, const int64_t* ld, const int* trans,
+                                             const int64_t* rows, const int64_t* K, void* const* img,
+                                             const int64_t* pitch_rows, int njobs, void* stream);
+
 extern "C" int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* trans, const int64_t* rows,
                                      const int64_t* K, void* const* img, int njobs, void* stream) {
+  return hg_gemm_x6_image_jobs_pitched(P, ld, trans, rows, K, img, nullptr, njobs, stream);
+}
+
+// pitch_rows (nullable; entry <= 0: the job's own rows): the row count of the image a job writes
+// into, so several jobs fill the row bands of ONE image (job j's img = the image + its first row
+// x 32 bytes, the first row a multiple of 32): the image of the rows stacked, e.g. two layers'
+// weights that read the same input as one [n_a + n_b, K] operand
+extern "C" int hg_gemm_x6_image_jobs_pitched(const float* const* P, const int64_t* ld, const int* trans,
+                                             const int64_t* rows, const int64_t* K, void* const* img,
+                                             const int64_t* pitch_rows, int njobs, void* stream) {
   if (njobs <= 0) return HG_OK;
   if (njobs > IMG_MAX || !P || !ld || !trans || !rows || !K || !img) return HG_ERR_ARG;
   ImageJobs J;
@@ -1197,7 +1223,9 @@ extern "C" int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, c
     J.P[j] = P[j];
     J.img[j] = reinterpret_cast<bf16x8*>(img[j]);
     J.ld[j] = ld[j];
-    J.pitch[j] = img_rows(rows[j]) * 2;
+    const int64_t prow = pitch_rows && pitch_rows[j] > 0 ? pitch_rows[j] : rows[j];
+    if (prow < rows[j] || prow > 0x7fffffff) return HG_ERR_ARG;
+    J.pitch[j] = img_rows(prow) * 2;
     J.trans[j] = trans[j];
     J.R[j] = (int)rows[j];
     J.K[j] = (int)K[j];
@@ -1231,6 +1259,21 @@ extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void
   GemmArgs g{a, la, reinterpret_cast<const float*>(Bimg), img_rows(N) * 2, bias, Y, ldY, C, ldc, colpart, M, N, K, 0, 0};
   GemmX6Args xa{g, 0, 0, 1};
   return x6_img_dispatch(tile, mode, Aimg ? 3 : 1, xa, vec, act == 1, (hipStream_t)stream);
+}
+
+extern "C" int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const float* bias, float* C,
+                                     int64_t ldc, float* C2, int64_t ldc2, int nsplit, int64_t M, int N, int K, int act,
+                                     int tile, int64_t bimg_bytes, void* stream) {
+  if (!A || !Bimg || !C || !C2 || M <= 0 || N <= 0 || K <= 0 || nsplit <= 0 || nsplit >= N || nsplit % 256 ||
+      ldc < nsplit || ldc2 < N - nsplit || lda < K || act < 0 || act > 1 || tile < 19 || tile > NTILES)
+    return HG_ERR_ARG;
+  if (bimg_bytes != hg_gemm_x6_image_bytes(N, K)) return HG_ERR_ARG;
+  if ((uintptr_t)A % 4 || (uintptr_t)Bimg % 16 || (uintptr_t)C % 4 || (uintptr_t)C2 % 4) return HG_ERR_ARG;
+  const bool vec = lda % 4 == 0 && (uintptr_t)A % 16 == 0;
+  GemmArgs g{A, lda, reinterpret_cast<const float*>(Bimg), img_rows(N) * 2, bias, nullptr, 0, C, ldc, nullptr, M, N, K,
+             0, 0, C2, ldc2, nsplit};
+  GemmX6Args xa{g, 0, 0, 1};
+  return x6_img_dispatch(tile, 0, 1, xa, vec, act == 1, (hipStream_t)stream);
 }
 
 extern "C" int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M,

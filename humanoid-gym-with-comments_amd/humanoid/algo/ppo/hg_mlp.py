@@ -310,35 +310,56 @@ def _gemm_fwd_tile(h, W, b):
     return _route(_GEMM_FWD, h.shape[0], W.shape[1], W.shape[0])
 
 
+def _img_rows(r):
+    return (r + 255) // 256 * 256
+
+
 def x6_images(jobs, dev):
-    """Operand images of the bf16-split tiles in one launch (hg_gemm_x6_image_jobs): jobs
-    [(P, trans, rows, K)] (trans 0: element (r, k) = P[r][k]; trans 1: P[k][r]) -> one image tensor
-    each, slices of a single allocation."""
+    """Operand images of the bf16-split tiles in one launch (hg_gemm_x6_image_jobs_pitched): jobs
+    [(P, trans, rows, K)] (trans 0: element (r, k) = P[r][k]; trans 1: P[k][r]) or
+    [("stack", (P_1, .., P_m), K)] (the trans-0 image of the P_i's rows stacked, each band written
+    by its own job into the shared image; every band but the last a multiple of 32 rows) -> one
+    image tensor each, slices of a single allocation."""
     if not jobs:
         return []
     L = N.lib()
-    sizes = [int(L.hg_gemm_x6_image_bytes(r, k)) for _, _, r, k in jobs]
+
+    def rows_of(j):
+        return sum(P.shape[0] for P in j[1]) if j[0] == "stack" else j[2]
+
+    sizes = [int(L.hg_gemm_x6_image_bytes(rows_of(j), j[-1])) for j in jobs]
     buf = torch.empty(sum(sizes) // 4, dtype=torch.float32, device=dev)
     imgs, off = [], 0
     for sz in sizes:
         imgs.append(buf[off // 4:(off + sz) // 4])
         off += sz
-    m = len(jobs)
+    cj = []  # (P, trans, rows, K, image address, pitch rows)
+    for j, im in zip(jobs, imgs):
+        if j[0] == "stack":
+            total, r0 = rows_of(j), 0
+            for P in j[1]:
+                if r0 % 32:
+                    raise ValueError("x6_images: stacked bands must start on a multiple of 32 rows")
+                cj.append((P, 0, P.shape[0], j[2], im.data_ptr() + 32 * r0, total))
+                r0 += P.shape[0]
+        else:
+            cj.append((j[0], j[1], j[2], j[3], im.data_ptr(), 0))
+    m = len(cj)
     vp = ctypes.c_void_p
-    rc = L.hg_gemm_x6_image_jobs((vp * m)(*[j[0].data_ptr() for j in jobs]),
-                                 (ctypes.c_int64 * m)(*[j[0].stride(0) for j in jobs]),
-                                 (ctypes.c_int * m)(*[j[1] for j in jobs]), (ctypes.c_int64 * m)(*[j[2] for j in jobs]),
-                                 (ctypes.c_int64 * m)(*[j[3] for j in jobs]), (vp * m)(*[im.data_ptr() for im in imgs]),
-                                 m, _stream(dev))
+    i64 = ctypes.c_int64
+    rc = L.hg_gemm_x6_image_jobs_pitched((vp * m)(*[c[0].data_ptr() for c in cj]), (i64 * m)(*[c[0].stride(0) for c in cj]),
+                                         (ctypes.c_int * m)(*[c[1] for c in cj]), (i64 * m)(*[c[2] for c in cj]),
+                                         (i64 * m)(*[c[3] for c in cj]), (vp * m)(*[c[4] for c in cj]),
+                                         (i64 * m)(*[c[5] for c in cj]), m, _stream(dev))
     if rc != 0:
-        raise RuntimeError(f"hg_gemm_x6_image_jobs failed ({rc})")
+        raise RuntimeError(f"hg_gemm_x6_image_jobs_pitched failed ({rc})")
     return imgs
 
 
-def _image_specs(params, n, rows, dx):
+def _image_specs(params, n, rows, dx, first=0):
     """The operand images an n-layer MLP call on ``rows`` rows uses: (kind, layer, W, trans, R, K)
-    for its routed bf16-split forward GEMMs (kind "f": W itself) and, when ``dx``, input-grad GEMMs
-    (kind "d": W^T)."""
+    for its routed bf16-split forward GEMMs of layers >= ``first`` (kind "f": W itself) and, when
+    ``dx``, input-grad GEMMs (kind "d": W^T)."""
     out = []
     if not (X6_IMAGE and GEMM):
         return out
@@ -347,7 +368,7 @@ def _image_specs(params, n, rows, dx):
         if not W.is_contiguous():
             continue
         nn_, kk = W.shape
-        if i < n - 1 and _route(_GEMM_FWD, rows, kk, nn_) >= X6_TILE0:
+        if first <= i < n - 1 and _route(_GEMM_FWD, rows, kk, nn_) >= X6_TILE0:
             out.append(("f", i, W, 0, nn_, kk))
         if dx and i > 0 and _route(_GEMM_DX, rows, nn_, kk) >= X6_TILE0:
             out.append(("d", i, W, 1, kk, nn_))
@@ -358,17 +379,27 @@ _SCOPE = None  # {(weight address, trans): image} while an image_scope is active
 
 
 @contextlib.contextmanager
-def image_scope(specs, dev):
+def image_scope(specs, dev, pairs=()):
     """The weight images of several fusable MLPs (``specs``: [(net, rows)]) built in ONE launch
     for the MLP calls inside the block — one image launch per PPO minibatch instead of one per
-    network.  The weights must not change inside the block."""
+    network; ``pairs`` [(net_a, net_b, rows)]: the stacked first-layer image of mlp_pair_forward
+    (those nets' own first-layer images are then not built).  The weights must not change inside
+    the block."""
     global _SCOPE
     jobs, keys = [], []
+    paired = set()
+    for net_a, net_b, rows in pairs:
+        if pair_ok(net_a, net_b, rows):
+            Wa, Wb = net_a[0].weight, net_b[0].weight
+            keys.append(("stack", Wa.data_ptr(), Wb.data_ptr()))
+            jobs.append(("stack", (Wa, Wb), Wa.shape[1]))
+            paired.update((id(net_a), id(net_b)))
     for net, rows in specs:
         if not fusable(net):
             continue
         params = _params(net)
-        for _, _, W, trans, R, K in _image_specs(params, len(params) // 2, rows, True):
+        first = 1 if id(net) in paired else 0
+        for _, _, W, trans, R, K in _image_specs(params, len(params) // 2, rows, True, first):
             key = (W.data_ptr(), trans)
             if key not in keys:
                 keys.append(key)
@@ -381,12 +412,12 @@ def image_scope(specs, dev):
         _SCOPE = prev
 
 
-def _forward_images(params, n, rows, dev, dx):
-    """{layer: image} of W for the routed bf16-split forward GEMMs of an n-layer MLP call on ``rows``
-    rows and, when ``dx``, of W^T for its routed bf16-split input-grad GEMMs — taken from the active
-    image_scope or built in one launch."""
+def _forward_images(params, n, rows, dev, dx, first=0):
+    """{layer: image} of W for the routed bf16-split forward GEMMs (layers >= ``first``) of an
+    n-layer MLP call on ``rows`` rows and, when ``dx``, of W^T for its routed bf16-split input-grad
+    GEMMs — taken from the active image_scope or built in one launch."""
     fwd, dxi = {}, {}
-    specs = _image_specs(params, n, rows, dx)
+    specs = _image_specs(params, n, rows, dx, first)
     if not specs:
         return fwd, dxi
     if _SCOPE is not None and all((W.data_ptr(), trans) in _SCOPE for _, _, W, trans, _, _ in specs):
@@ -481,24 +512,80 @@ def _hidden_forward(h, W, b, images=None, i=0):
     return F.elu(torch.addmm(b, h, W.t()))
 
 
+def _mlp_forward_layers(h, params, n, fimg, first, acts):
+    """Layers ``first`` .. n-1 of an n-layer MLP from h (layer ``first``'s input, appended to
+    ``acts`` with every later layer's input); returns the output."""
+    acts.append(h)
+    for i in range(first, n):
+        W, b = params[2 * i], params[2 * i + 1]
+        if i == n - 1 and _skinny_ok(h, W):
+            h = _skinny_forward(h, W, b)
+        elif i < n - 1:
+            h = _hidden_forward(h, W, b, fimg, i)
+        else:
+            h = torch.addmm(b, h, W.t())
+        if i < n - 1:
+            acts.append(h)
+    return h
+
+
+def _mlp_backward_layers(g, ins, Ws, n, dximg, need_x, red):
+    """The backward of an n-layer MLP from the output gradient g: ins = the inputs of every layer
+    (x, y_0 .. y_{n-2}), Ws its weights; returns ([dW_0, db_0, ..], dx or None).  The column sums
+    go to ``red`` (launched by the caller)."""
+    grads = [None] * (2 * n)
+    g = g.contiguous()
+    gx = None
+    pre = None  # (gh, gb) of layer i when the layer above produced them in its input-grad GEMM
+    for i in range(n - 1, -1, -1):
+        need_dx = i > 0 or need_x
+        gnext = None
+        if i == n - 1 and _skinny_ok(ins[i], Ws[i]):
+            if i > 0 and SKINNY_ACT:
+                # output layer: dW, db and the layer below's pre-activation gradient + bias
+                # gradient partials (its ELU backward fused into the skinny dX pass)
+                grads[2 * i], grads[2 * i + 1], gh_prev, gb_prev = _skinny_backward_act(g, ins[i], Ws[i], red)
+                pre = (gh_prev, gb_prev)
+            else:
+                # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
+                grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx, red)
+        else:
+            if pre is not None:
+                gh, gb = pre
+                pre = None
+            else:
+                rows, width = g.shape
+                gb = torch.empty(width, dtype=torch.float32, device=g.device)
+                # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
+                gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb, red)
+            grads[2 * i + 1] = gb
+            grads[2 * i] = _weight_grad(gh, ins[i], red)
+            if need_dx:
+                tile = _gemm_dx_tile(gh, Ws[i], ins[i]) if i > 0 else 0
+                if tile:
+                    # layer i-1's pre-activation gradient and bias gradient straight from this GEMM
+                    gb_prev = torch.empty(Ws[i].shape[1], dtype=torch.float32, device=gh.device)
+                    pre = (gemm_input_grad(gh, Ws[i], ins[i], gb_prev, red, tile, _img_for(dximg, i, tile)),
+                           gb_prev)
+                else:
+                    gnext = torch.mm(gh, Ws[i])
+        if i > 0:
+            # the next (lower) layer's incoming gradient goes through its ELU backward
+            g = gnext
+        else:
+            gx = gnext
+    return grads, gx
+
+
 class _MLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params):
         n = len(params) // 2
-        acts = [x]
-        h = x
         fimg, ctx.dximg = _forward_images(params, n, x.shape[0], x.device, any(ctx.needs_input_grad))
-        for i in range(n):
-            W, b = params[2 * i], params[2 * i + 1]
-            if i == n - 1 and _skinny_ok(h, W):
-                h = _skinny_forward(h, W, b)
-            elif i < n - 1:
-                h = _hidden_forward(h, W, b, fimg, i)
-            else:
-                h = torch.addmm(b, h, W.t())
-            acts.append(h)
+        acts = []
+        h = _mlp_forward_layers(x, params, n, fimg, 0, acts)
         # inputs of every layer (x, y_0 .. y_{n-2}) and the weights
-        ctx.save_for_backward(*acts[:-1], *params[0::2])
+        ctx.save_for_backward(*acts, *params[0::2])
         ctx.n = n
         return h
 
@@ -507,52 +594,100 @@ class _MLP(torch.autograd.Function):
         n = ctx.n
         saved = ctx.saved_tensors
         ins, Ws = saved[:n], saved[n:]
-        grads = [None] * (2 * n)
-        g = g.contiguous()
-        gx = None
         red = _Reductions() if DEFER_REDUCTIONS else None
-        pre = None  # (gh, gb) of layer i when the layer above produced them in its input-grad GEMM
-        for i in range(n - 1, -1, -1):
-            need_dx = i > 0 or ctx.needs_input_grad[0]
-            gnext = None
-            if i == n - 1 and _skinny_ok(ins[i], Ws[i]):
-                if i > 0 and SKINNY_ACT:
-                    # output layer: dW, db and the layer below's pre-activation gradient + bias
-                    # gradient partials (its ELU backward fused into the skinny dX pass)
-                    grads[2 * i], grads[2 * i + 1], gh_prev, gb_prev = _skinny_backward_act(g, ins[i], Ws[i], red)
-                    pre = (gh_prev, gb_prev)
-                else:
-                    # output layer: dW, db and dx as streaming passes (hg_linear_skinny_backward)
-                    grads[2 * i], grads[2 * i + 1], gnext = _skinny_backward(g, ins[i], Ws[i], need_dx, red)
-            else:
-                if pre is not None:
-                    gh, gb = pre
-                    pre = None
-                else:
-                    rows, width = g.shape
-                    gb = torch.empty(width, dtype=torch.float32, device=g.device)
-                    # layer i's output is ins[i + 1] (the ELU output) for hidden layers; identity for the last
-                    gh = _act_backward(g, ins[i + 1] if i < n - 1 else None, rows, width, gb, red)
-                grads[2 * i + 1] = gb
-                grads[2 * i] = _weight_grad(gh, ins[i], red)
-                if need_dx:
-                    tile = _gemm_dx_tile(gh, Ws[i], ins[i]) if i > 0 else 0
-                    if tile:
-                        # layer i-1's pre-activation gradient and bias gradient straight from this GEMM
-                        gb_prev = torch.empty(Ws[i].shape[1], dtype=torch.float32, device=gh.device)
-                        pre = (gemm_input_grad(gh, Ws[i], ins[i], gb_prev, red, tile, _img_for(ctx.dximg, i, tile)),
-                               gb_prev)
-                    else:
-                        gnext = torch.mm(gh, Ws[i])
-            if i > 0:
-                # the next (lower) layer's incoming gradient goes through its ELU backward
-                g = gnext
-            else:
-                gx = gnext
+        grads, gx = _mlp_backward_layers(g, ins, Ws, n, ctx.dximg, ctx.needs_input_grad[0], red)
         if red is not None:
             red.launch(ins[0].device)
         ctx.dximg = None
         return (gx, *grads)
+
+
+# Two MLPs reading the same input (the actor and the lin-vel estimator, both on the actor
+# observations: actor_critic.py act / base_get_lin_vel) with their first layers as ONE GEMM: the
+# stacked weight [n_a + n_b, K] from a stacked image (x6_images "stack", no weight copy), bias +
+# ELU in the epilogue, each network's columns stored to its own contiguous [rows, n] output
+# (hg_gemm_f32_img_split), so the rest of each network and its backward run exactly as apart.
+# (K, n_a + n_b) -> [(max rows, tile)]: 705 -> 640 at 24576 rows on tile 25, 143 us against 128 + 40
+# for the two products apart (scripts/gemm_tile_sweep.py, profiles/r5_gemm/gemm_tile_sweep.json).
+_PAIR_FWD = {(705, 640): [(8192, 0), (_BIG, 25)]}
+PAIR_FIRST = os.environ.get("HG_PAIR_FIRST", "1") != "0"
+
+
+def pair_ok(net_a, net_b, rows):
+    """net_a and net_b (fusable, fp32) can run their first layers as one stacked GEMM on ``rows``."""
+    if not (PAIR_FIRST and GEMM and X6_IMAGE and fusable(net_a) and fusable(net_b)):
+        return False
+    la, lb = net_a[0], net_b[0]
+    if len(net_a) < 3 or len(net_b) < 3 or la.in_features != lb.in_features or la.out_features % 256:
+        return False
+    ps = (la.weight, lb.weight, la.bias, lb.bias)
+    if not all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in ps):
+        return False
+    return _route(_PAIR_FWD, rows, la.in_features, la.out_features + lb.out_features) >= X6_TILE0
+
+
+class _MLPPair(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, na, *params):
+        pa, pb = params[:2 * na], params[2 * na:]
+        nb = len(pb) // 2
+        rows, K = x.shape
+        Wa, Wb = pa[0], pb[0]
+        ma, mb = Wa.shape[0], Wb.shape[0]
+        key = ("stack", Wa.data_ptr(), Wb.data_ptr())
+        img = _SCOPE.get(key) if _SCOPE is not None else None
+        if img is None:
+            img = x6_images([("stack", (Wa, Wb), K)], x.device)[0]
+        tile = _route(_PAIR_FWD, rows, K, ma + mb)
+        b0 = torch.cat((pa[1], pb[1]))
+        ha = torch.empty(rows, ma, dtype=torch.float32, device=x.device)
+        hb = torch.empty(rows, mb, dtype=torch.float32, device=x.device)
+        # one GEMM, each network's columns into its own contiguous output (the later layers and the
+        # backward then see exactly the operands of the separate calls)
+        rc = N.lib().hg_gemm_f32_img_split(x.data_ptr(), x.stride(0), img.data_ptr(), b0.data_ptr(), ha.data_ptr(), ma,
+                                           hb.data_ptr(), mb, ma, rows, ma + mb, K, 1, tile,
+                                           img.numel() * img.element_size(), _stream(x.device))
+        if rc != 0:
+            raise RuntimeError(f"hg_gemm_f32_img_split (paired first layers) failed ({rc})")
+        need = any(ctx.needs_input_grad)
+        fa, ctx.dxa = _forward_images(pa, na, rows, x.device, need, first=1)
+        fb, ctx.dxb = _forward_images(pb, nb, rows, x.device, need, first=1)
+        acts_a, acts_b = [x], [x]
+        ya = _mlp_forward_layers(ha, pa, na, fa, 1, acts_a)
+        yb = _mlp_forward_layers(hb, pb, nb, fb, 1, acts_b)
+        ctx.save_for_backward(*acts_a, *acts_b, *pa[0::2], *pb[0::2])
+        ctx.na, ctx.nb = na, nb
+        return ya, yb
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        na, nb = ctx.na, ctx.nb
+        saved = ctx.saved_tensors
+        ins_a, ins_b = saved[:na], saved[na:na + nb]
+        Wsa, Wsb = saved[na + nb:2 * na + nb], saved[2 * na + nb:]
+        red = _Reductions() if DEFER_REDUCTIONS else None
+        need_x = ctx.needs_input_grad[0]
+        dev = ins_a[0].device
+        if ga is None:
+            ga = torch.zeros(ins_a[0].shape[0], Wsa[-1].shape[0], dtype=torch.float32, device=dev)
+        if gb is None:
+            gb = torch.zeros(ins_b[0].shape[0], Wsb[-1].shape[0], dtype=torch.float32, device=dev)
+        grads_a, gxa = _mlp_backward_layers(ga, ins_a, Wsa, na, ctx.dxa, need_x, red)
+        grads_b, gxb = _mlp_backward_layers(gb, ins_b, Wsb, nb, ctx.dxb, need_x, red)
+        if red is not None:
+            red.launch(dev)
+        ctx.dxa = ctx.dxb = None
+        gx = None if not need_x else gxa + gxb
+        return (gx, None, *grads_a, *grads_b)
+
+
+def mlp_pair_forward(net_a, net_b, x):
+    """(net_a(x), net_b(x)) with the two first layers as one stacked GEMM (pair_ok) and the fused
+    backward of each network; the separate mlp_forward calls otherwise."""
+    if x.dim() == 2 and x.is_cuda and x.dtype == torch.float32 and x.stride(1) == 1 and pair_ok(net_a, net_b, x.shape[0]):
+        pa, pb = _params(net_a), _params(net_b)
+        return _MLPPair.apply(x, len(pa) // 2, *pa, *pb)
+    return mlp_forward(net_a, x), mlp_forward(net_b, x)
 
 
 def _params(net):

@@ -444,13 +444,22 @@ class PPO:
         outputs in one fused HIP forward launch pair and one backward launch (hg_loss.py).
         Returns (loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean]."""
         ac = self.actor_critic
+        own = ac.policy_dtype == "fp32" and ac.fused_mlp and obs_b.is_cuda
+        # the actor and the lin-vel estimator read the same observations: their first layers as one
+        # stacked GEMM (hg_mlp.mlp_pair_forward) where it is routed
+        pair = (own and obs_b.dtype == torch.float32 and obs_b.dim() == 2 and obs_b.stride(1) == 1
+                and hg_mlp.pair_ok(ac.actor, ac.base_lin_vel, obs_b.shape[0]))
         scope = (hg_mlp.image_scope([(ac.actor, obs_b.shape[0]), (ac.base_lin_vel, obs_b.shape[0]),
-                                     (ac.critic, critic_b.shape[0])], obs_b.device)
-                 if ac.policy_dtype == "fp32" and ac.fused_mlp and obs_b.is_cuda else contextlib.nullcontext())
+                                     (ac.critic, critic_b.shape[0])], obs_b.device,
+                                    pairs=[(ac.actor, ac.base_lin_vel, obs_b.shape[0])] if pair else ())
+                 if own else contextlib.nullcontext())
         with scope:  # the three networks' weight images in one launch
-            mu = ac._mlp(ac.actor, obs_b)
+            if pair:
+                mu, est_lin_vel = hg_mlp.mlp_pair_forward(ac.actor, ac.base_lin_vel, obs_b)
+            else:
+                mu = ac._mlp(ac.actor, obs_b)
+                est_lin_vel = ac.base_get_lin_vel(obs_b)
             ac.distribution = _DiagGaussian(mu, ac.std.expand_as(mu))
-            est_lin_vel = ac.base_get_lin_vel(obs_b)
             value_b = ac.evaluate(critic_b)
         data = {"actions": actions_b, "old_logp": old_logp_b, "advantages": adv_b, "target_values": target_values_b,
                 "returns": returns_b, "old_mu": old_mu_b, "old_sigma": old_sigma_b,

@@ -514,6 +514,14 @@ int64_t hg_gemm_colpart_rows(int64_t M, int tile);
 int64_t hg_gemm_x6_image_bytes(int64_t rows, int64_t K);
 int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* trans, const int64_t* rows,
                           const int64_t* K, void* const* img, int njobs, void* stream);
+/* hg_gemm_x6_image_jobs writing row bands of shared images: pitch_rows[j] (> 0; <= 0 or a NULL
+ * array: rows[j]) is the row count of the image job j writes into, img[j] = that image + the
+ * band's first row (a multiple of 32) x 32 bytes.  Jobs over the same K fill one image of the
+ * stacked rows, e.g. the first layers of two MLPs reading the same input as one [n_a + n_b, K]
+ * forward operand (hg_mlp.py mlp_pair_forward).  pitch_rows >= rows. */
+int hg_gemm_x6_image_jobs_pitched(const float* const* P, const int64_t* ld, const int* trans, const int64_t* rows,
+                                  const int64_t* K, void* const* img, const int64_t* pitch_rows, int njobs,
+                                  void* stream);
 /* hg_gemm_f32 modes 0 / 1 on a bf16-split tile with B from its image (Bimg: rows N, reduction K)
  * and A from its image (Aimg: rows M) or, Aimg NULL, staged from A (lda) as in hg_gemm_f32 — the
  * same epilogues and, bit for bit, the same result.  aimg_bytes / bimg_bytes: the images' sizes,
@@ -522,6 +530,13 @@ int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* t
 int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, const void* Bimg, const float* bias,
                     const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K,
                     int act, int tile, int64_t aimg_bytes, int64_t bimg_bytes, void* stream);
+/* hg_gemm_f32_img mode 0 (A staged from lda) writing its columns in two contiguous outputs: column
+ * c < nsplit to C[r ldc + c], c >= nsplit to C2[r ldc2 + c - nsplit] (nsplit a multiple of 256,
+ * 0 < nsplit < N) — one GEMM over two layers' stacked weights (hg_gemm_x6_image_jobs_pitched)
+ * with each layer's output in its own [M, n] buffer. */
+int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const float* bias, float* C, int64_t ldc,
+                          float* C2, int64_t ldc2, int nsplit, int64_t M, int N, int K, int act, int tile,
+                          int64_t bimg_bytes, void* stream);
 /* hg_gemm_f32_wgrad's split-K weight gradient from two images (Aimg: rows M, Bimg: rows N, both
  * with reduction K — build them with trans 1 from the row-major gh [K, M] and x [K, N]); the
  * slices start on 32-deep chunk pairs, ceil(K / slices) rounded up to a multiple of 32 rows each.

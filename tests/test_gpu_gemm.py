@@ -325,6 +325,43 @@ def test_mlp_backward_with_fused_gemm_matches_autograd():
         assert any(c[0] == "f" for c in calls), calls
 
 
+def test_paired_first_layers_match_separate_networks():
+    """hg_mlp.mlp_pair_forward (the actor's and the lin-vel estimator's first layers as ONE stacked
+    GEMM from a stacked image, the rest of each network on strided column slices of its result)
+    against the two networks run apart through hg_mlp: the same products on the same operands, so
+    outputs and every parameter gradient bit for bit; and against torch autograd at the MLP test's
+    tolerance.  Also inside an image_scope that builds the stacked image with the other images."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, hg_mlp
+    torch.manual_seed(12)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     base_lin_vel_hidden_dims=[128, 128]).cuda()
+    rows = 24576
+    assert hg_mlp.pair_ok(ac.actor, ac.base_lin_vel, rows)
+    x = torch.randn(rows, 705, device="cuda:0")
+    params = [*ac.actor.parameters(), *ac.base_lin_vel.parameters()]
+    ya0 = hg_mlp.mlp_forward(ac.actor, x)
+    yb0 = hg_mlp.mlp_forward(ac.base_lin_vel, x)
+    ga, gb = torch.randn_like(ya0), torch.randn_like(yb0)
+    ref = torch.autograd.grad((ya0, yb0), params, (ga, gb))
+    for scoped in (False, True):
+        ctx = (hg_mlp.image_scope([(ac.actor, rows), (ac.base_lin_vel, rows)], x.device,
+                                  pairs=[(ac.actor, ac.base_lin_vel, rows)]) if scoped else hg_mlp.contextlib.nullcontext())
+        with ctx:
+            ya, yb = hg_mlp.mlp_pair_forward(ac.actor, ac.base_lin_vel, x)
+            got = torch.autograd.grad((ya, yb), params, (ga, gb))
+        assert torch.equal(ya, ya0) and torch.equal(yb, yb0)
+        for a, b_ in zip(got, ref):
+            assert torch.equal(a, b_), (a - b_).abs().max().item()
+    x2 = x.clone()
+    ya2, yb2 = ac.actor(x2), ac.base_lin_vel(x2)
+    ref2 = torch.autograd.grad((ya2, yb2), params, (ga, gb))
+    torch.testing.assert_close(ya, ya2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(yb, yb2, rtol=1e-5, atol=1e-5)
+    for a, b_ in zip(got, ref2):
+        assert (a - b_).abs().max().item() <= 2e-5 * (b_.abs().max().item() + 1e-12) + 1e-6
+
+
 @pytest.mark.parametrize("rows,n", [(24576, 12), (777, 3), (64, 1), (65, 12)])
 def test_skinny_backward_act_matches_fp64(rows, n):
     """hg_linear_skinny_backward_act: the output layer's dW / db partials and its input gradient
