@@ -58,6 +58,7 @@ struct GemmArgs {
   float* C2;
   int64_t ldc2;
   int nsplit;
+  const float* bias2;  // the bias of the columns >= nsplit (bias2[c - nsplit])
 };
 
 template <int LAY>
@@ -185,14 +186,15 @@ __device__ __forceinline__ void mma_chunk(const float* __restrict__ As, const fl
 // forward (stores count on that counter too).  Values, stores and the column-sum order unchanged.
 template <int TM, int TN, bool ELU, bool BIAS>
 __device__ __forceinline__ void epi_forward(const f32x16 (&acc)[TM][TN], const GemmArgs& g, float* __restrict__ C,
-                                            int64_t row0, int col0, int i, int h, int64_t ldc, int cshift) {
+                                            int64_t row0, int col0, int i, int h, int64_t ldc, int cshift,
+                                            const float* __restrict__ bias) {
   const int64_t mmax = g.M - 1;
   const int nmax = g.N - 1;
 #pragma unroll
   for (int n = 0; n < TN; n++) {
     const int cidx = col0 + 32 * n + i;
     float bc = 0.f;
-    if (BIAS) bc = g.bias[min(cidx, nmax)];
+    if (BIAS) bc = bias[min(cidx, nmax) - cshift];
     asm volatile("" : "+v"(bc));  // the bias load retires here, once
     if (cidx > nmax) continue;
 #pragma unroll
@@ -343,8 +345,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm(GemmArgs g) {
 
   // epilogue (epi_forward / epi_input_grad)
   if (MODE == 0) {
-    if (g.bias) epi_forward<TM, TN, ELU, true>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h, g.ldc, 0);
-    else epi_forward<TM, TN, ELU, false>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h, g.ldc, 0);
+    if (g.bias) epi_forward<TM, TN, ELU, true>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h, g.ldc, 0, g.bias);
+    else epi_forward<TM, TN, ELU, false>(acc, g, g.C, m0 + wm0, n0 + wn0, i, h, g.ldc, 0, g.bias);
   } else {
     float* red = lds;  // [WGM][BN] column partials of the waves along M (staging buffers are free)
     float cs[TN];
@@ -780,13 +782,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
     float* Cs = g.C + (SPLITK ? (int64_t)slice * xa.cstride : 0);  // mode 3 takes the input-grad epilogue
     int64_t ldcs = g.ldc;
     int cshift = 0;
+    const float* bs = g.bias;
     if (MODE == 0 && g.nsplit > 0 && n0 >= g.nsplit) {  // block-uniform: the split is a multiple of BN
       Cs = g.C2;
       ldcs = g.ldc2;
       cshift = g.nsplit;
+      bs = g.bias2;
     }
-    if (MODE == 0 && g.bias) epi_forward<TM, TN, MODE == 0 && ELU, true>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h, ldcs, cshift);
-    else epi_forward<TM, TN, MODE == 0 && ELU, false>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h, ldcs, cshift);
+    if (MODE == 0 && g.bias) epi_forward<TM, TN, MODE == 0 && ELU, true>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h, ldcs, cshift, bs);
+    else epi_forward<TM, TN, MODE == 0 && ELU, false>(acc, g, Cs, m0 + wm0, n0 + wn0, i, h, ldcs, cshift, bs);
   } else {
     float* red = reinterpret_cast<float*>(lds);  // [WGM][BN] column partials of the waves along M
     float cs[TN];
@@ -1261,17 +1265,17 @@ extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void
   return x6_img_dispatch(tile, mode, Aimg ? 3 : 1, xa, vec, act == 1, (hipStream_t)stream);
 }
 
-extern "C" int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const float* bias, float* C,
-                                     int64_t ldc, float* C2, int64_t ldc2, int nsplit, int64_t M, int N, int K, int act,
-                                     int tile, int64_t bimg_bytes, void* stream) {
-  if (!A || !Bimg || !C || !C2 || M <= 0 || N <= 0 || K <= 0 || nsplit <= 0 || nsplit >= N || nsplit % 256 ||
+extern "C" int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const float* bias,
+                                     const float* bias2, float* C, int64_t ldc, float* C2, int64_t ldc2, int nsplit,
+                                     int64_t M, int N, int K, int act, int tile, int64_t bimg_bytes, void* stream) {
+  if (!A || !Bimg || !C || !C2 || !bias != !bias2 || M <= 0 || N <= 0 || K <= 0 || nsplit <= 0 || nsplit >= N || nsplit % 256 ||
       ldc < nsplit || ldc2 < N - nsplit || lda < K || act < 0 || act > 1 || tile < 19 || tile > NTILES)
     return HG_ERR_ARG;
   if (bimg_bytes != hg_gemm_x6_image_bytes(N, K)) return HG_ERR_ARG;
   if ((uintptr_t)A % 4 || (uintptr_t)Bimg % 16 || (uintptr_t)C % 4 || (uintptr_t)C2 % 4) return HG_ERR_ARG;
   const bool vec = lda % 4 == 0 && (uintptr_t)A % 16 == 0;
   GemmArgs g{A, lda, reinterpret_cast<const float*>(Bimg), img_rows(N) * 2, bias, nullptr, 0, C, ldc, nullptr, M, N, K,
-             0, 0, C2, ldc2, nsplit};
+             0, 0, C2, ldc2, nsplit, bias2};
   GemmX6Args xa{g, 0, 0, 1};
   return x6_img_dispatch(tile, 0, 1, xa, vec, act == 1, (hipStream_t)stream);
 }

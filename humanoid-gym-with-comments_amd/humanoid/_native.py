@@ -279,7 +279,7 @@ def load_library(path=LIB_PATH):
                                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(vp),
                                                 ctypes.POINTER(ctypes.c_int64), ctypes.c_int, vp]
     L.hg_gemm_f32_img_split.restype = ctypes.c_int
-    L.hg_gemm_f32_img_split.argtypes = [vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int,
+    L.hg_gemm_f32_img_split.argtypes = [vp, ctypes.c_int64, vp, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int64, vp]
     L.hg_gemm_f32_img.restype = ctypes.c_int

@@ -605,7 +605,7 @@ class _MLP(torch.autograd.Function):
 # Two MLPs reading the same input (the actor and the lin-vel estimator, both on the actor
 # observations: actor_critic.py act / base_get_lin_vel) with their first layers as ONE GEMM: the
 # stacked weight [n_a + n_b, K] from a stacked image (x6_images "stack", no weight copy), bias +
-# ELU in the epilogue, each network's columns stored to its own contiguous [rows, n] output
+# ELU in the epilogue (each network's own bias), each network's columns stored to its own contiguous [rows, n] output
 # (hg_gemm_f32_img_split), so the rest of each network and its backward run exactly as apart.
 # (K, n_a + n_b) -> [(max rows, tile)]: 705 -> 640 at 24576 rows on tile 25, 143 us against 128 + 40
 # for the two products apart (scripts/gemm_tile_sweep.py, profiles/r5_gemm/gemm_tile_sweep.json).
@@ -639,12 +639,12 @@ class _MLPPair(torch.autograd.Function):
         if img is None:
             img = x6_images([("stack", (Wa, Wb), K)], x.device)[0]
         tile = _route(_PAIR_FWD, rows, K, ma + mb)
-        b0 = torch.cat((pa[1], pb[1]))
         ha = torch.empty(rows, ma, dtype=torch.float32, device=x.device)
         hb = torch.empty(rows, mb, dtype=torch.float32, device=x.device)
         # one GEMM, each network's columns into its own contiguous output (the later layers and the
         # backward then see exactly the operands of the separate calls)
-        rc = N.lib().hg_gemm_f32_img_split(x.data_ptr(), x.stride(0), img.data_ptr(), b0.data_ptr(), ha.data_ptr(), ma,
+        rc = N.lib().hg_gemm_f32_img_split(x.data_ptr(), x.stride(0), img.data_ptr(), pa[1].data_ptr(), pb[1].data_ptr(),
+                                           ha.data_ptr(), ma,
                                            hb.data_ptr(), mb, ma, rows, ma + mb, K, 1, tile,
                                            img.numel() * img.element_size(), _stream(x.device))
         if rc != 0:

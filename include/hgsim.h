@@ -531,12 +531,13 @@ int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void* Aimg, con
                     const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K,
                     int act, int tile, int64_t aimg_bytes, int64_t bimg_bytes, void* stream);
 /* hg_gemm_f32_img mode 0 (A staged from lda) writing its columns in two contiguous outputs: column
- * c < nsplit to C[r ldc + c], c >= nsplit to C2[r ldc2 + c - nsplit] (nsplit a multiple of 256,
- * 0 < nsplit < N) — one GEMM over two layers' stacked weights (hg_gemm_x6_image_jobs_pitched)
- * with each layer's output in its own [M, n] buffer. */
-int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const float* bias, float* C, int64_t ldc,
-                          float* C2, int64_t ldc2, int nsplit, int64_t M, int N, int K, int act, int tile,
-                          int64_t bimg_bytes, void* stream);
+ * c < nsplit to C[r ldc + c] with bias[c], c >= nsplit to C2[r ldc2 + c - nsplit] with
+ * bias2[c - nsplit] (nsplit a multiple of 256, 0 < nsplit < N; both biases or neither) — one GEMM
+ * over two layers' stacked weights (hg_gemm_x6_image_jobs_pitched), each layer's bias and output
+ * its own. */
+int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const float* bias, const float* bias2,
+                          float* C, int64_t ldc, float* C2, int64_t ldc2, int nsplit, int64_t M, int N, int K, int act,
+                          int tile, int64_t bimg_bytes, void* stream);
 /* hg_gemm_f32_wgrad's split-K weight gradient from two images (Aimg: rows M, Bimg: rows N, both
  * with reduction K — build them with trans 1 from the row-major gh [K, M] and x [K, N]); the
  * slices start on 32-deep chunk pairs, ceil(K / slices) rounded up to a multiple of 32 rows each.
