@@ -1,7 +1,9 @@
 """The update's large GEMMs in isolation, for PMC passes (scripts/pmc_gemm.sh): the routed x6
 forward 705->512 (tile 20, weight image), the x6 input gradient 256->768 (tile 22, W^T image,
-ELU backward), the weight gradient 512x705 on k_wgrad_tr (tile 40, 32 slices) and on hipBLASLt
-(torch.mm, the committed TunableOp table), at the 24576-row minibatch; ITERS launches each."""
+ELU backward), the weight gradient 512x705 on k_wgrad_tr (tile 40, 32 slices; round 5: also the
+routed tile 49) and on hipBLASLt (torch.mm, the committed TunableOp table), and (round 5) the
+paired first layers 705->640 (tile 25, stacked image, split output), at the 24576-row minibatch;
+ITERS launches each.  scripts/gemm_sq_summary.py turns the PMC passes into per-kernel figures."""
 import os
 import sys
 
@@ -34,6 +36,9 @@ def main():
     out_d = torch.empty(R, 768, device=dev)
     cp = torch.empty(int(L.hg_gemm_colpart_rows(R, 22)), 768, device=dev)
     part = torch.empty(32, 512, 705, device=dev)
+    Wl, bl = torch.randn(128, 705, device=dev) * 0.03, torch.zeros(128, device=dev)
+    img_p = hg_mlp.x6_images([("stack", (W1, Wl), 705)], dev)[0]
+    out_l = torch.empty(R, 128, device=dev)
     for _ in range(ITERS):
         for img, out in ((img_f, out_f),):
             N.check(L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), None, img.data_ptr(), b1.data_ptr(), None, 0,
@@ -44,6 +49,11 @@ def main():
                                   img_d.numel() * img_d.element_size(), s))
         N.check(L.hg_gemm_f32_wgrad(gh.data_ptr(), gh.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), 705,
                                     512 * 705, 512, 705, R, 32, 0, 40, s))
+        N.check(L.hg_gemm_f32_wgrad(gh.data_ptr(), gh.stride(0), x.data_ptr(), x.stride(0), part.data_ptr(), 705,
+                                    512 * 705, 512, 705, R, 32, 0, 49, s))
+        N.check(L.hg_gemm_f32_img_split(x.data_ptr(), x.stride(0), img_p.data_ptr(), b1.data_ptr(), bl.data_ptr(),
+                                        out_f.data_ptr(), 512, out_l.data_ptr(), 128, 512, R, 640, 705, 1, 25,
+                                        img_p.numel() * img_p.element_size(), s))
         torch.mm(gh.t(), x)
     torch.cuda.synchronize()
     print("done", flush=True)
