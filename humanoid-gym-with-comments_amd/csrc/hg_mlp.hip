@@ -601,7 +601,7 @@ struct ColsumJobs {
   float* dst[CJ_MAX];
   int64_t width[CJ_MAX];
   int parts[CJ_MAX];
-  int wide[CJ_MAX];        // four columns per thread (see above)
+  int wide[CJ_MAX];        // 1: four columns per thread; 2: eight threads per four columns (see above)
   int block0[CJ_MAX + 1];  // first block of each job; block0[njobs] = grid size
   int njobs;
 };
@@ -614,6 +614,44 @@ __global__ void __launch_bounds__(TPB) k_colsum_jobs(ColsumJobs J) {
   const int64_t width = J.width[j];
   const int parts = J.parts[j];
   const int lb = bid - J.block0[j];
+  if (J.wide[j] == 2) {
+    // many parts: eight threads per four columns, thread u summing parts u, u + 8, u + 16, .. in
+    // order (its loads all in flight at once), the eight sums combined in LDS by the fixed tree —
+    // the interleaved-accumulator order below, so the same bits, with 8x the waves in flight
+    constexpr int CW = TPB / 8;  // float4 columns per block
+    const int u = threadIdx.x / CW, cl = threadIdx.x % CW;
+    const int64_t c4 = (int64_t)lb * CW + cl;
+    const int64_t w4 = width / 4;
+    const float4* __restrict__ s4 = reinterpret_cast<const float4*>(src) + c4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < w4) {
+      int p = u;
+      for (; p + 56 < parts; p += 64) {  // eight loads per round, issued together
+        float4 x[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = s4[(int64_t)(p + 8 * q) * w4];
+#pragma unroll
+        for (int q = 0; q < 8; q++) { acc.x += x[q].x; acc.y += x[q].y; acc.z += x[q].z; acc.w += x[q].w; }
+      }
+      for (; p < parts; p += 8) {
+        const float4 x = s4[(int64_t)p * w4];
+        acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+      }
+    }
+    __shared__ float4 red4[8][CW];
+    red4[u][cl] = acc;
+    __syncthreads();
+    if (u == 0 && c4 < w4) {
+      auto tree = [&](int k) {
+        const float* r0 = &red4[0][cl].x;
+        const int st = CW * 4;
+        return ((r0[k] + r0[st + k]) + (r0[2 * st + k] + r0[3 * st + k])) +
+               ((r0[4 * st + k] + r0[5 * st + k]) + (r0[6 * st + k] + r0[7 * st + k]));
+      };
+      reinterpret_cast<float4*>(J.dst[j])[c4] = make_float4(tree(0), tree(1), tree(2), tree(3));
+    }
+    return;
+  }
   if (J.wide[j]) {
     const int64_t c4 = (int64_t)lb * TPB + threadIdx.x;
     if (4 * c4 >= width) return;
@@ -701,9 +739,11 @@ extern "C" int hg_colsum_jobs(const float* const* src, float* const* dst, const 
     J.width[j] = width[j];
     J.parts[j] = parts[j];
     J.wide[j] = width[j] >= CJ_WIDE && width[j] % 4 == 0 && (uintptr_t)src[j] % 16 == 0 && (uintptr_t)dst[j] % 16 == 0;
+    if (J.wide[j] && parts[j] > CJ_SEQ_MAXPARTS) J.wide[j] = 2;  // eight threads per four columns
     J.block0[j] = (int)blocks;
-    blocks += J.wide[j] ? (width[j] / 4 + TPB - 1) / TPB
-                        : parts[j] <= CJ_SEQ_MAXPARTS ? (width[j] + TPB - 1) / TPB : (width[j] + FC - 1) / FC;
+    blocks += J.wide[j] == 2 ? (width[j] / 4 + TPB / 8 - 1) / (TPB / 8)
+              : J.wide[j] ? (width[j] / 4 + TPB - 1) / TPB
+                          : parts[j] <= CJ_SEQ_MAXPARTS ? (width[j] + TPB - 1) / TPB : (width[j] + FC - 1) / FC;
     if (blocks > (int64_t)1 << 30) return HG_ERR_ARG;
   }
   J.block0[njobs] = (int)blocks;
