@@ -91,3 +91,32 @@ def test_model_table():
     bodies = [b["name"] for b in js["bodies"]]
     assert bodies.index("left_ankle_roll_link") == 6 and bodies.index("right_ankle_roll_link") == 12
     assert bodies.index("left_knee_link") == 4 and bodies.index("right_knee_link") == 10
+
+
+def test_stacked_image_and_split_gemm_reject_bad_arguments():
+    """hg_gemm_x6_image_jobs_pitched and hg_gemm_f32_img_split validate their arguments before any
+    device work (CPU: every call here is refused, nothing is launched)."""
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("libhgsim.so not built")
+    L = N.load_library()
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    fake = vp(0x10000)  # 16-byte aligned, never dereferenced on a refused call
+    P, ld, tr = (vp * 1)(fake), (i64 * 1)(705), (ctypes.c_int * 1)(0)
+    rows, K, img = (i64 * 1)(128), (i64 * 1)(705), (vp * 1)(fake)
+    # pitch rows below the job's rows
+    assert L.hg_gemm_x6_image_jobs_pitched(P, ld, tr, rows, K, img, (i64 * 1)(64), 1, None) != 0
+    nbytes = L.hg_gemm_x6_image_bytes(640, 705)
+    args = dict(A=fake, lda=705, Bimg=fake, bias=fake, bias2=fake, C=fake, ldc=512, C2=fake, ldc2=128, nsplit=512,
+                M=24576, N=640, K=705, act=1, tile=25, nbytes=nbytes)
+
+    def call(**kw):
+        a = dict(args, **kw)
+        return L.hg_gemm_f32_img_split(a["A"], a["lda"], a["Bimg"], a["bias"], a["bias2"], a["C"], a["ldc"], a["C2"],
+                                       a["ldc2"], a["nsplit"], a["M"], a["N"], a["K"], a["act"], a["tile"],
+                                       a["nbytes"], None)
+    assert call(nsplit=500) != 0          # not a multiple of 256
+    assert call(nsplit=640) != 0          # no second band
+    assert call(bias2=None) != 0          # one bias without the other
+    assert call(ldc=256) != 0             # first output narrower than its band
+    assert call(nbytes=nbytes - 16) != 0  # image built for another shape
+    assert call(tile=5) != 0              # f32 tiles have no image form
