@@ -361,6 +361,23 @@ def test_step_physics_parity(physics_env):
     _step_parity(env, 77)
 
 
+def test_step_physics_parity_after_update_cfg():
+    """K_step takes its physics scalars by value from the handle's host copy of hg_cfg at each
+    launch: after hg_update_cfg changes the PGS sweeps, the contact offset and the Baumgarte
+    factor mid-run, the next step (on a contact state) matches the oracle run with the new values."""
+    _need_gpu()
+    import ctypes
+    from humanoid import _native as N
+    env = _make_env(N_ENVS)
+    for _ in range(TOUCHDOWN_STEPS):
+        env.step(torch.randn(env.num_envs, 12, device="cuda:0") * 0.3)
+    hc = env._hgcfg
+    hc.pgs_iterations, hc.contact_offset, hc.baumgarte = 2, 0.02, 0.1
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(env.hg.hg_update_cfg(env.sim, ctypes.byref(hc), stream), env.sim)
+    _step_parity(env, 91)
+
+
 @pytest.fixture(scope="module")
 def bench_env():
     """The bench's size (4096 envs: 2048 blocks, 256 per XCD, the full XCD-aware block -> env-pair
