@@ -1418,3 +1418,90 @@ extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, in
     default: return launch_x6<64, 128, 2, 2, 1>(md, xa, vec, false, s);
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Split-K forward (round 5): y = act(A W^T + b) at few rows (the rollout's 4096-row policy layers),
+// where a row tile's whole K loop on one block leaves most CUs idle and the block's per-chunk
+// latency sets the time.  k_gemm_x6 mode 4 writes S partial products (slice s: k in [s kslice,
+// (s + 1) kslice)) to a workspace ws [S][M][N]; k_splitk_finish sums them in fixed order (s = 0,
+// 1, ..., S - 1, then + b) and applies the ELU as epi_forward does.  Deterministic; the products
+// are the exact three-term splits of k_gemm_x6, only the split-K order of the sum differs from the
+// one-pass tiles.
+namespace {
+template <bool ELU>
+__global__ void __launch_bounds__(256) k_splitk_finish(const float* __restrict__ ws, int64_t sstride,
+                                                       const float* __restrict__ bias, float* __restrict__ C,
+                                                       int64_t ldc, int64_t M, int N, int S, bool vec) {
+  const int nq = (N + 3) >> 2;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= M * nq) return;
+  const int64_t m = t / nq;
+  const int n0 = (int)(t % nq) * 4;
+  const float* p = ws + m * N + n0;
+  float v[4];
+  if (vec) {  // N % 4 == 0, C rows 16-byte aligned
+    float4 a = *reinterpret_cast<const float4*>(p);
+    for (int s = 1; s < S; s++) {
+      const float4 b = *reinterpret_cast<const float4*>(p + s * sstride);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
+    v[0] = a.x + bb.x; v[1] = a.y + bb.y; v[2] = a.z + bb.z; v[3] = a.w + bb.w;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (ELU) v[q] = v[q] > 0.f ? v[q] : expm1f(v[q]);
+    *reinterpret_cast<float4*>(C + m * ldc + n0) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int q = 0; q < 4 && n0 + q < N; q++) {
+      float a = p[q];
+      for (int s = 1; s < S; s++) a += p[q + s * sstride];
+      float x = a + bias[n0 + q];
+      if (ELU) x = x > 0.f ? x : expm1f(x);
+      C[m * ldc + n0 + q] = x;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int64_t hg_gemm_splitk_kslice(int K, int slices) {
+  if (K <= 0 || slices < 1) return -1;
+  return (((int64_t)K + slices - 1) / slices + 15) & ~(int64_t)15;
+}
+
+extern "C" int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
+                                  float* C, int64_t ldc, float* ws, int64_t ws_floats, int64_t M, int N, int K,
+                                  int act, int tile, int slices, void* stream) {
+  if (!A || !B || !bias || !C || !ws || M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N ||
+      act < 0 || act > 1 || tile < 20 || tile > 28 || slices < 2 || slices > 16)
+    return HG_ERR_ARG;
+  const int64_t kslice = hg_gemm_splitk_kslice(K, slices);
+  if ((slices - 1) * kslice >= K) return HG_ERR_ARG;  // every slice holds part of the reduction
+  if (ws_floats < slices * M * (int64_t)N) return HG_ERR_ARG;
+  if ((uintptr_t)A % 4 || (uintptr_t)B % 4 || (uintptr_t)C % 4 || (uintptr_t)bias % 4 || (uintptr_t)ws % 16)
+    return HG_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  GemmArgs g{A, lda, B, ldb, nullptr, nullptr, 0, ws, N, nullptr, M, N, K, 0, 0};
+  GemmX6Args xa{g, kslice, M * (int64_t)N, slices};
+  const bool vec = lda % 4 == 0 && ldb % 4 == 0 && (uintptr_t)A % 16 == 0 && (uintptr_t)B % 16 == 0;
+  const bool elu = act == 1;
+  const int md = 4;
+  int rc;
+  switch (tile) {
+    case 20: rc = launch_x6<128, 128, 2, 2, 1>(md, xa, vec, elu, s); break;
+    case 21: rc = launch_x6<128, 128, 2, 4, 1>(md, xa, vec, elu, s); break;
+    case 22: rc = launch_x6<128, 64, 2, 2, 1>(md, xa, vec, elu, s); break;
+    case 23: rc = launch_x6<64, 64, 2, 2, 1>(md, xa, vec, elu, s); break;
+    case 24: rc = launch_x6<128, 128, 2, 2, 2>(md, xa, vec, elu, s); break;
+    case 25: rc = launch_x6<256, 128, 4, 2, 1>(md, xa, vec, elu, s); break;
+    case 26: rc = launch_x6<128, 128, 2, 4, 2>(md, xa, vec, elu, s); break;
+    case 27: rc = launch_x6<128, 256, 2, 4, 1>(md, xa, vec, elu, s); break;
+    default: rc = launch_x6<64, 256, 2, 4, 1>(md, xa, vec, elu, s); break;
+  }
+  if (rc != HG_OK) return rc;
+  const int64_t threads = M * ((N + 3) / 4);
+  const bool fvec = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)bias % 16 == 0;
+  const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+  if (elu) hipLaunchKernelGGL(k_splitk_finish<true>, grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, slices, fvec);
+  else hipLaunchKernelGGL(k_splitk_finish<false>, grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, slices, fvec);
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

@@ -310,6 +310,44 @@ def _gemm_fwd_tile(h, W, b):
     return _route(_GEMM_FWD, h.shape[0], W.shape[1], W.shape[0])
 
 
+# Split-K forwards (hg_gemm_f32_splitk): (k, n) -> [(max rows, (tile, slices))].  At the rollout's
+# 4096 rows the first policy layer's one-pass tiles leave most CUs idle behind the K loop's
+# per-chunk latency: 705 -> 512 on tile 5 40.4 us, as two split-K slices on tile 21 26.7 us + the
+# fused sum / bias / ELU pass (profiles/r5_gemm/roll_splitk/, scripts/probes/roll_splitk_probe.py;
+# the 512 -> 256 and 256 -> 128 layers gain nothing).  In the bench's kernel trace (same box):
+# 37.3 us on tile 5 -> 25.6 + 8.9 us as four slices on tile 25 (21 x 2: 28.2 + 7.0 us; r5_v4: 26.0 + 9.0); a finish
+# inside the GEMM launch (per-tile tickets, the last slice block summing) measured 97-174 us: its
+# device-scope fences write back and invalidate the XCD's L2 under every other block
+# (profiles/r5_gemm/roll_splitk/).  Rows above the bound keep _GEMM_FWD.
+_GEMM_FWD_SPLITK = {(705, 512): [(4096, (25, 4))]}
+SPLITK_FWD = os.environ.get("HG_SPLITK_FWD", "1") != "0"
+if os.environ.get("HG_SPLITK_ROUTE"):  # "tile,slices": a diagnostic override of the 705 -> 512 route
+    _GEMM_FWD_SPLITK[(705, 512)] = [(4096, tuple(int(v) for v in os.environ["HG_SPLITK_ROUTE"].split(",")))]
+
+
+def _gemm_fwd_splitk(h, W, b):
+    if not SPLITK_FWD or not _gemm_fwd_tile(h, W, b):
+        return None
+    for max_rows, route in _GEMM_FWD_SPLITK.get((W.shape[1], W.shape[0]), ()):
+        if h.shape[0] <= max_rows:
+            return route
+    return None
+
+
+def gemm_forward_splitk(h, W, b, tile, slices, elu=True):
+    """y = elu(h W^T + b) as ``slices`` split-K partial products on bf16-split ``tile`` plus one
+    fixed-order finishing launch (hg_gemm_f32_splitk); the slices' workspace is a per-call tensor."""
+    rows, n, k = h.shape[0], W.shape[0], W.shape[1]
+    y = torch.empty(rows, n, dtype=torch.float32, device=h.device)
+    ws = torch.empty(slices * rows * n, dtype=torch.float32, device=h.device)
+    rc = N.lib().hg_gemm_f32_splitk(h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), y.data_ptr(),
+                                    y.stride(0), ws.data_ptr(), ws.numel(), rows, n, k, 1 if elu else 0, tile, slices,
+                                    _stream(h.device))
+    if rc != 0:
+        raise RuntimeError(f"hg_gemm_f32_splitk failed ({rc})")
+    return y
+
+
 def _img_rows(r):
     return (r + 255) // 256 * 256
 
@@ -504,6 +542,9 @@ DEFER_REDUCTIONS = os.environ.get("HG_DEFER_REDUCTIONS", "1") != "0"
 def _hidden_forward(h, W, b, images=None, i=0):
     """One hidden layer: the LDS-staged GEMM (with layer i's B image from ``images`` when built for
     the routed tile), the register-operand fused kernel, or addmm + ELU."""
+    split = _gemm_fwd_splitk(h, W, b)
+    if split is not None:
+        return gemm_forward_splitk(h, W, b, *split)
     tile = _gemm_fwd_tile(h, W, b)
     if tile:
         return gemm_forward(h, W, b, True, tile, img=_img_for(images, i, tile))

@@ -544,6 +544,17 @@ int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bimg, const f
  * aimg_bytes / bimg_bytes as hg_gemm_f32_img. */
 int hg_gemm_wgrad_img(const void* Aimg, const void* Bimg, float* C, int64_t ldc, int64_t cstride, int64_t M, int N,
                       int64_t K, int slices, int tile, int64_t aimg_bytes, int64_t bimg_bytes, void* stream);
+/* Forward y = act(A W^T + bias) (the hidden-layer forward of actor_critic.py:53-89, as hg_gemm_f32
+ * mode 0) in `slices` (2..16) split-K passes for few rows (the rollout's policy layers): the
+ * bf16-split tile `tile` (20..28) writes slice s = sum over k in [s kslice, (s + 1) kslice)
+ * (kslice = hg_gemm_splitk_kslice(K, slices); every slice non-empty) to ws + s M N (ws 16-byte
+ * aligned, >= slices M N floats, dense [M, N] per slice), then a second launch writes
+ * C[r ldc + c] = act(ws_0 + ... + ws_{S-1} + bias[c]), summed in slice order (deterministic).
+ * A [M, K] (lda), W [N, K] (ldb) k-contiguous. */
+int64_t hg_gemm_splitk_kslice(int K, int slices);
+int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, float* C,
+                       int64_t ldc, float* ws, int64_t ws_floats, int64_t M, int N, int K, int act, int tile,
+                       int slices, void* stream);
 
 /* library build info; hg_source_hash: first 16 hex digits of the sha256 of the sources the
  * library was built from (the Makefile's SRCS, csrc/hg_common.h, include/hgsim.h, concatenated) */

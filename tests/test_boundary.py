@@ -120,3 +120,31 @@ def test_stacked_image_and_split_gemm_reject_bad_arguments():
     assert call(ldc=256) != 0             # first output narrower than its band
     assert call(nbytes=nbytes - 16) != 0  # image built for another shape
     assert call(tile=5) != 0              # f32 tiles have no image form
+
+
+def test_splitk_forward_rejects_bad_arguments():
+    """hg_gemm_f32_splitk validates its arguments before any device work (CPU: every call here is
+    refused, nothing is launched); hg_gemm_splitk_kslice is the slice length it checks against."""
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("libhgsim.so not built")
+    L = N.load_library()
+    assert L.hg_gemm_splitk_kslice(705, 2) == 368
+    assert L.hg_gemm_splitk_kslice(705, 4) == 192
+    assert L.hg_gemm_splitk_kslice(0, 2) < 0
+    fake = ctypes.c_void_p(0x10000)  # 16-byte aligned, never dereferenced on a refused call
+    args = dict(A=fake, lda=705, B=fake, ldb=705, bias=fake, C=fake, ldc=512, ws=fake, wsf=2 * 4096 * 512, M=4096,
+                N=512, K=705, act=1, tile=21, slices=2)
+
+    def call(**kw):
+        a = dict(args, **kw)
+        return L.hg_gemm_f32_splitk(a["A"], a["lda"], a["B"], a["ldb"], a["bias"], a["C"], a["ldc"], a["ws"], a["wsf"],
+                                    a["M"], a["N"], a["K"], a["act"], a["tile"], a["slices"], None)
+    assert call(slices=1) != 0                    # not split
+    assert call(slices=17) != 0
+    assert call(K=16, lda=16, ldb=16) != 0        # an empty slice (kslice 16: slice 1 starts at K)
+    assert call(wsf=2 * 4096 * 512 - 1) != 0      # workspace short of slices x M x N
+    assert call(ws=ctypes.c_void_p(0x10004)) != 0  # workspace not 16-byte aligned
+    assert call(tile=5) != 0                      # f32 tiles have no split-K form
+    assert call(bias=None) != 0
+    assert call(ldc=500) != 0
+    assert call(act=2) != 0

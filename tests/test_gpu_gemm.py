@@ -434,3 +434,80 @@ def test_colsum_jobs_wide_and_narrow_orders(parts, width):
         assert np.array_equal(dst.cpu().numpy(), want)
     ref = nar.double().sum(0)
     assert torch.allclose(dst_n.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+# (rows, k, n, lda pad, output pad): the rollout's first policy layer, 16-byte rows (the staged
+# float4 loads), ragged rows / k / columns (n % 4 != 0: the finishing pass's scalar path), a strided
+# input and a strided output
+SPLITK_CASES = [(4096, 705, 512, 0, 0), (4096, 512, 256, 0, 0), (777, 219, 768, 0, 0), (65, 33, 129, 0, 0), (130, 64, 96, 3, 3)]
+
+
+@pytest.mark.parametrize("rows,k,n,pad,opad", SPLITK_CASES)
+def test_gemm_splitk_forward_matches_fp64(rows, k, n, pad, opad):
+    """hg_gemm_f32_splitk (slices of k_gemm_x6 mode 4 + the fixed-order finishing launch) within the
+    stated per-element bound of the fp64 product, for every bf16-split tile and 2-4 slices; a repeat
+    is bit-identical (the workspace is refilled with NaN before every call: every slice element is
+    written before the finish reads it)."""
+    _need_gpu()
+    from humanoid import _native as N
+    L = N.lib()
+    torch.manual_seed(rows + k + n + 1)
+    dev = "cuda:0"
+    xs = torch.randn(rows, k + pad, device=dev)
+    x = xs[:, :k]
+    W = torch.randn(n, k, device=dev) / k ** 0.5
+    b = torch.randn(n, device=dev) * 0.1
+    pre = torch.addmm(b.double(), x.double(), W.double().t())
+    bound = REL * (x.double().abs() @ W.double().abs().t() + b.double().abs())
+    ran = 0
+    for tile in range(20, 29):
+        for S in (2, 3, 4):
+            if (S - 1) * L.hg_gemm_splitk_kslice(k, S) >= k:
+                continue
+            for act in (1, 0):
+                outs = []
+                for _ in range(2):
+                    ws = torch.full((S * rows * n,), float("nan"), device=dev)
+                    y = torch.full((rows, n + opad), 7.0, device=dev)
+                    rc = L.hg_gemm_f32_splitk(x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(),
+                                              y.data_ptr(), y.stride(0), ws.data_ptr(), ws.numel(), rows, n, k, act,
+                                              tile, S, _stream())
+                    assert rc == 0
+                    outs.append(y)
+                y = outs[0]
+                ref = F.elu(pre) if act else pre
+                err = (y[:, :n].double() - ref).abs()
+                assert (err <= bound).all(), f"tile {tile} S {S} act {act}: worst ratio {(err / bound).max().item():.3f}"
+                assert (y[:, n:] == 7.0).all()
+                assert torch.equal(outs[0], outs[1]), f"tile {tile} S {S} act {act}"
+                ran += 1
+    assert ran > 0
+
+
+def test_rollout_first_layer_routes_to_splitk():
+    """The rollout's 4096-row 705 -> 512 hidden layer goes through hg_gemm_f32_splitk
+    (_GEMM_FWD_SPLITK) and matches the one-pass route within the stated bound; 24576 rows keep
+    the one-pass tiles."""
+    _need_gpu()
+    from humanoid.algo.ppo import hg_mlp
+    dev = "cuda:0"
+    torch.manual_seed(7)
+    W = torch.randn(512, 705, device=dev) / 705 ** 0.5
+    b = torch.randn(512, device=dev) * 0.1
+    calls = []
+    orig = hg_mlp.gemm_forward_splitk
+
+    def spy(*a, **kw):
+        calls.append(a[0].shape[0])
+        return orig(*a, **kw)
+    hg_mlp.gemm_forward_splitk = spy
+    try:
+        for rows in (4096, 24576):
+            x = torch.randn(rows, 705, device=dev)
+            y = hg_mlp._hidden_forward(x, W, b)
+            pre = torch.addmm(b.double(), x.double(), W.double().t())
+            bound = REL * (x.double().abs() @ W.double().abs().t() + b.double().abs())
+            assert ((y.double() - F.elu(pre)).abs() <= bound).all()
+    finally:
+        hg_mlp.gemm_forward_splitk = orig
+    assert calls == ([4096] if hg_mlp.SPLITK_FWD else [])
