@@ -1428,7 +1428,8 @@ extern "C" int hg_gemm_f32_wgrad(const float* A, int64_t lda, const float* B, in
 // are the exact three-term splits of k_gemm_x6, only the split-K order of the sum differs from the
 // one-pass tiles.
 namespace {
-template <bool ELU>
+// SC > 0: the slice count at compile time (every slice's load issued before the first add); 0: S
+template <bool ELU, int SC>
 __global__ void __launch_bounds__(256) k_splitk_finish(const float* __restrict__ ws, int64_t sstride,
                                                        const float* __restrict__ bias, float* __restrict__ C,
                                                        int64_t ldc, int64_t M, int N, int S, bool vec) {
@@ -1440,10 +1441,21 @@ __global__ void __launch_bounds__(256) k_splitk_finish(const float* __restrict__
   const float* p = ws + m * N + n0;
   float v[4];
   if (vec) {  // N % 4 == 0, C rows 16-byte aligned
-    float4 a = *reinterpret_cast<const float4*>(p);
-    for (int s = 1; s < S; s++) {
-      const float4 b = *reinterpret_cast<const float4*>(p + s * sstride);
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    float4 a;
+    if (SC > 0) {
+      typedef float fin4 __attribute__((ext_vector_type(4)));
+      fin4 x[SC > 0 ? SC : 1];
+#pragma unroll
+      for (int s = 0; s < SC; s++) x[s] = __builtin_nontemporal_load(reinterpret_cast<const fin4*>(p + s * sstride));
+#pragma unroll
+      for (int s = 1; s < SC; s++) { x[0].x += x[s].x; x[0].y += x[s].y; x[0].z += x[s].z; x[0].w += x[s].w; }
+      a = make_float4(x[0].x, x[0].y, x[0].z, x[0].w);
+    } else {
+      a = *reinterpret_cast<const float4*>(p);
+      for (int s = 1; s < S; s++) {
+        const float4 b = *reinterpret_cast<const float4*>(p + s * sstride);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
     }
     const float4 bb = *reinterpret_cast<const float4*>(bias + n0);
     v[0] = a.x + bb.x; v[1] = a.y + bb.y; v[2] = a.z + bb.z; v[3] = a.w + bb.w;
@@ -1501,7 +1513,17 @@ extern "C" int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, i
   const int64_t threads = M * ((N + 3) / 4);
   const bool fvec = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)bias % 16 == 0;
   const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
-  if (elu) hipLaunchKernelGGL(k_splitk_finish<true>, grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, slices, fvec);
-  else hipLaunchKernelGGL(k_splitk_finish<false>, grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, slices, fvec);
+#define HG_FIN(E, SC) hipLaunchKernelGGL((k_splitk_finish<E, SC>), grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, \
+                                         slices, fvec)
+  if (elu) {
+    if (slices == 4) HG_FIN(true, 4);
+    else if (slices == 2) HG_FIN(true, 2);
+    else HG_FIN(true, 0);
+  } else {
+    if (slices == 4) HG_FIN(false, 4);
+    else if (slices == 2) HG_FIN(false, 2);
+    else HG_FIN(false, 0);
+  }
+#undef HG_FIN
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
