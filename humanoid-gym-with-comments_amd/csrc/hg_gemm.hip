@@ -1491,6 +1491,8 @@ extern "C" int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, i
   if (ws_floats < slices * M * (int64_t)N) return HG_ERR_ARG;
   if ((uintptr_t)A % 4 || (uintptr_t)B % 4 || (uintptr_t)C % 4 || (uintptr_t)bias % 4 || (uintptr_t)ws % 16)
     return HG_ERR_ARG;
+  const int64_t threads = M * ((N + 3) / 4);  // the finishing launch: one thread per 4 columns
+  if ((threads + 255) / 256 > 0x7fffffff) return HG_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   GemmArgs g{A, lda, B, ldb, nullptr, nullptr, 0, ws, N, nullptr, M, N, K, 0, 0};
   GemmX6Args xa{g, kslice, M * (int64_t)N, slices};
@@ -1510,7 +1512,6 @@ extern "C" int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, i
     default: rc = launch_x6<64, 256, 2, 4, 1>(md, xa, vec, elu, s); break;
   }
   if (rc != HG_OK) return rc;
-  const int64_t threads = M * ((N + 3) / 4);
   const bool fvec = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)bias % 16 == 0;
   const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
 #define HG_FIN(E, SC) hipLaunchKernelGGL((k_splitk_finish<E, SC>), grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, \
