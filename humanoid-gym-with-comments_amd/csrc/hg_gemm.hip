@@ -1208,8 +1208,13 @@ extern "C" int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, c
 
 // pitch_rows (nullable; entry <= 0: the job's own rows): the row count of the image a job writes
 // into, so several jobs fill the row bands of ONE image (job j's img = the image + its first row
-// x 32 bytes, the first row a multiple of 32): the image of the rows stacked, e.g. two layers'
-// weights that read the same input as one [n_a + n_b, K] operand
+// x 32 bytes): the image of the rows stacked, e.g. two layers' weights that read the same input as
+// one [n_a + n_b, K] operand.  Every job writes img_rows(its rows) rows (zero past them), so the
+// bands of one image must come as one chain of consecutive jobs (same pitch_rows and K, each band
+// starting where the previous one ends) whose rows sum to pitch_rows, every band but the last a
+// multiple of 256 rows: then no band's zero padding lands on the next band and the last one's ends
+// at img_rows(pitch_rows), inside the image (a 480 + 32 split would race on rows 480..511 and write
+// past the image).
 extern "C" int hg_gemm_x6_image_jobs_pitched(const float* const* P, const int64_t* ld, const int* trans,
                                              const int64_t* rows, const int64_t* K, void* const* img,
                                              const int64_t* pitch_rows, int njobs, void* stream) {
@@ -1239,6 +1244,20 @@ extern "C" int hg_gemm_x6_image_jobs_pitched(const float* const* P, const int64_
     if (blocks > (int64_t)1 << 30) return HG_ERR_ARG;
   }
   J.block0[njobs] = (int)blocks;
+  for (int j = 0; j < njobs;) {  // band chains (see above)
+    const int64_t prow = pitch_rows && pitch_rows[j] > 0 ? pitch_rows[j] : rows[j];
+    int64_t sum = rows[j];
+    int e = j + 1;
+    while (e < njobs && pitch_rows && pitch_rows[e] == prow && K[e] == K[j] && sum < prow &&
+           (uintptr_t)img[e] == (uintptr_t)img[e - 1] + (uintptr_t)(32 * rows[e - 1])) {
+      sum += rows[e];
+      e++;
+    }
+    if (sum != prow) return HG_ERR_ARG;
+    for (int b = j; b + 1 < e; b++)
+      if (rows[b] % 256) return HG_ERR_ARG;
+    j = e;
+  }
   hipLaunchKernelGGL(k_x6_image_jobs, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

@@ -356,8 +356,9 @@ def x6_images(jobs, dev):
     """Operand images of the bf16-split tiles in one launch (hg_gemm_x6_image_jobs_pitched): jobs
     [(P, trans, rows, K)] (trans 0: element (r, k) = P[r][k]; trans 1: P[k][r]) or
     [("stack", (P_1, .., P_m), K)] (the trans-0 image of the P_i's rows stacked, each band written
-    by its own job into the shared image; every band but the last a multiple of 32 rows) -> one
-    image tensor each, slices of a single allocation."""
+    by its own job into the shared image; every band but the last a multiple of 256 rows, since
+    each job zero-pads its band to a multiple of 256 — hgsim.h) -> one image tensor each, slices of
+    a single allocation."""
     if not jobs:
         return []
     L = N.lib()
@@ -376,8 +377,9 @@ def x6_images(jobs, dev):
         if j[0] == "stack":
             total, r0 = rows_of(j), 0
             for P in j[1]:
-                if r0 % 32:
-                    raise ValueError("x6_images: stacked bands must start on a multiple of 32 rows")
+                if r0 % 256:
+                    raise ValueError("x6_images: stacked bands must start on a multiple of 256 rows "
+                                     "(every band but the last a multiple of 256 rows)")
                 cj.append((P, 0, P.shape[0], j[2], im.data_ptr() + 32 * r0, total))
                 r0 += P.shape[0]
         else:

@@ -516,9 +516,12 @@ int hg_gemm_x6_image_jobs(const float* const* P, const int64_t* ld, const int* t
                           const int64_t* K, void* const* img, int njobs, void* stream);
 /* hg_gemm_x6_image_jobs writing row bands of shared images: pitch_rows[j] (> 0; <= 0 or a NULL
  * array: rows[j]) is the row count of the image job j writes into, img[j] = that image + the
- * band's first row (a multiple of 32) x 32 bytes.  Jobs over the same K fill one image of the
- * stacked rows, e.g. the first layers of two MLPs reading the same input as one [n_a + n_b, K]
- * forward operand (hg_mlp.py mlp_pair_forward).  pitch_rows >= rows. */
+ * band's first row x 32 bytes.  Jobs over the same K fill one image of the stacked rows, e.g. the
+ * first layers of two MLPs reading the same input as one [n_a + n_b, K] forward operand (hg_mlp.py
+ * mlp_pair_forward).  The bands of one image come as ONE chain of consecutive jobs (same
+ * pitch_rows and K, each band starting where the previous one ends, in order) whose rows sum to
+ * pitch_rows, every band but the last a multiple of 256 rows (each job zero-pads its band to a
+ * multiple of 256 rows); anything else returns HG_ERR_ARG before any launch. */
 int hg_gemm_x6_image_jobs_pitched(const float* const* P, const int64_t* ld, const int* trans, const int64_t* rows,
                                   const int64_t* K, void* const* img, const int64_t* pitch_rows, int njobs,
                                   void* stream);

@@ -744,3 +744,17 @@ void ref_set_threads(int n) {
 #endif
 }
 #endif
+
+/* Forward kinematics of n states without stepping: rigid[n][13][13] (position, quaternion xyzw,
+ * linear and angular velocity of every body, world frame) — the rigid_states() that ends every
+ * ref_step, exposed so tests can pin the joint conventions against an independent FK
+ * (tests/test_fk_mjcf.py, oracle/mjcf_fk.py). */
+int API(ref_rigid_states)(const hg_model* hm, int n, const real* root, const real* q, const real* qd,
+                          const real* mass0, real* rigid) {
+  Model m;
+  load_model(hm, &m);
+  for (int e = 0; e < n; e++)
+    rigid_states(&m, root + (size_t)e * 13, q + (size_t)e * ND, qd + (size_t)e * ND, mass0[e],
+                 rigid + (size_t)e * NB * 13);
+  return 0;
+}

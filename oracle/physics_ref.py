@@ -67,6 +67,21 @@ class RefSim:
                 _p(self.contact), _p(self.rigid), _p(self.nonfinite), _p(self.dropped))
 
 
+def rigid_states(model, root, q, qd, mass0=None, precision="f64"):
+    """[n, 13, 13] body states (position, quaternion xyzw, linear / angular velocity, world frame)
+    of n states, by the oracle's own forward kinematics (physics_ref.c rigid_states), no step."""
+    dt = np.float64 if precision == "f64" else np.float32
+    root = np.ascontiguousarray(np.atleast_2d(root), dt)
+    n = root.shape[0]
+    q = np.ascontiguousarray(np.broadcast_to(q, (n, 12)), dt)
+    qd = np.ascontiguousarray(np.broadcast_to(qd, (n, 12)), dt)
+    m0 = np.ascontiguousarray(np.full(n, model.mass[0] if mass0 is None else mass0), dt)
+    out = np.zeros((n, 13, 13), dt)
+    getattr(lib(), "ref_rigid_states_" + precision)(ctypes.byref(model), ctypes.c_int(n), _p(root), _p(q), _p(qd),
+                                                    _p(m0), _p(out))
+    return out
+
+
 def ground(cfg, hf, x, y):
     """(height, unit normal[..., 3]) of the terrain under world points (x, y), numpy float64: the
     plane z = 0, or the int16 heightfield triangulated along the (i, j)-(i+1, j+1) diagonal —

@@ -113,8 +113,9 @@ def compare(cand, r64, gap32, spread, fields, kp, kd, K):
         tols[name], yards[name], rnds[name] = tol, yard, rnd
         excess = np.maximum(np.abs(x - a64) - rnd, 0.0)
         ratio = np.where(yard > 0, excess / np.where(yard > 0, yard, 1.0), np.where(excess > 0, np.inf, 0.0))
-        headroom[name] = float(ratio.max())
-        bad[name] = np.abs(x - a64) > tol
+        headroom[name] = float(np.nanmax(ratio)) if np.isfinite(x).all() else float("inf")
+        # written as "not within": a NaN in the candidate compares False both ways and must count
+        bad[name] = ~(np.abs(x - a64) <= tol)
     return bad, headroom, tols
 
 
@@ -163,3 +164,64 @@ def flip_null_rate(hgcfg, model, S, a_ref, r64, spread, fields, kp, kd, K, hf=No
             if be.any():
                 res["max_err"][f] = max(res["max_err"][f], float(np.abs(cand[f][be] - base[f][be]).max()))
     return res
+
+
+# multiple of the yardstick an element may deviate by (tests/test_gpu_parity.py STEP_TOL_K: the
+# achieved maximum over every parity call is ~6, so 12 keeps a 2x margin)
+STEP_TOL_K = 12.0
+# outlier envs may deviate by at most this multiple of the largest deviation an independent CPU
+# f32 build shows in its own outlier envs (zero when those builds have none)
+OUTLIER_ERR_FACTOR = 4.0
+
+
+def check_step(hgcfg, model, S, a_ref, cand, fields=FIELDS, hf=None, K=STEP_TOL_K, members=3, candidates=4):
+    """THE verdict on one candidate K_step, shared by tests/test_gpu_parity.py::_step_parity and
+    __graft_entry__.smoke() so the driver's gate and the parity tests apply one rule.
+
+    `S` holds the pre-step state (root_states, dof_pos, dof_vel, lambda, body_mass, env_frictions),
+    `a_ref` the preprocessed actions, `cand` the candidate outputs per field.  Rule:
+      * every candidate element is finite;
+      * per element |x - f64| <= K * max(f32 ensemble gap, f64 conditioning spread) + 2^-20 (1 + |f64|);
+      * envs with an element outside: at most allowed_outliers() of the fp32 null rate measured
+        on the same state, and each field's largest deviation there within OUTLIER_ERR_FACTOR x the
+        largest such an independent f32 build shows (so: none when those builds show none).
+    Returns (r64, report, fails, bad): the f64 reference sim, a JSON-able report (achieved
+    multiples, counts), the list of failure strings (empty = pass) and the per-field bad masks."""
+    r64 = ref_sim(hgcfg, model, S, "f64", hf)
+    r64.step(a_ref)
+    gap32 = gap(f32_members(hgcfg, model, S, a_ref, fields, hf, members=members), r64, fields)
+    sp = f64_spread(hgcfg, model, S, a_ref, r64, fields, hf)
+    kp = np.array([hgcfg.kp[j] for j in range(12)])
+    kd = np.array([hgcfg.kd[j] for j in range(12)])
+    bad, headroom, _ = compare(cand, r64, gap32, sp, fields, kp, kd, K)
+    outl = bad_envs(bad)
+    base = outputs(r64)
+    report = {"ratio": headroom, "outlier_envs": int(outl.sum()), "outlier_ids": [int(i) for i in np.flatnonzero(outl)]}
+    fails = []
+    for f in fields:
+        nf = int((~np.isfinite(np.asarray(cand[f], np.float64))).sum())
+        if nf:
+            fails.append(f"{f}: {nf} non-finite elements")
+    if outl.any():
+        null = flip_null_rate(hgcfg, model, S, a_ref, r64, sp, fields, kp, kd, K, hf=hf, members=members,
+                              candidates=candidates)
+        allowed = allowed_outliers(null["bad_envs"], len(outl))
+        err = {f: float(np.abs(np.asarray(cand[f], np.float64)[outl] - base[f][outl]).max()) for f in fields}
+        report.update(null_outlier_envs=null["bad_envs"], allowed_outlier_envs=allowed, outlier_max_err=err,
+                      null_outlier_max_err=null["max_err"])
+        if outl.sum() > allowed:
+            fails.append(f"{int(outl.sum())} envs outside the element tolerance, fp32 rate allows {allowed} "
+                         f"(independent CPU f32 builds: {null['bad_envs']})")
+        for f in fields:
+            if not err[f] <= OUTLIER_ERR_FACTOR * null["max_err"][f]:
+                fails.append(f"{f}: outlier deviation {err[f]:.3e} > {OUTLIER_ERR_FACTOR:g} x the f32 builds' "
+                             f"{null['max_err'][f]:.3e}")
+        if fails:
+            for name in fields:
+                x, a64 = np.asarray(cand[name], np.float64), base[name]
+                detail = "; ".join(f"{tuple(int(i) for i in ix)} cand {x[tuple(ix)]:+.6f} f64 {a64[tuple(ix)]:+.6f} "
+                                   f"f32 gap {gap32[name][tuple(ix)]:.2e} spread {sp[name][tuple(ix)]:.2e}"
+                                   for ix in np.argwhere(bad[name])[:6])
+                if bad[name].any():
+                    fails.append(f"{name}: {bad[name].sum()} mismatches, max err {np.nanmax(np.abs(x - a64))}: {detail}")
+    return r64, report, fails, bad

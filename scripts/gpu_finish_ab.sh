@@ -5,7 +5,7 @@
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R" || exit 1
 export TMPDIR=/tmp
-BASE=${BASE_LIB:-ab/libhgsim_base.so}
+BASE=${BASE_LIB:-abpush/libhgsim_base.so}
 OUT=gpurun_out/finish_ab
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py -m gpu -x -q --timeout 300 --timeout-method thread \

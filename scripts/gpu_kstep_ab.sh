@@ -1,6 +1,6 @@
 #!/bin/bash
 # K_step same-box A/B (round 5): the -m gpu suite + smoke on the tree's library, then the launch time
-# at 256 and 4096 envs for the base build (HG_LIB, default ab/libhgsim_base.so) and the tree's, the
+# at 256 and 4096 envs for the base build (HG_LIB, default abpush/libhgsim_base.so) and the tree's, the
 # SQ counters of the tree's K_step, and a short bench.  Every GPU step has its own time limit; the
 # script stops at the first failure.
 set -o pipefail
@@ -9,7 +9,7 @@ cd "$R" || exit 1
 mkdir -p gpurun_out/kstep_ab
 export TMPDIR=/tmp
 export HG_TOL_REPORT=${HG_TOL_REPORT:-gpurun_out/tol_report.jsonl}
-BASE=${BASE_LIB:-ab/libhgsim_base.so}
+BASE=${BASE_LIB:-abpush/libhgsim_base.so}
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
     > gpurun_out/pytest_gpu.log 2>&1

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Same-box A/B of the bf16-split GEMM's staging order (round 5): the base build (BASE_LIB, default
-# ab/libhgsim_base.so) against the tree's, per shape (scripts/x6r_probe.py, with a sha256 of every
+# abpush/libhgsim_base.so) against the tree's, per shape (scripts/x6r_probe.py, with a sha256 of every
 # output, so the two builds are compared bit for bit) and on the bench, alternated twice; then the
 # GEMM GPU tests on the tree's library.  Every GPU step has its own time limit; the script stops at
 # the first failure.
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R" || exit 1
-BASE=${BASE_LIB:-ab/libhgsim_base.so}
+BASE=${BASE_LIB:-abpush/libhgsim_base.so}
 OUT=gpurun_out/x6store_ab
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_gemm.py -m gpu -x -q --timeout 120 --timeout-method thread \

@@ -3,7 +3,7 @@ the batched epilogues (every epilogue load issued up front) and the ring-pipelin
 (k_gemm_x6r, tiles 30-35).  Each process times every (shape, tile) on seeded inputs (HIP events
 over back-to-back launches) and records a sha256 of each output, so two runs compare bit for bit.
 
-  HG_LIB=ab/libhgsim_base.so python scripts/x6r_probe.py base   -> gpurun_out/x6r_base.json
+  HG_LIB=abpush/libhgsim_base.so python scripts/x6r_probe.py base   -> gpurun_out/x6r_base.json
   python scripts/x6r_probe.py new                               -> gpurun_out/x6r_new.json
   python scripts/x6r_probe.py compare                           -> table + bitwise check
 """

@@ -15,7 +15,7 @@ Recipe:
     on them are "parity unpinned" (see DESIGN.md).
 
 Usage:  python tests/golden/gen_goldens.py [name ...]   (writes tests/golden/*.npz; names: gae actor_critic
-        ppo_update ppo_update_full env math pipeline heights terrain mjcf)
+        ppo_update ppo_update_full ppo_update_config1 env math pipeline heights terrain mjcf)
 """
 import importlib.util
 import os
@@ -231,12 +231,15 @@ def gen_ppo_update(mods):
     np.savez_compressed(os.path.join(OUT, "ppo_update.npz"), **out)
 
 
-def gen_ppo_update_full(mods):
+def gen_ppo_update_full(mods, n_envs=None, name="ppo_update_full.npz", margin=1.5):
     """ppo_update_full.npz: the reference's PPO.update (ppo.py:144-226) at the production network
     dims on a 2048 x 24 rollout (12288-row minibatches), inputs from ppo_full_recipe (regenerated by
     the test, not committed).  Outputs: the three loss means, the learning rate and every final
     parameter; also the per-minibatch KL means (the adaptive rule's input; asserted to sit inside
-    one branch of the rule with a 1.5x margin, so the LR schedule is not decided by rounding)."""
+    one branch of the rule with a 1.5x margin, so the LR schedule is not decided by rounding).
+    n_envs = ppo_full_recipe.CONFIG1_ENVS -> ppo_update_config1.npz: BASELINE config 1's rollout
+    (4 envs x 24 steps, 24-row minibatches) through the same networks; its KL means (~0.0035) sit
+    1.4x inside the raise branch, so its margin is 1.25."""
     import ppo_full_recipe as R
     AC = mods["actor_critic"].ActorCritic
     PPO = mods["ppo"].PPO
@@ -246,9 +249,9 @@ def gen_ppo_update_full(mods):
     init = R.parameters(shapes)
     ac.load_state_dict({k: torch.from_numpy(v) for k, v in init.items()})
     ppo = PPO(ac, device="cpu", **R.PPO_KW)
-    ppo.init_storage(R.N_ENVS, R.T, [R.DIMS["num_actor_obs"]], [R.DIMS["num_critic_obs"]], [R.DIMS["num_actions"]])
+    ppo.init_storage(n_envs or R.N_ENVS, R.T, [R.DIMS["num_actor_obs"]], [R.DIMS["num_critic_obs"]], [R.DIMS["num_actions"]])
     st = ppo.storage
-    for k, v in R.storage(init["std"]).items():
+    for k, v in R.storage(init["std"], n_envs).items():
         getattr(st, k).copy_(torch.from_numpy(v))
     st.step = R.T
     kls = []
@@ -266,12 +269,12 @@ def gen_ppo_update_full(mods):
     finally:
         torch.mean = real_mean
     lo, hi = R.PPO_KW["desired_kl"] / 2.0, R.PPO_KW["desired_kl"] * 2.0
-    print("ppo_update_full: minibatch KL means", kls, "lr", ppo.learning_rate)
-    assert len(kls) == 8 and all(k < lo / 1.5 or lo * 1.5 < k < hi / 1.5 or k > hi * 1.5 for k in kls), kls
+    print(name, ": minibatch KL means", kls, "lr", ppo.learning_rate)
+    assert len(kls) == 8 and all(k < lo / margin or lo * margin < k < hi / margin or k > hi * margin for k in kls), kls
     out = dict(value_loss=np.float64(vloss), surrogate_loss=np.float64(sloss), lin_vel_loss=np.float64(lvloss),
                learning_rate=np.float64(ppo.learning_rate), kl_means=np.asarray(kls, np.float64))
     out.update({"final/" + k: v.detach().numpy().copy() for k, v in ac.state_dict().items()})
-    np.savez_compressed(os.path.join(OUT, "ppo_update_full.npz"), **out)
+    np.savez_compressed(os.path.join(OUT, name), **out)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -816,6 +819,9 @@ def main(only=None):
         gen_ppo_update(mods)
     if run("ppo_update_full"):
         gen_ppo_update_full(mods)
+    if run("ppo_update_config1"):
+        import ppo_full_recipe as R
+        gen_ppo_update_full(mods, n_envs=R.CONFIG1_ENVS, name="ppo_update_config1.npz", margin=1.25)
     install_stubs()
     from humanoid.envs.custom import humanoid_env as he
     if run("env"):

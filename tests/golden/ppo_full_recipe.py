@@ -9,7 +9,8 @@ Sizes: the production networks (XBotLCfgPPO: ActorCritic 705 / 219 / 12, actor [
 critic [768, 256, 128], lin-vel [128, 128]) and a 2048-env x 24-step rollout, so each of the 4
 minibatches holds 12288 rows — above the 8192-row bounds of hg_mlp's routes: every bf16-split
 forward / input-gradient tile, the weight images and the split-K weight gradients of the
-production update run.  numpy's Generator draws are platform independent and the recipe uses
+production update run.  CONFIG1_ENVS: BASELINE config 1's rollout (4 envs x 24 steps, 24-row
+minibatches; ppo_update_config1.npz), the smallest shapes every route handles.  numpy's Generator draws are platform independent and the recipe uses
 no BLAS, so the generator and the GPU box build bit-identical inputs.
 """
 import math
@@ -17,6 +18,7 @@ import math
 import numpy as np
 
 N_ENVS, T = 2048, 24
+CONFIG1_ENVS = 4
 DIMS = dict(num_actor_obs=705, num_critic_obs=219, num_actions=12, actor_hidden_dims=[512, 256, 128],
             critic_hidden_dims=[768, 256, 128], base_lin_vel_hidden_dims=[128, 128], init_noise_std=1.0)
 PPO_KW = dict(num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.994, lam=0.9, value_loss_coef=1.0,
@@ -51,11 +53,12 @@ def parameters(shapes):
     return out
 
 
-def storage(std):
+def storage(std, n_envs=None):
     """Rollout-storage contents [T, N, .] (float32) the update reads: observations, privileged
     observations (whose [53:56] columns are the lin-vel target), actions drawn around small old
     means with the policy's std, their Normal log-probabilities (+ - * / and the 12 logs of std
     only), values, returns and advantages."""
+    N_ENVS = n_envs or globals()["N_ENVS"]  # noqa: N806  (config 1's golden: 4 envs)
     rng = np.random.default_rng(20241018)
     f32 = np.float32
     obs = rng.standard_normal((T, N_ENVS, DIMS["num_actor_obs"]), dtype=f32)

@@ -105,6 +105,21 @@ def test_stacked_image_and_split_gemm_reject_bad_arguments():
     rows, K, img = (i64 * 1)(128), (i64 * 1)(705), (vp * 1)(fake)
     # pitch rows below the job's rows
     assert L.hg_gemm_x6_image_jobs_pitched(P, ld, tr, rows, K, img, (i64 * 1)(64), 1, None) != 0
+    # band chains: a 480 + 32 split would race on rows 480..511 and write past the
+    # image; a lone band smaller than its pitch leaves rows nobody writes; a gap between bands
+    base = 0x100000
+
+    def bands(rs, addr=None, pitch=None):
+        m = len(rs)
+        offs = addr or [sum(rs[:i]) for i in range(m)]
+        return L.hg_gemm_x6_image_jobs_pitched((vp * m)(*[fake] * m), (i64 * m)(*[705] * m), (ctypes.c_int * m)(*[0] * m),
+                                               (i64 * m)(*rs), (i64 * m)(*[705] * m),
+                                               (vp * m)(*[vp(base + 32 * o) for o in offs]),
+                                               (i64 * m)(*[pitch or sum(rs)] * m), m, None)
+    assert bands([480, 32]) != 0
+    assert bands([96, 32]) != 0
+    assert bands([128], pitch=640) != 0
+    assert bands([512, 128], addr=[0, 544]) != 0
     nbytes = L.hg_gemm_x6_image_bytes(640, 705)
     args = dict(A=fake, lda=705, Bimg=fake, bias=fake, bias2=fake, C=fake, ldc=512, C2=fake, ldc2=128, nsplit=512,
                 M=24576, N=640, K=705, act=1, tile=25, nbytes=nbytes)

@@ -362,6 +362,24 @@ def test_paired_first_layers_match_separate_networks():
         assert (a - b_).abs().max().item() <= 2e-5 * (b_.abs().max().item() + 1e-12) + 1e-6
 
 
+def test_stacked_image_bands_non_256_tail():
+    """A stacked image whose last band is not a multiple of 256 rows (256 + 40 over K = 219): its
+    bytes equal the image of the two weights concatenated, built as one job; a 480 + 32 split (the
+    first band's zero padding would land on the second band) is refused."""
+    _need_gpu()
+    from humanoid.algo.ppo import hg_mlp
+    torch.manual_seed(13)
+    A = torch.randn(256, 219, device="cuda:0")
+    B = torch.randn(40, 219, device="cuda:0")
+    (stacked,) = hg_mlp.x6_images([("stack", (A, B), 219)], A.device)
+    (whole,) = hg_mlp.x6_images([(torch.cat([A, B]), 0, 296, 219)], A.device)
+    torch.cuda.synchronize()
+    assert stacked.numel() == whole.numel() and torch.equal(stacked.view(torch.int32), whole.view(torch.int32))
+    with pytest.raises(ValueError):
+        hg_mlp.x6_images([("stack", (torch.randn(480, 219, device="cuda:0"), torch.randn(32, 219, device="cuda:0")),
+                           219)], A.device)
+
+
 @pytest.mark.parametrize("rows,n", [(24576, 12), (777, 3), (64, 1), (65, 12)])
 def test_skinny_backward_act_matches_fp64(rows, n):
     """hg_linear_skinny_backward_act: the output layer's dW / db partials and its input gradient

@@ -75,3 +75,40 @@ def test_allowance_is_twice_the_rate_with_a_floor():
     assert ST.allowed_outliers([0, 0, 0, 0], 64) == 2
     assert ST.allowed_outliers([0, 0, 0, 0], 4096) == 82
     assert ST.allowed_outliers([3, 0, 1, 0], 64) == 2
+
+
+def test_nan_in_a_candidate_is_caught(contact_step):
+    """A non-finite candidate element is outside every tolerance (|NaN - x| <= tol is False) and
+    check_step names it (the old `> tol` test let a NaN through)."""
+    c = contact_step
+    fields = ST.FIELDS
+    cand = {f: ST.outputs(c["r64"])[f].copy() for f in fields}
+    cand["q"][5, 2] = np.nan
+    cand["rigid"][9, 3, 4] = np.inf
+    bad, head, _ = ST.compare(cand, c["r64"], c["g32"], c["spread"], fields, c["kp"], c["kd"], 12.0)
+    assert np.flatnonzero(ST.bad_envs(bad)).tolist() == [5, 9]
+    assert head["q"] == float("inf") and head["rigid"] == float("inf")
+
+
+def test_check_step_bounds_outlier_size(contact_step):
+    """check_step (the rule smoke() and the GPU parity tests share): the f64 step itself passes; an
+    env pushed far outside (1 rad on one joint) fails by count or by the 4 x deviation bound even
+    when the count alone would be allowed; a NaN fails as non-finite."""
+    c = contact_step
+    n = 64
+    S = {k: np.asarray(v)[:n] for k, v in c["S"].items() if hasattr(v, "shape") and np.asarray(v).shape[:1] == (c["n"],)}
+    a = c["a_ref"][:n]
+    r64 = ST.ref_sim(c["hc"], c["model"], S, "f64")
+    r64.step(a)
+    exact = {f: ST.outputs(r64)[f].copy() for f in ST.FIELDS}
+    _, rep, fails, _ = ST.check_step(c["hc"], c["model"], S, a, exact)
+    assert not fails and rep["outlier_envs"] == 0
+    off = {f: v.copy() for f, v in exact.items()}
+    off["q"][3, 7] += 1.0
+    _, rep, fails, _ = ST.check_step(c["hc"], c["model"], S, a, off)
+    assert rep["outlier_envs"] >= 1 and 3 in rep["outlier_ids"] and fails
+    assert any("outlier deviation" in f or "envs outside" in f for f in fails)
+    nan = {f: v.copy() for f, v in exact.items()}
+    nan["torques"][0, 0] = np.nan
+    _, _, fails, _ = ST.check_step(c["hc"], c["model"], S, a, nan)
+    assert any("non-finite" in f for f in fails)
