@@ -61,6 +61,20 @@ typedef double real;
 #define R(x) ((double)(x))
 #endif
 
+/* REF_APPROX_QUOT (with REF_FLOAT): the fp32 variant "f32q" whose quotients are formed as the HIP
+ * kernel forms them (csrc/hg_physics.hip: v_rcp_f32 / v_rsq_f32 products instead of correctly
+ * rounded divisions in the Cholesky pivots and solves, the PGS 1 / D, the friction-disc scale, the
+ * segment-segment closest points, the pair normals and the tangent basis), each as a product with
+ * a correctly rounded reciprocal — the kernel's 1-ulp quotients in kind, not bit for bit.  Used to
+ * classify K_step outliers (scripts/classify_kstep_outlier.py): does an fp32 build with the
+ * kernel's quotient structure deviate where the plain fp32 build does not? */
+#ifdef REF_APPROX_QUOT
+#define QDIV(a, b) ((a) * (R(1) / (b)))
+#define RSQRT(x) (R(1) / sqrt(x))
+#else
+#define QDIV(a, b) ((a) / (b))
+#define RSQRT(x) (R(1) / sqrt(x))
+#endif
 #define NB 13
 #define ND 12
 #define NV 18
@@ -342,7 +356,7 @@ static int cholesky(real* A, int n, int ld) { /* in-place lower */
     for (int i = j + 1; i < n; i++) {
       real s = A[i * ld + j];
       for (int k = 0; k < j; k++) s -= A[i * ld + k] * A[j * ld + k];
-      A[i * ld + j] = s / d;
+      A[i * ld + j] = QDIV(s, d);
     }
   }
   return 0;
@@ -351,12 +365,12 @@ static void chol_solve(const real* L, int n, int ld, real* x) {
   for (int i = 0; i < n; i++) {
     real s = x[i];
     for (int k = 0; k < i; k++) s -= L[i * ld + k] * x[k];
-    x[i] = s / L[i * ld + i];
+    x[i] = QDIV(s, L[i * ld + i]);
   }
   for (int i = n - 1; i >= 0; i--) {
     real s = x[i];
     for (int k = i + 1; k < n; k++) s -= L[k * ld + i] * x[k];
-    x[i] = s / L[i * ld + i];
+    x[i] = QDIV(s, L[i * ld + i]);
   }
 }
 
@@ -391,10 +405,10 @@ static void seg_seg(const real* p1, const real* q1, const real* p2, const real* 
   const real a = v3_dot(d1, d1), e = v3_dot(d2, d2), f = v3_dot(d2, r);
   const real c = v3_dot(d1, r), b = v3_dot(d1, d2);
   const real denom = a * e - b * b;
-  real s = denom > R(1e-6) * a * e ? clamp01((b * f - c * e) / denom) : 0;
-  real t = (b * s + f) / e;
-  if (t < 0) { t = 0; s = clamp01(-c / a); }
-  else if (t > 1) { t = 1; s = clamp01((b - c) / a); }
+  real s = denom > R(1e-6) * a * e ? clamp01(QDIV(b * f - c * e, denom)) : 0;
+  real t = QDIV(b * s + f, e);
+  if (t < 0) { t = 0; s = clamp01(QDIV(-c, a)); }
+  else if (t > 1) { t = 1; s = clamp01(QDIV(b - c, a)); }
   for (int i = 0; i < 3; i++) { c1[i] = p1[i] + d1[i] * s; c2[i] = p2[i] + d2[i] * t; }
 }
 
@@ -404,8 +418,13 @@ static void tangents(const real* n, real* t1, real* t2) {
   ref[fabs(n[0]) < R(0.9) ? 0 : 1] = 1;
   const real dd = v3_dot(ref, n);
   for (int i = 0; i < 3; i++) t1[i] = ref[i] - dd * n[i];
+#ifdef REF_APPROX_QUOT
+  const real itn = RSQRT(v3_dot(t1, t1));
+  for (int i = 0; i < 3; i++) t1[i] *= itn;
+#else
   const real tn = sqrt(v3_dot(t1, t1));
   for (int i = 0; i < 3; i++) t1[i] /= tn;
+#endif
   v3_cross(n, t1, t2);
 }
 
@@ -518,7 +537,7 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
         seg_seg(a0, a1, b0, b1, pa, pb);
         for (int i = 0; i < 3; i++) dv[i] = pb[i] - pa[i];
         dist = sqrt(v3_dot(dv, dv));
-        if (dist > R(1e-9)) for (int i = 0; i < 3; i++) ct->n[i] = dv[i] / dist;
+        if (dist > R(1e-9)) for (int i = 0; i < 3; i++) ct->n[i] = QDIV(dv[i], dist);
         else { ct->n[0] = 0; ct->n[1] = -1; ct->n[2] = 0; }  /* left -> right is -y in the base frame */
       }
       ct->phi = dist - ra - rb;
@@ -605,7 +624,7 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
       Row* rn = &rows[r];
       real v = 0;
       for (int i = 0; i < NV; i++) v += rn->J[i] * nu[i];
-      real ln = rn->lam + (rn->target - v) / rn->D;
+      real ln = rn->lam + QDIV(rn->target - v, rn->D);
       if (rn->kind == 4) ln = ln < rn->lo ? rn->lo : (ln > rn->hi ? rn->hi : ln);
       else if (ln < 0) ln = 0;
       const real dl = ln - rn->lam;
@@ -616,9 +635,13 @@ static void substep(const hg_cfg* cfg, const Model* m, const int16_t* hf, real* 
         Row* r2 = &rows[r + 2];
         real v1 = 0, v2 = 0;
         for (int i = 0; i < NV; i++) { v1 += r1->J[i] * nu[i]; v2 += r2->J[i] * nu[i]; }
-        real l1 = r1->lam - v1 / r1->D, l2 = r2->lam - v2 / r2->D;
+        real l1 = r1->lam - QDIV(v1, r1->D), l2 = r2->lam - QDIV(v2, r2->D);
         const real lim = rn->mu * rn->lam, nn = sqrt(l1 * l1 + l2 * l2);
+#ifdef REF_APPROX_QUOT
+        if (nn > lim) { const real sc = lim * RSQRT(l1 * l1 + l2 * l2); l1 *= sc; l2 *= sc; }
+#else
         if (nn > lim) { const real sc = lim / nn; l1 *= sc; l2 *= sc; }
+#endif
         const real d1 = l1 - r1->lam, d2 = l2 - r2->lam;
         r1->lam = l1; r2->lam = l2;
         for (int i = 0; i < NV; i++) nu[i] += r1->Y[i] * d1 + r2->Y[i] * d2;
@@ -685,7 +708,9 @@ static void rigid_states(const Model* m, const real* root, const real* q, const 
  *   fric[n];  outputs torques[n][12] (last substep), contact[n][13][3], rigid[n][13][13],
  *   nonfinite[n], dropped[n] (+= rows / contact points over the budget, summed over the
  *   substeps).  Returns 0. */
-#ifdef REF_FLOAT
+#if defined(REF_FLOAT) && defined(REF_APPROX_QUOT)
+#define API(name) name##_f32q
+#elif defined(REF_FLOAT)
 #define API(name) name##_f32
 #else
 #define API(name) name##_f64

@@ -112,3 +112,25 @@ def test_check_step_bounds_outlier_size(contact_step):
     nan["torques"][0, 0] = np.nan
     _, _, fails, _ = ST.check_step(c["hc"], c["model"], S, a, nan)
     assert any("non-finite" in f for f in fails)
+
+
+def test_round6_smoke_outlier_is_a_cone_event():
+    """The K_step outlier of round 6's smoke() dump (tests/golden/kstep_outlier_r6.npz: the GPU's
+    pre-step state, actions and outputs; profiles/r6_smoke/classification.md): the shared rule
+    passes it with env 54 the only outlier, and in the f64 step that env's sole contact ground6
+    comes within 0.5 % of its friction cone at substep 6 (the stick / slip boundary fp32 rounding
+    decides; plain and kernel-quotient f32 builds flip it alike)."""
+    import classify_kstep_outlier as C
+    D = np.load(os.path.join(REPO, "tests", "golden", "kstep_outlier_r6.npz"), allow_pickle=False)
+    S = {k[2:]: D[k] for k in D.files if k.startswith("S_")}
+    gpu = {k[4:]: D[k] for k in D.files if k.startswith("gpu_")}
+    hc, model, _ = C.smoke_cfg(D["a_ref"].shape[0])
+    _, rep, fails, _ = ST.check_step(hc, model, S, D["a_ref"], gpu)
+    assert not fails and rep["outlier_ids"] == [54]
+    e = 54
+    S1 = {k: np.asarray(v)[e:e + 1] for k, v in S.items()}
+    _, lams, _ = C.replay(hc, model, S1, D["a_ref"][e:e + 1], "f64")
+    mu = 0.5 * (float(S["env_frictions"].reshape(-1)[e]) + float(hc.ground_friction))
+    lv = lams[6]
+    ratio = np.hypot(lv[3 * 6 + 1], lv[3 * 6 + 2]) / (mu * lv[3 * 6])
+    assert 0.995 < ratio < 1.0
