@@ -250,6 +250,30 @@ def cpu_baseline(n_envs=256, T=24, threads=None, iterations=3):
     return n_envs * T * iterations / dt, threads, dt
 
 
+def comm_report(runner, timer, world, rank_ms):
+    """The data-parallel exchange of one iteration (None at world size 1): the per-minibatch
+    flat-gradient (+ KL slot) all-reduce and the advantage-statistics all-reduce, each timed with
+    HIP events on a sampled subset of the timed region (KernelTimer, this rank), and the per-rank
+    spread of the iteration time.  In the one-graph form the gradient all-reduce runs inside the
+    replay and is not separable (null)."""
+    if world <= 1:
+        return None
+    alg = runner.alg
+    per_it = alg.num_learning_epochs * alg.num_mini_batches
+    ar, adv = timer.mean_ms("allreduce"), timer.mean_ms("allreduce_adv_stats")
+    sep = timer.count("allreduce") > 0
+    total = (per_it * ar if sep else float("nan")) + (adv if timer.count("allreduce_adv_stats") else 0.0)
+    nbytes = alg._flat_grad.numel() * alg._flat_grad.element_size() if alg._flat_grad is not None else None
+    return {"backend": dist.get_backend(), "update_graph": alg.update_graph,
+            "grad_allreduce_bytes": nbytes, "grad_allreduces_per_iteration": per_it,
+            "grad_allreduce_ms_mean": round(ar, 4) if sep else None,
+            "adv_stats_allreduce_ms_mean": round(adv, 4) if timer.count("allreduce_adv_stats") else None,
+            "allreduce_ms_per_iteration": round(total, 4) if sep else None,
+            "allreduce_samples": timer.count("allreduce"),
+            "timing": f"HIP events on this rank's current stream, 1 in {timer.every} calls of the timed region",
+            "rank_ms_per_step": rank_ms}
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -358,6 +382,9 @@ def main():
                             log_dir=None, device=device)
     timer = KernelTimer(every=int(os.environ.get("HG_TIMER_EVERY", "4")))
     env.kernel_timer = timer
+    if world > 1:  # the eager data-parallel all-reduces (gradients + KL per minibatch, advantage stats)
+        runner.alg.comm_timer = timer
+        runner.alg.storage.comm_timer = timer
     runner.learn(args.warmup, init_at_random_ep_len=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -370,9 +397,13 @@ def main():
         dist.barrier()
     elapsed = time.time() - t0
     timer.enabled = False
+    rank_ms = None
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        tmin = t.clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+        rank_ms = {"max": round(t.item() / args.steps * 1e3, 3), "min": round(tmin.item() / args.steps * 1e3, 3)}
         elapsed = t.item()
     env_steps = args.envs * args.T * args.steps * world
     value = env_steps / elapsed
@@ -418,6 +449,7 @@ def main():
                             "the other products on f32 MFMA (own kernels) or hipBLASLt f32"
                             if not c5 else "bf16 policy (config 5)")},
         "roofline": roofline,
+        "comm": comm_report(runner, timer, world, rank_ms),
         "collection_time_s": round(runner.last_iteration_stats.get("collection_time", float("nan")), 4),
         "learn_time_s": round(runner.last_iteration_stats.get("learn_time", float("nan")), 4),
     }

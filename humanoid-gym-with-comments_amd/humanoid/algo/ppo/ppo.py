@@ -121,6 +121,9 @@ class PPO:
         self._graph_warm = False
         self.update_graph = "eager"   # the update form last run: "eager" | "one" | "two" graphs
         self.capture_error = None     # why the in-graph collective fell back, if it did
+        # optional timer with start(name) / stop(name) (bench.py KernelTimer: HIP events on the
+        # current stream, sampled): brackets every eager data-parallel all-reduce as "allreduce"
+        self.comm_timer = None
         self._flat_grad = None
         if self._dp:
             with torch.no_grad():
@@ -544,7 +547,7 @@ class PPO:
                 self._flat_grad.zero_()
                 loss.backward()
                 if self._dp:
-                    dist.all_reduce(self._flat_grad)
+                    self._timed_all_reduce(self._flat_grad)
                     self._flat_grad /= self.world_size
             else:
                 self.optimizer.zero_grad()
@@ -574,8 +577,8 @@ class PPO:
     # HIP-graph update: the minibatch step is captured once as two graphs and replayed
     #   A: gather the minibatch rows (static index buffer) -> losses -> backward into the flat
     #      gradient buffer; KL mean; loss sums
-    #   (data parallel: all-reduce of the flat gradients and of the KL mean — captured in the one
-    #   update graph on RCCL, eager between the two graphs' replays on gloo)
+    #   (data parallel: all-reduce of the flat gradients and of the KL mean — eager between the two
+    #   graphs' replays by default; captured in the one update graph with HG_DP_GRAPH_COLLECTIVE=1)
     #   B: adaptive learning rate, global-norm clip, fused Adam
     # The first update() runs eagerly on a side stream (the warm-up graph capture needs); the
     # graphs are captured at the start of the second one.  Minibatch order: one randperm per
@@ -633,11 +636,11 @@ class PPO:
             tables.insert(1 if not frames else 0, (critic, self._mb_critic))
         self._mb_tables, self._mb_widths = tables, widths
         # the whole update (epochs x minibatches, each with its LR rule and Adam step) is ONE graph
-        # reading its row indices from a static permutation buffer: at world size 1, and with ranks
-        # on RCCL, whose gradient all-reduce is captured inside the graph between each backward and
-        # its step (RCCL kernels replay like any other node; the communicator exists from the
-        # eager warm-up update).  gloo cannot be captured: two graphs per minibatch with the
-        # all-reduce between their replays.
+        # reading its row indices from a static permutation buffer at world size 1.  Data parallel,
+        # the default is two graphs per minibatch with the eager gradient all-reduce between their
+        # replays (RCCL or gloo; timed by comm_timer).  On request (HG_DP_GRAPH_COLLECTIVE=1, RCCL
+        # only) the all-reduce is captured inside the one graph between each backward and its step;
+        # a rank whose capture fails pulls every rank back to the two-graph form in this process.
         self._whole = (not self._dp and self._flat_grad is None) or self._collective_in_graph()
         if self._whole:
             nmb = self.num_mini_batches
@@ -683,6 +686,16 @@ class PPO:
             self._mb_step()
         self._graphs = (ga, gb, mb, self._storage_key())
         self.update_graph = "two"
+
+    def _timed_all_reduce(self, t):
+        """The eager per-minibatch all-reduce, bracketed by comm_timer when one is attached (the
+        in-graph form of the one-graph update cannot be bracketed: its time is inside the replay)."""
+        tm = self.comm_timer
+        if tm is not None:
+            tm.start("allreduce")
+        dist.all_reduce(t)
+        if tm is not None:
+            tm.stop("allreduce")
 
     def _collective_in_graph(self):
         """Whether the per-minibatch gradient all-reduce is captured inside the one update graph.
@@ -775,7 +788,7 @@ class PPO:
                     self._idx.copy_(indices[i * mb:(i + 1) * mb])
                     ga.replay()
                     if self._dp:
-                        dist.all_reduce(self._flat_grad)  # gradients + the KL slot
+                        self._timed_all_reduce(self._flat_grad)  # gradients + the KL slot
                     gb.replay()
         num_updates = self.num_learning_epochs * nmb
         means = self._sums / num_updates

@@ -219,7 +219,12 @@ class RolloutStorage:
         """All-reduce (sum A, sum A^2) over the data-parallel group; returns the global count."""
         if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1
                                                               or os.environ.get("HG_DP_FORCE") == "1"):
+            tm = getattr(self, "comm_timer", None)
+            if tm is not None:
+                tm.start("allreduce_adv_stats")
             dist.all_reduce(self._stats)
+            if tm is not None:
+                tm.stop("allreduce_adv_stats")
             count *= dist.get_world_size()
         return count
 

@@ -1607,7 +1607,8 @@ def test_kstep_fk_matches_mjcf_at_random_poses():
     holding them (actions = q / action_scale; about 0.01 rad median drift), then every env's rigid_state against the
     independent MJCF walk (oracle/mjcf_fk.py, XBot-L.xml:394-481) at the GPU's own post-step root,
     q and qd: positions and orientations to 2e-5 (the MJCF's 6-digit quaternions + fp32), linear
-    and angular velocities to 2e-4."""
+    and angular velocities to 2e-5 x (1 + the env's largest |qd|) (the held poses that collide
+    leave the step with tens of rad/s on some joint)."""
     _need_gpu()
     import ctypes as C
     import mjcf_fk as MF
@@ -1631,16 +1632,18 @@ def test_kstep_fk_matches_mjcf_at_random_poses():
     # limit rows act within the step): the FK is compared at the GPU's own post-step state anyway
     assert np.median(np.abs(qq - g(q))) < 0.05
     bodies = MF.load()
-    worst = dict(pos=0.0, rot=0.0, vel=0.0, ang=0.0)
+    worst = dict(pos=0.0, rot=0.0, vel=0.0, ang=0.0, max_qd=0.0)
     for e in range(n):
         o, R, v, w = MF.fk_array(bodies, root[e], qq[e], qqd[e])
+        sc = 1.0 + np.abs(qqd[e]).max()  # velocities: relative to the env's fastest joint
         worst["pos"] = max(worst["pos"], np.abs(rs[e, :, 0:3] - o).max())
         worst["rot"] = max(worst["rot"], np.abs(MF.quat_xyzw_to_mat(rs[e, :, 3:7]) - R).max())
-        worst["vel"] = max(worst["vel"], np.abs(rs[e, :, 7:10] - v).max())
-        worst["ang"] = max(worst["ang"], np.abs(rs[e, :, 10:13] - w).max())
+        worst["vel"] = max(worst["vel"], np.abs(rs[e, :, 7:10] - v).max() / sc)
+        worst["ang"] = max(worst["ang"], np.abs(rs[e, :, 10:13] - w).max() / sc)
+        worst["max_qd"] = max(worst["max_qd"], sc - 1.0)
     print("K_step rigid_state vs MJCF FK, worst over 256 envs x 13 bodies:", worst)
     assert worst["pos"] < 2e-5 and worst["rot"] < 2e-5, worst
-    assert worst["vel"] < 2e-4 and worst["ang"] < 2e-4, worst
+    assert worst["vel"] < 2e-5 and worst["ang"] < 2e-5, worst
 
 
 def test_config1_workload_through_the_product():
