@@ -595,7 +595,7 @@ struct X6Op {
 // in two register sets, so the activations' HBM latency has two chunks of MFMAs to hide behind
 // (the B image comes from L2 by LDS-DMA one chunk ahead as before); same products, same bits
 template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, int IMG = 0, bool APF = false>
-__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
+__device__ __forceinline__ void gemm_x6_body(const GemmX6Args& xa) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int TM = BM / WGM / 32, TN = BN / WGN / 32;
   constexpr int PA = BM * 2 * KG, PB = BN * 2 * KG;  // 16-byte slots per plane
@@ -815,6 +815,22 @@ __global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
   }
 }
 
+template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, int IMG = 0, bool APF = false>
+__global__ void __launch_bounds__(64 * WGM * WGN) k_gemm_x6(GemmX6Args xa) {
+  gemm_x6_body<BM, BN, WGM, WGN, KG, VEC, MODE, ELU, IMG, APF>(xa);
+}
+
+// The same kernel compiled for OCC waves per SIMD (amdgpu_waves_per_eu: the register allocation
+// held to 512 / OCC): a 256 x 128 tile on 8 waves uses 138 registers as k_gemm_x6, i.e. one block
+// per CU, so a 480-block grid runs 1.875 dispatch rounds; at <= 128 registers (OCC 4) two blocks
+// share a CU (LDS 2 x 72 KB) and the grid is one round
+template <int BM, int BN, int WGM, int WGN, int KG, bool VEC, int MODE, bool ELU, int IMG = 0, bool APF = false,
+          int OCC = 4>
+__global__ void __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(OCC)))
+k_gemm_x6_occ(GemmX6Args xa) {
+  gemm_x6_body<BM, BN, WGM, WGN, KG, VEC, MODE, ELU, IMG, APF>(xa);
+}
+
 // Operand images of the bf16-split kernels, a list of operands in one launch.  An operand X with
 // R rows (the product's M or N side) and reduction length K: element (r, k) = P[r ld + k]
 // (trans 0: k-contiguous rows — W of the forward, activations, gradients as the A side) or
@@ -869,7 +885,7 @@ __global__ void __launch_bounds__(256) k_x6_image_jobs(ImageJobs J) {
   base[2 * pitch] = x2;
 }
 
-template <int BM, int BN, int WGM, int WGN, int KG, bool APF = false>
+template <int BM, int BN, int WGM, int WGN, int KG, bool APF = false, int OCC = 0>
 int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
   GemmArgs& g = xa.g;
   g.tiles_n = (g.N + BN - 1) / BN;
@@ -878,7 +894,11 @@ int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStrea
   if (mode != 2) xa.slices = 1;
   if (g.tiles * xa.slices > 0x7fffffff) return HG_ERR_ARG;
   const dim3 grid((unsigned)(g.tiles * xa.slices)), block(64 * WGM * WGN);
-#define HG_X6I(V, MD, E, I) hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, I, APF>), grid, block, 0, s, xa)
+#define HG_X6I(V, MD, E, I)                                                                                      \
+  do {                                                                                                             \
+    if constexpr (OCC > 0) hipLaunchKernelGGL((k_gemm_x6_occ<BM, BN, WGM, WGN, KG, V, MD, E, I, APF, OCC>), grid, block, 0, s, xa); \
+    else hipLaunchKernelGGL((k_gemm_x6<BM, BN, WGM, WGN, KG, V, MD, E, I, APF>), grid, block, 0, s, xa);             \
+  } while (0)
   if (mode == 2) {
     HG_X6I(false, 2, false, 3);
   } else if (img == 3) {
@@ -918,6 +938,11 @@ int x6_img_dispatch(int tile, int mode, int img, GemmX6Args xa, bool vec, bool e
     // 29: tile 23 with A two chunks ahead (APF; B-image form only).  The same variant of tiles 20,
     // 21, 22 and 28 measured slower on every routed shape (profiles/r4_gemm/x6_apf_probe.jsonl)
     case 29: return launch_x6_img<64, 64, 2, 2, 1, true>(mode, img, xa, vec, elu, s);
+    // 30: tile 25 at two blocks per CU; 31: tile 22 at four (k_gemm_x6_occ, 4 waves per SIMD)
+    case 30: return launch_x6_img<256, 128, 4, 2, 1, false, 4>(mode, img, xa, vec, elu, s);
+    case 31: return launch_x6_img<128, 64, 2, 2, 1, false, 4>(mode, img, xa, vec, elu, s);
+    // 32: tile 21 (128 x 128 on 8 waves, 90 registers: two blocks per CU) at three (6 waves per SIMD)
+    case 32: return launch_x6_img<128, 128, 2, 4, 1, false, 6>(mode, img, xa, vec, elu, s);
     default: return launch_x6_img<64, 128, 2, 2, 1>(mode, img, xa, vec, elu, s);  // 19
   }
 }
@@ -958,11 +983,12 @@ int launch_x6(int mode, GemmX6Args xa, bool vec, bool elu, hipStream_t s) {
 }
 
 constexpr int NTILES = 29;  // 29: tile 23 with A two chunks ahead (image entry)
+constexpr int NTILES_IMG = 32;  // the image entries also take 30 / 31 / 32: tiles 25 / 22 / 21 at more waves per SIMD
 // block rows of a tile id (the column-partial row count of mode 1)
 int tile_bm(int tile) {
-  if (tile == 25) return 256;
+  if (tile == 25 || tile == 30) return 256;
   return (tile <= 2 || (tile >= 8 && tile <= 10) || tile == 12 || tile == 13 || tile == 16 || tile == 17 ||
-          (tile >= 20 && tile <= 22) || tile == 24 || tile == 26 || tile == 27)
+          (tile >= 20 && tile <= 22) || tile == 24 || tile == 26 || tile == 27 || tile == 31 || tile == 32)
              ? 128
              : 64;
 }
@@ -1267,7 +1293,7 @@ extern "C" int hg_gemm_f32_img(int mode, const float* A, int64_t lda, const void
                                int64_t M, int N, int K, int act, int tile, int64_t aimg_bytes, int64_t bimg_bytes,
                                void* stream) {
   if ((!A && !Aimg) || !Bimg || !C || M <= 0 || N <= 0 || K <= 0 || ldc < N || (mode != 0 && mode != 1) || act < 0 ||
-      act > 1 || tile < 19 || tile > NTILES)
+      act > 1 || tile < 19 || tile > NTILES_IMG)
     return HG_ERR_ARG;
   if (!Aimg && lda < K) return HG_ERR_ARG;
   // the images must be the ones hg_gemm_x6_image_jobs builds for this product's shape
@@ -1288,7 +1314,7 @@ extern "C" int hg_gemm_f32_img_split(const float* A, int64_t lda, const void* Bi
                                      const float* bias2, float* C, int64_t ldc, float* C2, int64_t ldc2, int nsplit,
                                      int64_t M, int N, int K, int act, int tile, int64_t bimg_bytes, void* stream) {
   if (!A || !Bimg || !C || !C2 || !bias != !bias2 || M <= 0 || N <= 0 || K <= 0 || nsplit <= 0 || nsplit >= N || nsplit % 256 ||
-      ldc < nsplit || ldc2 < N - nsplit || lda < K || act < 0 || act > 1 || tile < 19 || tile > NTILES)
+      ldc < nsplit || ldc2 < N - nsplit || lda < K || act < 0 || act > 1 || tile < 19 || tile > NTILES_IMG)
     return HG_ERR_ARG;
   if (bimg_bytes != hg_gemm_x6_image_bytes(N, K)) return HG_ERR_ARG;
   if ((uintptr_t)A % 4 || (uintptr_t)Bimg % 16 || (uintptr_t)C % 4 || (uintptr_t)C2 % 4) return HG_ERR_ARG;
@@ -1326,7 +1352,7 @@ extern "C" int hg_gemm_tile(int mode, int64_t M, int N, int K) {
 }
 
 extern "C" int64_t hg_gemm_colpart_rows(int64_t M, int tile) {
-  if (tile < 1 || tile > NTILES) return -1;
+  if (tile < 1 || tile > NTILES_IMG) return -1;
   const int bm = tile_bm(tile);
   return (M + bm - 1) / bm;
 }
@@ -1334,6 +1360,11 @@ extern "C" int64_t hg_gemm_colpart_rows(int64_t M, int tile) {
 extern "C" int hg_gemm_f32(int mode, const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
                            const float* Y, int64_t ldY, float* C, int64_t ldc, float* colpart, int64_t M, int N, int K,
                            int act, int tile, void* stream) {
+  // the occupancy tiles of the image entries run here (no image) as their base blocking: the same
+  // products in the same order, so the same bits
+  if (tile == 30) tile = 25;
+  else if (tile == 31) tile = 22;
+  else if (tile == 32) tile = 21;
   if (!A || !B || !C || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || mode < 0 || mode > 3 || mode == 2 ||
       act < 0 || act > 1 || tile < 1 || tile > NTILES)
     return HG_ERR_ARG;

@@ -264,7 +264,7 @@ _BIG = 1 << 40
 X6_TILE0 = 19  # tiles >= 19: the bf16-split (6-term) kernels of hg_gemm_f32
 _GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG, 22)],
              (256, 128): [(8192, 0), (32768, 5), (_BIG, 20)], (705, 128): [(8192, 5), (_BIG, 29)],
-             (128, 128): [(8192, 0), (_BIG, 5)], (219, 768): [(32768, 21), (_BIG, 20)],
+             (128, 128): [(8192, 0), (_BIG, 5)], (219, 768): [(8192, 21), (_BIG, 32)],
              (768, 256): [(32768, 22), (_BIG, 20)]}
 # input gradients (24576 rows, torch mm + ELU-backward pass -> fused; gemm_probe_x6.jsonl): 256->512
 # 84.7 -> 72.9 (bf16-split tile 22), 256->768 118 -> 103 (f32 tile 16), 128->256 33 -> 24.8 (16),
@@ -279,7 +279,16 @@ _GEMM_FWD = {(705, 512): [(8192, 5), (_BIG, 20)], (512, 256): [(8192, 5), (_BIG,
 # (scripts/x6_apf_probe.py, profiles/r4_gemm/x6_apf_probe.jsonl)
 if os.environ.get("HG_X6_APF", "1") == "0":
     _GEMM_FWD[(705, 128)] = [(8192, 5), (_BIG, 23)]
-_GEMM_DX = {(256, 512): [(_BIG, 28)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 22)], (128, 128): [(_BIG, 5)]}
+# Round 6: tiles 30 / 31 / 32 are tiles 25 / 22 / 21 compiled for more waves per SIMD
+# (k_gemm_x6_occ: registers held to 128 / 128 / 85, so 2 / 4 / 3 blocks share a CU; the same
+# products in the same order, bit-identical; scripts/probes/occ_probe.py,
+# profiles/r6_gemm/occ_sweep.json): at 24576 rows the paired 705 -> 640 forward 139 -> 126 us (the
+# 480-block grid in one dispatch round instead of 1.875), the critic's 219 -> 768 forward 70.5 ->
+# 64, its 256 -> 768 input gradient 82 -> 80; the critic's 98304-row value pass 219 -> 768 259 ->
+# 243.  The same sweep moved the actor's 256 -> 512 input gradient from tile 28 (55.1 us) to 22
+# (53.9).  Same-box bench A/B (HG_OCC_TILES=0, three alternations): 5.469-5.485 -> 5.495-5.503 M
+# env-steps/s.
+_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 31)], (128, 128): [(_BIG, 5)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
 # The bf16-split tiles read B (the weight) from an image split once per MLP call
 # (hg_gemm_x6_image_jobs: every routed layer's forward and input-grad image in ONE launch) and
@@ -652,7 +661,12 @@ class _MLP(torch.autograd.Function):
 # (hg_gemm_f32_img_split), so the rest of each network and its backward run exactly as apart.
 # (K, n_a + n_b) -> [(max rows, tile)]: 705 -> 640 at 24576 rows on tile 25, 143 us against 128 + 40
 # for the two products apart (scripts/gemm_tile_sweep.py, profiles/r5_gemm/gemm_tile_sweep.json).
-_PAIR_FWD = {(705, 640): [(8192, 0), (_BIG, 25)]}
+_PAIR_FWD = {(705, 640): [(8192, 0), (_BIG, 30)]}
+if os.environ.get("HG_OCC_TILES", "1") == "0":  # A/B: the round-5 tiles
+    _PAIR_FWD[(705, 640)] = [(8192, 0), (_BIG, 25)]
+    _GEMM_DX[(256, 768)] = [(_BIG, 22)]
+    _GEMM_DX[(256, 512)] = [(_BIG, 28)]
+    _GEMM_FWD[(219, 768)] = [(32768, 21), (_BIG, 20)]
 PAIR_FIRST = os.environ.get("HG_PAIR_FIRST", "1") != "0"
 
 
