@@ -49,6 +49,48 @@ def _axis_angle(axis, th):
     return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * (K @ K)
 
 
+def collapse(bodies):
+    """MJCF tree -> {jointed body: dict(mass, com (body frame), I (3x3 about the COM, body frame),
+    T (4x4 in the parent jointed body's frame), parent, joint)}, merging every joint-less MJCF body
+    into its nearest jointed ancestor (Isaac Gym's collapse_fixed_joints, humanoid_config.py:93)."""
+    by = {b["name"]: b for b in bodies}
+    T_world = {}
+    for b in bodies:  # bodies are listed parents first
+        T = np.eye(4)
+        T[:3, :3] = _qmat_wxyz(b["quat"])
+        T[:3, 3] = b["pos"]
+        T_world[b["name"]] = T if b["parent"] is None else T_world[b["parent"]] @ T
+
+    def owner(name):
+        while not by[name]["joints"]:
+            name = by[name]["parent"]
+        return name
+    out = {}
+    for b in bodies:
+        if b["joints"]:
+            par = owner(b["parent"]) if b["parent"] else None
+            Tp = np.linalg.inv(T_world[par]) @ T_world[b["name"]] if par else np.eye(4)
+            out[b["name"]] = dict(parent=par, T=Tp, joint=b["joints"][0], items=[])
+    for b in bodies:
+        inn = b.get("inertial")
+        if inn is None:
+            continue
+        o = owner(b["name"])
+        T = np.linalg.inv(T_world[o]) @ T_world[b["name"]]
+        R = T[:3, :3] @ _qmat_wxyz(inn["quat"])
+        c = T[:3, :3] @ np.asarray(inn["pos"]) + T[:3, 3]
+        out[o]["items"].append((inn["mass"], c, R @ np.diag(inn["diaginertia"]) @ R.T))
+    for rec in out.values():
+        m = sum(i[0] for i in rec["items"])
+        com = sum(i[0] * i[1] for i in rec["items"]) / m
+        I = np.zeros((3, 3))
+        for mi, ci, Ii in rec["items"]:
+            d = ci - com
+            I += Ii + mi * (d @ d * np.eye(3) - np.outer(d, d))
+        rec.update(mass=m, com=com, I=I)
+    return out
+
+
 def load(path=MJCF_JSON):
     with open(path) as f:
         return json.load(f)["bodies"]

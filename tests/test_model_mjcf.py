@@ -27,52 +27,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODEL = os.path.join(REPO, "humanoid-gym-with-comments_amd", "model", "xbotl_model.json")
 
 
-def _qmat(q):  # MuJoCo quaternion (w, x, y, z)
-    w, x, y, z = np.asarray(q, float) / np.linalg.norm(q)
-    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
-                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
-                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
-
-
 def _collapse(bodies):
-    """MJCF tree -> {jointed body: dict(mass, com, I (about COM, body frame), T_parent (4x4 in the
-    parent jointed body's frame), parent, joint)}, merging joint-less bodies into their ancestor."""
-    by = {b["name"]: b for b in bodies}
-    T_world = {}
-    for b in bodies:  # bodies are listed parents first
-        T = np.eye(4)
-        T[:3, :3] = _qmat(b["quat"])
-        T[:3, 3] = b["pos"]
-        T_world[b["name"]] = T if b["parent"] is None else T_world[b["parent"]] @ T
-
-    def owner(name):
-        while not by[name]["joints"]:
-            name = by[name]["parent"]
-        return name
-    out = {}
-    for b in bodies:
-        if b["joints"]:
-            par = owner(b["parent"]) if b["parent"] else None
-            Tp = np.linalg.inv(T_world[par]) @ T_world[b["name"]] if par else np.eye(4)
-            out[b["name"]] = dict(parent=par, T=Tp, joint=b["joints"][0], items=[])
-    for b in bodies:
-        inn = b.get("inertial")
-        if inn is None:
-            continue
-        o = owner(b["name"])
-        T = np.linalg.inv(T_world[o]) @ T_world[b["name"]]
-        R = T[:3, :3] @ _qmat(inn["quat"])
-        c = T[:3, :3] @ np.asarray(inn["pos"]) + T[:3, 3]
-        out[o]["items"].append((inn["mass"], c, R @ np.diag(inn["diaginertia"]) @ R.T))
-    for rec in out.values():
-        m = sum(i[0] for i in rec["items"])
-        com = sum(i[0] * i[1] for i in rec["items"]) / m
-        I = np.zeros((3, 3))
-        for mi, ci, Ii in rec["items"]:
-            d = ci - com
-            I += Ii + mi * (d @ d * np.eye(3) - np.outer(d, d))
-        rec.update(mass=m, com=com, I=I)
-    return out
+    """The MJCF tree collapsed to its jointed bodies (oracle/mjcf_fk.py collapse)."""
+    import mjcf_fk
+    return mjcf_fk.collapse(bodies)
 
 
 @pytest.fixture(scope="module")
