@@ -287,8 +287,9 @@ if os.environ.get("HG_X6_APF", "1") == "0":
 # 64, its 256 -> 768 input gradient 82 -> 80; the critic's 98304-row value pass 219 -> 768 259 ->
 # 243.  The same sweep moved the actor's 256 -> 512 input gradient from tile 28 (55.1 us) to 22
 # (53.9).  Same-box bench A/B (HG_OCC_TILES=0, three alternations): 5.469-5.485 -> 5.495-5.503 M
-# env-steps/s.
-_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 16)], (256, 768): [(_BIG, 31)], (128, 128): [(_BIG, 5)]}
+# env-steps/s.  The 128 -> 256 input gradients (actor and critic, 24576 rows) moved from the f32 tile
+# 16 (24.0 us) to tile 31 (20.2 us, profiles/r6_gemm/occ_sweep2.json).
+_GEMM_DX = {(256, 512): [(_BIG, 22)], (128, 256): [(_BIG, 31)], (256, 768): [(_BIG, 31)], (128, 128): [(_BIG, 5)]}
 GEMM = os.environ.get("HG_GEMM", "1") != "0"
 # The bf16-split tiles read B (the weight) from an image split once per MLP call
 # (hg_gemm_x6_image_jobs: every routed layer's forward and input-grad image in ONE launch) and
@@ -666,6 +667,7 @@ if os.environ.get("HG_OCC_TILES", "1") == "0":  # A/B: the round-5 tiles
     _PAIR_FWD[(705, 640)] = [(8192, 0), (_BIG, 25)]
     _GEMM_DX[(256, 768)] = [(_BIG, 22)]
     _GEMM_DX[(256, 512)] = [(_BIG, 28)]
+    _GEMM_DX[(128, 256)] = [(_BIG, 16)]
     _GEMM_FWD[(219, 768)] = [(32768, 21), (_BIG, 20)]
 PAIR_FIRST = os.environ.get("HG_PAIR_FIRST", "1") != "0"
 

@@ -6,7 +6,8 @@ events, 200 calls after 20 warm-up, three interleaved rounds).
 
 Cases (name: kind rows k n [tiles]):
   pair    the paired 705 -> 640 forward (hg_gemm_f32_img_split, bias + ELU)
-  fwd     a hidden-layer forward k -> n (hg_gemm_f32_img mode 0, bias + ELU, B image)
+  fwd     a hidden-layer forward k -> n (hg_gemm_f32_img mode 0, bias + ELU, B image; tiles < 19:
+          hg_gemm_f32's f32-MFMA tiles, compared bitwise among themselves)
   dx      an input gradient gh [rows, k] x W [k, n] with the ELU backward and bias partials
           (hg_gemm_f32_img mode 1, W^T image)
 
@@ -68,6 +69,10 @@ def build(case, L, hg_mlp, dev, s):
             out = torch.empty(rows, n, device=dev)
 
             def f(t=t, out=out):
+                if t < 19:  # the f32-MFMA tiles (no image)
+                    assert L.hg_gemm_f32(0, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(), None, 0,
+                                         out.data_ptr(), out.stride(0), None, rows, n, k, 1, t, s) == 0
+                    return
                 assert L.hg_gemm_f32_img(0, x.data_ptr(), x.stride(0), None, img.data_ptr(), b.data_ptr(), None, 0,
                                          out.data_ptr(), out.stride(0), None, rows, n, k, 1, t, 0,
                                          img.numel() * img.element_size(), s) == 0
@@ -82,6 +87,11 @@ def build(case, L, hg_mlp, dev, s):
             cp = torch.empty(int(L.hg_gemm_colpart_rows(rows, t)), n, device=dev)
 
             def f(t=t, out=out, cp=cp):
+                if t < 19:
+                    assert L.hg_gemm_f32(1, gh.data_ptr(), gh.stride(0), W.data_ptr(), W.stride(0), None,
+                                         y_prev.data_ptr(), y_prev.stride(0), out.data_ptr(), out.stride(0),
+                                         cp.data_ptr(), rows, n, k, 1, t, s) == 0
+                    return
                 assert L.hg_gemm_f32_img(1, gh.data_ptr(), gh.stride(0), None, img.data_ptr(), None, y_prev.data_ptr(),
                                          y_prev.stride(0), out.data_ptr(), out.stride(0), cp.data_ptr(), rows, n, k, 1,
                                          t, 0, img.numel() * img.element_size(), s) == 0
@@ -90,7 +100,10 @@ def build(case, L, hg_mlp, dev, s):
         calls[t]()
     torch.cuda.synchronize()
     t0 = tiles[0]
-    same = all(all(torch.equal(a, b) for a, b in zip(outs[t0], outs[t])) for t in tiles)
+    # f32-MFMA and bf16-split tiles differ in rounding: compare within each family only
+    fam = lambda t: t >= 19  # noqa: E731
+    same = all(all(torch.equal(a, b) for a, b in zip(outs[next(u for u in tiles if fam(u) == fam(t))], outs[t]))
+               for t in tiles)
     return calls, same
 
 
