@@ -34,7 +34,7 @@ struct Layout {
   size_t off[HG_T_COUNT + 8];
   size_t bytes;
   // extra regions
-  size_t obs_buf, priv_buf, frame_obs, frame_priv, cfg, model, obs_noise, noise_counter;
+  size_t obs_buf, priv_buf, frame_obs, frame_priv, cfg, model, obs_noise, noise_counter, env_rows, env_order;
 };
 
 enum { X_OBS0 = HG_T_COUNT, X_OBS1, X_PRIV0, X_PRIV1, X_FOBS, X_FPRIV, X_CFG, X_MODEL };
@@ -100,6 +100,8 @@ Layout make_layout(const hg_cfg* c) {
   L.model = o; o += align256(sizeof(hg_model));
   L.obs_noise = o; o += align256((size_t)48 * np * 4);
   L.noise_counter = o; o += align256(sizeof(uint64_t));
+  L.env_rows = o; o += align256((size_t)np * 4);
+  L.env_order = o; o += align256((size_t)np * 4);
   L.off[HG_T_OBS_BUF] = L.obs_buf;
   L.off[HG_T_PRIV_BUF] = L.priv_buf;
   L.bytes = o;
@@ -142,6 +144,7 @@ __global__ void k_init(HgState S) {
   S.friction[e] = 1.0f;
   S.proj_gravity[2 * np + e] = -1.0f;
   S.reset_buf[e] = 1;
+  S.env_order[e] = e;  // identity until the first step has counted rows
 }
 
 }  // namespace
@@ -245,6 +248,13 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   S.model = (const hg_model*)(s->arena + s->L.model);
   S.obs_noise = (float*)(s->arena + s->L.obs_noise);
   S.noise_counter = (uint64_t*)(s->arena + s->L.noise_counter);
+  S.env_rows = (int32_t*)(s->arena + s->L.env_rows);
+  S.env_order = (int32_t*)(s->arena + s->L.env_order);
+  {
+    // K_step's wave balancing (hg_physics.hip k_env_order): on unless HG_WAVE_BALANCE=0
+    const char* wb = getenv("HG_WAVE_BALANCE");
+    S.balance = (wb && wb[0] == '0') ? 0 : 1;
+  }
   // zero the arena, upload cfg/model, initial state (synchronous: creation is not on the hot path)
   if (hipMemset(arena, 0, s->L.bytes) != hipSuccess ||
       hipMemcpy((void*)S.cfg, &s->cfg, sizeof(hg_cfg), hipMemcpyHostToDevice) != hipSuccess ||

@@ -58,6 +58,10 @@ struct HgState {
   float* obs_noise;       // [np][48] N(0,1) observation noise of the next post launch (K_step epilogue;
                           // per-env rows, so each wave writes whole cache lines)
   uint64_t* noise_counter;// [1] the post counter obs_noise was drawn for (~0: none)
+  int32_t* env_rows;      // [np] constraint rows of each env's last substep (K_step), the cost the next
+                          // step's wave balancing sorts by
+  int32_t* env_order;     // [np] K_step's env order: within each XCD's env range, heaviest first
+  int balance;            // 1: K_step maps block -> env pair through env_order (hg_create: HG_WAVE_BALANCE)
   const hg_cfg* cfg;      // device copy
   const hg_model* model;  // device copy
 };

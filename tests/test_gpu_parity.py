@@ -1677,3 +1677,24 @@ def test_config1_workload_through_the_product():
     assert torch.isfinite(env.obs_buf).all() and torch.isfinite(env.privileged_obs_buf).all()
     for p in runner.alg.actor_critic.parameters():
         assert torch.isfinite(p).all()
+
+
+def test_wave_balancing_does_not_change_results(monkeypatch):
+    """K_step's wave balancing (HG_WAVE_BALANCE, on by default: each XCD's envs re-paired by the
+    previous step's constraint rows, heaviest wave and lightest on one SIMD) only changes which
+    env shares a wave: 30 policy steps of 512 envs (spawn, touchdown, contact) with and without it
+    give every physics field and the rewards bit for bit."""
+    _need_gpu()
+    from humanoid import _native as N
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("HG_WAVE_BALANCE", flag)
+        env = _make_env(512)
+        gen = torch.Generator(device="cuda:0").manual_seed(21)
+        for _ in range(30):
+            env.step(torch.randn(env.num_envs, 12, device="cuda:0", generator=gen) * 0.4)
+        torch.cuda.synchronize()
+        outs.append({k: getattr(env, k).detach().cpu().numpy().copy() for k in
+                     ("root_states", "dof_pos", "dof_vel", "torques", "contact_forces", "rigid_state", "rew_buf")})
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
