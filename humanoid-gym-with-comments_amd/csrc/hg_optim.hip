@@ -312,35 +312,30 @@ __global__ void __launch_bounds__(LOSS_TPB) k_ppo_loss_rows(hg_ppo_batch Bt, int
   }
 }
 
-__global__ void __launch_bounds__(256) k_ppo_loss_final(const double* __restrict__ partial, int nb, int64_t rows,
-                                                       int A, const float* __restrict__ std, float c_v, float c_e,
-                                                       float c_l, float* __restrict__ loss_out,
-                                                       float* __restrict__ stats, int accum,
-                                                       float* __restrict__ g_std) {
-  // thread t sums blocks t, t+256, ... of every column (independent loads in flight), then a
-  // fixed-order wave and cross-wave reduction: deterministic
-  __shared__ double ws[4][4 + LOSS_MAX_A];
+constexpr int FIN_WAVES = 16;
+__global__ void __launch_bounds__(64 * FIN_WAVES) k_ppo_loss_final(const double* __restrict__ partial, int nb,
+                                                                  int64_t rows, int A, const float* __restrict__ std,
+                                                                  float c_v, float c_e, float c_l,
+                                                                  float* __restrict__ loss_out,
+                                                                  float* __restrict__ stats, int accum,
+                                                                  float* __restrict__ g_std) {
+  // one wave per column (columns w, w + 16, ..): lane l sums blocks l, l + 64, .. in order (all
+  // its loads in flight at once), then one fixed-order wave reduction — deterministic, and the
+  // column chains run side by side instead of one after another in a single block's threads
   __shared__ double col[4 + LOSS_MAX_A];
+  __shared__ double ent_a[LOSS_MAX_A];
   const int K = 4 + A;
-  double acc[4 + LOSS_MAX_A];
-#pragma unroll
-  for (int k = 0; k < 4 + LOSS_MAX_A; k++) acc[k] = 0.0;
-  for (int b = threadIdx.x; b < nb; b += 256) {
-    const double* row = partial + (int64_t)b * K;
-#pragma unroll
-    for (int k = 0; k < 4 + LOSS_MAX_A; k++)
-      if (k < K) acc[k] += row[k];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // the entropy's per-action terms by the last wave's lanes (fp64 log, in parallel; summed in
+  // action order below)
+  if (wv == FIN_WAVES - 1 && lane < A) ent_a[lane] = 0.5 + (double)LOG_SQRT_2PI + log((double)std[lane]);
+  for (int k = wv; k < K; k += FIN_WAVES) {
+    double x = 0.0;
+#pragma unroll 8
+    for (int b = lane; b < nb; b += 64) x += partial[(int64_t)b * K + k];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) col[k] = x;
   }
-#pragma unroll
-  for (int k = 0; k < 4 + LOSS_MAX_A; k++) {
-    if (k < K) {  // uniform over the block
-      double x = acc[k];
-      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-      if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6][k] = x;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < K) col[threadIdx.x] = (ws[0][threadIdx.x] + ws[1][threadIdx.x]) + (ws[2][threadIdx.x] + ws[3][threadIdx.x]);
   __syncthreads();
   if (threadIdx.x < A) {
     const float s = std[threadIdx.x];
@@ -350,7 +345,7 @@ __global__ void __launch_bounds__(256) k_ppo_loss_final(const double* __restrict
   if (threadIdx.x == 0) {
     const double n = (double)rows;
     double ent = 0.0;
-    for (int a = 0; a < A; a++) ent += 0.5 + (double)LOG_SQRT_2PI + log((double)std[a]);
+    for (int a = 0; a < A; a++) ent += ent_a[a];
     const double surr = col[0] / n, vl = col[1] / n, lv = col[2] / (3.0 * n), kl = col[3] / n;
     loss_out[0] = (float)(surr + (double)c_v * vl - (double)c_e * ent + (double)c_l * lv);
     stats[0] = accum ? stats[0] + (float)vl : (float)vl;
@@ -398,7 +393,7 @@ extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float cli
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_ppo_loss_rows, dim3(nb), dim3(LOSS_TPB), 0, s, *B, rows, A, clip_lo, clip_hi, value_clip,
                      clipped_value_loss, c_s, c_v, c_l, grad_mu, grad_value, grad_lin_vel, scratch);
-  hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(256), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
+  hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(64 * FIN_WAVES), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
                      entropy_coef, lin_vel_coef, loss_out, stats_out, accumulate_stats, grad_std);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

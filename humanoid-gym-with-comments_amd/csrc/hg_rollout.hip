@@ -442,52 +442,50 @@ __global__ void __launch_bounds__(TPB) k_gather_stacked(const int64_t* __restric
     }
   }
   const int back = t - 1 - lane;
-  const bool rs = lane < F - 1 && back >= 0 && dones[(int64_t)back * dts + (int64_t)e * des] != 0;
-  const uint64_t m = __ballot(rs);
-  const int jz = m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0;  // positions j < jz are zero
+  // the reset scan's byte loaded first and unconditionally (a clamped slot): waiting for it later
+  // (in-order vmcnt) leaves the frame loads issued after it in flight
+  const bool scan = lane < F - 1 && back >= 0;
+  uint32_t dz = dones[(int64_t)max(back, 0) * dts + (int64_t)e * des];
   // element c of the row: zero below Z (the history a reset cleared), slot 0's stack below Bnd
   // (positions before the rollout: init position j + t, i.e. init row + t W + c), then the
   // env's frames tau = t - (F - 1) + j .. t — one contiguous run in the env-major frame table
   const int row = F * W;
-  const int Z = jz * W;
   const int Bnd = (t < F - 1 ? F - 1 - t : 0) * W;
   const S* __restrict__ srcA = init + (int64_t)e * row + (int64_t)t * W;
   const int64_t offB = ((int64_t)e * T + t - (F - 1)) * W;  // frames + offB + c, for c >= Bnd only
   D* __restrict__ out = dst + i * (int64_t)row;
-  auto elem = [&](int c) -> float {
-    return c < Z ? 0.f : (c < Bnd ? (float)srcA[c] : (float)frames[offB + c]);
-  };
   if constexpr (std::is_same<S, float>::value && std::is_same<D, float>::value) {
-    // 16-byte accesses: each lane moves groups of 4 consecutive elements (4-byte-aligned vector
-    // loads / stores), a group straddling Z or Bnd element by element
-    constexpr int KV = 3;  // 768 elements per pass: a 705-wide stack in one
-    for (int base = 0; base < row; base += 256 * KV) {
-      f32x4u v[KV];
+    // 4-byte accesses, 64 consecutive elements per wave instruction, every load unconditional (a
+    // clamped address past the row's end, the source picked by Bnd with a select): the compiler
+    // keeps all of a pass's loads in flight at once.  They depend on the row index only, so they
+    // are issued before the reset scan resolves (one dependent round trip instead of two); the
+    // history a reset cleared (below Z) is zeroed afterwards.  A 705-wide stack is one pass.
+    constexpr int KD = 12;
+    for (int base = 0; base < row; base += 64 * KD) {
+      float v[KD];
 #pragma unroll
-      for (int k = 0; k < KV; k++) {
-        const int c = base + 4 * (lane + 64 * k);
-        if (c + 3 < row && (c >= Z || c + 3 < Z) && (c >= Bnd || c + 3 < Bnd)) {
-          if (c + 3 < Z) v[k] = (f32x4u){0.f, 0.f, 0.f, 0.f};
-          else if (c + 3 < Bnd) v[k] = *reinterpret_cast<const f32x4u*>(srcA + c);
-          else v[k] = *reinterpret_cast<const f32x4u*>(frames + offB + c);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; q++) v[k][q] = c + q < row ? elem(c + q) : 0.f;
-        }
+      for (int k = 0; k < KD; k++) {
+        const int c = min(base + lane + 64 * k, row - 1);
+        // one load from a selected address (not two predicated loads and a select)
+        const uintptr_t a = c < Bnd ? (uintptr_t)(srcA + c) : (uintptr_t)(frames + offB + c);
+        v[k] = *reinterpret_cast<const __attribute__((address_space(1))) float*>(a);  // a global load
       }
+      // the scan byte is consumed only now, after the frame loads have been issued
+      asm volatile("" : "+v"(dz));
+      const uint64_t m = __ballot(scan && dz != 0);
+      const int Z = (m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0) * W;  // positions j < jz are zero
 #pragma unroll
-      for (int k = 0; k < KV; k++) {
-        const int c = base + 4 * (lane + 64 * k);
-        if (c + 3 < row) {
-          *reinterpret_cast<f32x4u*>(out + c) = v[k];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; q++)
-            if (c + q < row) out[c + q] = v[k][q];
-        }
+      for (int k = 0; k < KD; k++) {
+        const int c = base + lane + 64 * k;
+        if (c < row) out[c] = c < Z ? 0.f : v[k];
       }
     }
   } else {
+    const uint64_t m = __ballot(scan && dz != 0);
+    const int Z = (m ? F - 1 - (__ffsll((unsigned long long)m) - 1) : 0) * W;
+    auto elem = [&](int c) -> float {
+      return c < Z ? 0.f : (c < Bnd ? (float)srcA[c] : (float)frames[offB + c]);
+    };
     constexpr int KB = 16;
     for (int base = 0; base < row; base += 64 * KB) {
       float v[KB];
