@@ -251,7 +251,7 @@ int hg_create(const hg_cfg* cfg, const hg_model* model, void* arena, size_t aren
   S.env_rows = (int32_t*)(s->arena + s->L.env_rows);
   S.env_order = (int32_t*)(s->arena + s->L.env_order);
   {
-    // K_step's wave balancing (hg_physics.hip k_env_order): on unless HG_WAVE_BALANCE=0
+    // K_step's wave balancing (hg_common.h hg_env_order_block, run by the post launch): on unless HG_WAVE_BALANCE=0
     const char* wb = getenv("HG_WAVE_BALANCE");
     S.balance = (wb && wb[0] == '0') ? 0 : 1;
   }

@@ -153,3 +153,47 @@ __device__ __forceinline__ f3 quat_apply(float qx, float qy, float qz, float qw,
   f3 t = 2.0f * cross(xyz, v);
   return v + qw * t + cross(xyz, t);
 }
+
+// K_step's env order for wave balancing (HgState::env_order; k_step maps its blocks through it):
+// per XCD env range (k_step's block -> pair map: XCD x owns pairs p0 .. p0 + cnt - 1 of the nb =
+// ceil(n / 2) pairs), a stable counting sort of the range's envs by the PGS groups of their last
+// substep (HgState::env_rows), heaviest first (12 bins: ceil(rows / 3) capped at 11).  One
+// 256-thread block per range, run as extra blocks of the post launch (k_window_stats), so the
+// order is ready for the next step's K_step without a launch of its own.
+constexpr int HG_ORD_T = 256, HG_ORD_BINS = 12;
+__device__ __forceinline__ int hg_order_bin(int rows) {
+  return HG_ORD_BINS - 1 - min((max(rows, 0) + 2) / 3, HG_ORD_BINS - 1);
+}
+__device__ inline void hg_env_order_block(const int32_t* __restrict__ rows, int32_t* __restrict__ order, int n,
+                                          int xcd) {
+  __shared__ int c[HG_ORD_BINS * HG_ORD_T];
+  __shared__ int ws[HG_ORD_T];
+  const int nb = (n + 1) / 2, t = threadIdx.x;
+  const int cnt = (nb >> 3) + (xcd < (nb & 7) ? 1 : 0);
+  const int p0 = xcd * (nb >> 3) + min(xcd, nb & 7);
+  const int e0 = 2 * p0, m = max(0, min(n, 2 * (p0 + cnt)) - e0);
+  const int per = (m + HG_ORD_T - 1) / HG_ORD_T;
+  const int a0 = e0 + min(m, t * per), a1 = e0 + min(m, (t + 1) * per);
+  for (int k = 0; k < HG_ORD_BINS; k++) c[k * HG_ORD_T + t] = 0;
+  for (int e = a0; e < a1; e++) c[hg_order_bin(rows[e]) * HG_ORD_T + t] += 1;  // own column: no atomics
+  __syncthreads();
+  // exclusive prefix of c in (bin, thread) order: thread t owns flat entries [12 t, 12 t + 12)
+  int s = 0;
+  for (int i = 0; i < HG_ORD_BINS; i++) s += c[HG_ORD_BINS * t + i];
+  ws[t] = s;
+  __syncthreads();
+  for (int off = 1; off < HG_ORD_T; off <<= 1) {
+    const int v = t >= off ? ws[t - off] : 0;
+    __syncthreads();
+    ws[t] += v;
+    __syncthreads();
+  }
+  int run = ws[t] - s;
+  for (int i = 0; i < HG_ORD_BINS; i++) {
+    const int v = c[HG_ORD_BINS * t + i];
+    c[HG_ORD_BINS * t + i] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int e = a0; e < a1; e++) order[e0 + c[hg_order_bin(rows[e]) * HG_ORD_T + t]++] = e;
+}

@@ -1129,7 +1129,16 @@ constexpr int WIN_ROWS = 4;  // (env, table) rows per k_window_stats block, one 
 __global__ void __launch_bounds__(64 * WIN_ROWS) k_window_stats(HgWindow A, HgWindow B, const float* __restrict__ frame_a,
                                                       const float* __restrict__ frame_b,
                                                       const uint8_t* __restrict__ reset, int n, float* ep_stats,
-                                                      float inv_len_s, int ring_slot) {
+                                                      float inv_len_s, int ring_slot,
+                                                      const int32_t* __restrict__ env_rows,
+                                                      int32_t* __restrict__ env_order, int nsort) {
+  static_assert(64 * WIN_ROWS == HG_ORD_T, "the order blocks use the window block's threads");
+  // blocks 0 .. nsort - 1: the next K_step's env order (hg_common.h), first so that they start
+  // with the launch and run beside the window rows
+  if ((int)blockIdx.x < nsort) {
+    hg_env_order_block(env_rows, env_order, n, blockIdx.x);
+    return;
+  }
   if (blockIdx.x == gridDim.x - 1) {
     const int k = threadIdx.x;
     float* acc = ep_stats + 24;
@@ -1148,7 +1157,7 @@ __global__ void __launch_bounds__(64 * WIN_ROWS) k_window_stats(HgWindow A, HgWi
     return;
   }
   // one wave per (env, table) row, WIN_ROWS rows per block
-  const int b = blockIdx.x * WIN_ROWS + (threadIdx.x >> 6);
+  const int b = (blockIdx.x - nsort) * WIN_ROWS + (threadIdx.x >> 6);
   if (b >= 2 * n) return;
   const int lane = threadIdx.x & 63;
   const bool a = b < n;
@@ -1178,8 +1187,11 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
   else
     hipLaunchKernelGGL(k_post, dim3((n + 63) / 64), dim3(64), 0, stream, *S, counter, mode, mask, frame_obs,
                        frame_priv);
-  const int g = (2 * n + WIN_ROWS - 1) / WIN_ROWS + 1;  // WIN_ROWS (env, table) rows per block + the statistics block
+  // the env-order blocks (K_step's wave balancing), WIN_ROWS (env, table) rows per block, the
+  // statistics block
+  const int nsort = S->balance ? 8 : 0;
+  const int g = nsort + (2 * n + WIN_ROWS - 1) / WIN_ROWS + 1;
   hipLaunchKernelGGL(k_window_stats, dim3(g), dim3(64 * WIN_ROWS), 0, stream, obs, priv, frame_obs, frame_priv,
-                     S->reset_buf, n, S->ep_stats, inv_len_s, ep_slot);
+                     S->reset_buf, n, S->ep_stats, inv_len_s, ep_slot, S->env_rows, S->env_order, nsort);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -609,8 +609,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   // on the same SIMD (scripts/probes/placement_probe.hip: every SIMD of the chip gets one block
   // of each half, in dispatch order), i.e. within an XCD block kx and kx + cnt / 2.  A wave's cost
   // is its heavier env's constraint rows (the PGS runs max of the two envs' groups) and the launch
-  // ends with its slowest SIMD, so the XCD's env pairs, sorted heaviest first by k_env_order from
-  // the previous step's rows, go heaviest to block kx and lightest to its SIMD partner.  Every env
+  // ends with its slowest SIMD, so the XCD's env pairs, sorted heaviest first by env_order_block
+  // (hg_common.h; run inside the post launch after each step) from the step's rows, go heaviest to block kx and lightest to its SIMD partner.  Every env
   // stays in its XCD's range (the L2 locality of the SoA stores) and its result does not depend
   // on which env shares its wave.
   int pair = p0 + kx;
@@ -1319,50 +1319,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   for (int i = l; i < HG_LAMW; i += 32) S.lambda[i * np + e] = E.lamst[i];
 }
 
-// K_step's env order for wave balancing: per XCD env range (the block -> pair map of k_step), a
-// stable counting sort of the envs by the PGS groups of their last substep, heaviest first (12
-// bins: ceil(rows / 3) capped at 11).  One block per range; thread t counts a contiguous chunk.
-constexpr int ORD_T = 256, ORD_BINS = 12;
-__device__ __forceinline__ int order_bin(int rows) { return ORD_BINS - 1 - min((max(rows, 0) + 2) / 3, ORD_BINS - 1); }
-
-__global__ void __launch_bounds__(ORD_T) k_env_order(const int32_t* __restrict__ rows, int32_t* __restrict__ order, int n,
-                                                     int nb) {
-  __shared__ int c[ORD_BINS * ORD_T];
-  __shared__ int ws[ORD_T];
-  const int xcd = blockIdx.x, t = threadIdx.x;
-  const int cnt = (nb >> 3) + (xcd < (nb & 7) ? 1 : 0);
-  const int p0 = xcd * (nb >> 3) + min(xcd, nb & 7);
-  const int e0 = 2 * p0, m = max(0, min(n, 2 * (p0 + cnt)) - e0);
-  const int per = (m + ORD_T - 1) / ORD_T;
-  const int a0 = e0 + min(m, t * per), a1 = e0 + min(m, (t + 1) * per);
-  for (int k = 0; k < ORD_BINS; k++) c[k * ORD_T + t] = 0;
-  for (int e = a0; e < a1; e++) c[order_bin(rows[e]) * ORD_T + t] += 1;  // own column: no atomics
-  __syncthreads();
-  // exclusive prefix of c in (bin, thread) order: thread t owns flat entries [12 t, 12 t + 12)
-  int s = 0;
-  for (int i = 0; i < ORD_BINS; i++) s += c[ORD_BINS * t + i];
-  ws[t] = s;
-  __syncthreads();
-  for (int off = 1; off < ORD_T; off <<= 1) {
-    const int v = t >= off ? ws[t - off] : 0;
-    __syncthreads();
-    ws[t] += v;
-    __syncthreads();
-  }
-  int run = ws[t] - s;
-  for (int i = 0; i < ORD_BINS; i++) {
-    const int v = c[ORD_BINS * t + i];
-    c[ORD_BINS * t + i] = run;
-    run += v;
-  }
-  __syncthreads();
-  for (int e = a0; e < a1; e++) order[e0 + c[order_bin(rows[e]) * ORD_T + t]++] = e;
-}
-
 extern "C" int hg_launch_step(const HgState* S, const hg_cfg* hcfg, const float* actions, uint64_t step_counter,
                               hipStream_t stream) {
-  const int grid = (S->n + 1) / 2;
-  if (S->balance) hipLaunchKernelGGL(k_env_order, dim3(8), dim3(ORD_T), 0, stream, S->env_rows, S->env_order, S->n, grid);
+  const int grid = (S->n + 1) / 2;  // env pairs (env_order: rebuilt by the post launch, hg_envlogic.hip)
   StepParams P;
   P.dt = hcfg->sim_dt;
   P.gz = hcfg->gravity_z;
