@@ -197,3 +197,69 @@ __device__ inline void hg_env_order_block(const int32_t* __restrict__ rows, int3
   __syncthreads();
   for (int e = a0; e < a1; e++) order[e0 + c[hg_order_bin(rows[e]) * HG_ORD_T + t]++] = e;
 }
+
+// One wave's 16 x 16 tile of x W^T on v_mfma_f32_16x16x4_f32 (A[i = l & 15][k = l >> 4], B[k = l >> 4]
+// [j = l & 15], C row 4 (l >> 4) + q, column l & 15): lane group g = l >> 4 owns the 8 consecutive k
+// [8g, 8g + 8) of each 32-wide chunk (xr / wr point at its row's element 8g); MFMA step s takes
+// k = 8g + s, two accumulators (even / odd steps) cover the dependent-accumulator latency, the next
+// chunk's loads are issued before the current chunk's MFMAs.  k past the end loads 0 (the last,
+// partial chunk only).  VEC: rows 16-byte aligned.  Used by k_linear_act16 (hg_linear.hip) and the
+// rollout's fused policy tail (hg_rollout.hip), which therefore produce the same bits.
+typedef float hg_f32x4 __attribute__((ext_vector_type(4)));
+typedef float hg_f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+template <bool VEC, bool TAIL>
+__device__ __forceinline__ void hg_ld8k(const float* __restrict__ p, int k0, int K, float v[8]) {
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (!TAIL) {
+      if (VEC) {
+        const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+      } else {
+        const hg_f32x4u t = *reinterpret_cast<const hg_f32x4u*>(p + 4 * q);
+        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; j++) v[4 * q + j] = (k0 + 4 * q + j < K) ? p[4 * q + j] : 0.f;
+    }
+  }
+}
+template <bool VEC>
+__device__ __forceinline__ void hg_lin16_acc(const float* __restrict__ xr, const float* __restrict__ wr, int K, int g,
+                                             hg_f32x4& acc0, hg_f32x4& acc1) {
+  acc0 = (hg_f32x4)0.f;
+  acc1 = (hg_f32x4)0.f;
+  const int kfull = K & ~31;
+  float a[2][8], w[2][8];
+  if (kfull > 0) {
+    hg_ld8k<VEC, false>(xr, 0, K, a[0]);
+    hg_ld8k<VEC, false>(wr, 0, K, w[0]);
+  }
+  for (int kb = 0; kb < kfull; kb += 64) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int kn = kb + 32 * (j + 1);
+      if (kn < kfull) {
+        hg_ld8k<VEC, false>(xr + kn, kn, K, a[j ^ 1]);
+        hg_ld8k<VEC, false>(wr + kn, kn, K, w[j ^ 1]);
+      }
+      if (kb + 32 * j < kfull) {
+#pragma unroll
+        for (int s2 = 0; s2 < 8; s2 += 2) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s2], w[j][s2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s2 + 1], w[j][s2 + 1], acc1, 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (kfull < K) {
+    hg_ld8k<VEC, true>(xr + kfull, kfull, K - 8 * g, a[0]);
+    hg_ld8k<VEC, true>(wr + kfull, kfull, K - 8 * g, w[0]);
+#pragma unroll
+    for (int s2 = 0; s2 < 8; s2 += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2], w[0][s2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2 + 1], w[0][s2 + 1], acc1, 0, 0, 0);
+    }
+  }
+}

@@ -173,32 +173,9 @@ __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act(const float* __re
   }
 }
 
-// Small-output variant: one wave per 16 x 16 tile on v_mfma_f32_16x16x4_f32 (A[i = l & 15][k = l >> 4],
-// B[k = l >> 4][j = l & 15], C row 4 (l >> 4) + q, column l & 15).  Lane group g = l >> 4 owns the 8
-// consecutive k [8g, 8g + 8) of each 32-wide chunk; MFMA step s takes k = 8g + s.  Four times the
+// Small-output variant: one wave per 16 x 16 tile (hg_lin16_acc, hg_common.h: shared with the
+// rollout's fused policy tail in hg_rollout.hip, so the two give the same bits).  Four times the
 // waves of the 32 x 32 tile for the same output, for the latency-bound 4096-row rollout layers.
-// Two accumulators (even / odd steps) cover the 40-cycle dependent-accumulator latency.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <bool VEC, bool TAIL>
-__device__ __forceinline__ void ld8k(const float* __restrict__ p, int k0, int K, float v[8]) {
-#pragma unroll
-  for (int q = 0; q < 2; q++) {
-    if (!TAIL) {
-      if (VEC) {
-        const float4 t = *reinterpret_cast<const float4*>(p + 4 * q);
-        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
-      } else {
-        const f32x4u t = *reinterpret_cast<const f32x4u*>(p + 4 * q);
-        v[4 * q] = t[0]; v[4 * q + 1] = t[1]; v[4 * q + 2] = t[2]; v[4 * q + 3] = t[3];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; j++) v[4 * q + j] = (k0 + 4 * q + j < K) ? p[4 * q + j] : 0.f;
-    }
-  }
-}
-
 template <bool VEC, bool ELU>
 __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act16(const float* __restrict__ x, int64_t ldx,
                                                                  const float* __restrict__ W,
@@ -216,39 +193,8 @@ __global__ void __launch_bounds__(64 * LIN_WAVES) k_linear_act16(const float* __
   const int c0 = (int)(t % tiles_n) * 16;
   const float* xr = x + min<int64_t>(r0 + i, rows - 1) * ldx + 8 * g;
   const float* wr = W + (int64_t)min(c0 + i, N - 1) * K + 8 * g;
-  f32x4 acc0 = (f32x4)0.f, acc1 = (f32x4)0.f;
-  const int kfull = K & ~31;
-  float a[2][8], w[2][8];
-  if (kfull > 0) {
-    ld8k<VEC, false>(xr, 0, K, a[0]);
-    ld8k<VEC, false>(wr, 0, K, w[0]);
-  }
-  for (int kb = 0; kb < kfull; kb += 64) {
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const int kn = kb + 32 * (j + 1);
-      if (kn < kfull) {
-        ld8k<VEC, false>(xr + kn, kn, K, a[j ^ 1]);
-        ld8k<VEC, false>(wr + kn, kn, K, w[j ^ 1]);
-      }
-      if (kb + 32 * j < kfull) {
-#pragma unroll
-        for (int s2 = 0; s2 < 8; s2 += 2) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s2], w[j][s2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s2 + 1], w[j][s2 + 1], acc1, 0, 0, 0);
-        }
-      }
-    }
-  }
-  if (kfull < K) {
-    ld8k<VEC, true>(xr + kfull, kfull, K - 8 * g, a[0]);
-    ld8k<VEC, true>(wr + kfull, kfull, K - 8 * g, w[0]);
-#pragma unroll
-    for (int s2 = 0; s2 < 8; s2 += 2) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2], w[0][s2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][s2 + 1], w[0][s2 + 1], acc1, 0, 0, 0);
-    }
-  }
+  hg_f32x4 acc0, acc1;
+  hg_lin16_acc<VEC>(xr, wr, K, g, acc0, acc1);
   const int c = c0 + i;
   if (c >= N) return;
   const float bc = b ? b[c] : 0.f;

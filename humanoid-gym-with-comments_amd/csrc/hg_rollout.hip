@@ -49,6 +49,91 @@ struct ActHead {
   const float* b;
 };
 
+// mean of the row h (HEAD_K values; global memory or LDS) = W h + b for lane j of the env's 16-lane
+// group, as k_skinny_fwd<12> computes it (same fma chain, the same xor-shuffle tree, the bias added
+// last), so bitwise the two-launch result
+__device__ __forceinline__ float act_head_mean(const float* __restrict__ hrow, const float* __restrict__ W,
+                                               const float* __restrict__ b, int j) {
+  const int k0 = 8 * j;
+  const float4 xa = *reinterpret_cast<const float4*>(hrow + k0);
+  const float4 xb = *reinterpret_cast<const float4*>(hrow + k0 + 4);
+  const float v[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+  float out = 0.f;
+#pragma unroll
+  for (int q = 0; q < HEAD_N; q++) {
+    const float4 wa = *reinterpret_cast<const float4*>(W + q * HEAD_K + k0);
+    const float4 wb = *reinterpret_cast<const float4*>(W + q * HEAD_K + k0 + 4);
+    const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s = fmaf(v[i], w[i], s);
+    s += __shfl_xor(s, 8, 16);
+    s += __shfl_xor(s, 4, 16);
+    s += __shfl_xor(s, 2, 16);
+    s += __shfl_xor(s, 1, 16);
+    out = (j == q) ? s : out;
+  }
+  return out + (j < HEAD_N ? b[j] : 0.f);
+}
+
+// one env's sample / log-prob / storage writes by its 16-lane group, one lane per action (its Philox
+// block computed by each of the group's lanes); the log-prob terms are summed in action order by
+// every lane of the group (the same additions as the one-thread-per-env loop of k_act)
+__device__ __forceinline__ void act_env16(int e, int j, int A, float m, const float* __restrict__ std,
+                                          const float* __restrict__ value, float* __restrict__ act_out,
+                                          float* __restrict__ logp_out, float* __restrict__ mu_out,
+                                          float* __restrict__ sigma_out, float* __restrict__ value_out,
+                                          int row_offset, uint64_t seed, uint64_t counter) {
+  const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
+  float term = 0.f;
+  if (j < A) {
+    float z4[4];
+    normals4(philox_key(seed, (uint32_t)(e + row_offset), counter, (uint32_t)(j >> 2)), z4);
+    const float z = (j & 3) == 0 ? z4[0] : (j & 3) == 1 ? z4[1] : (j & 3) == 2 ? z4[2] : z4[3];
+    const float s = std[j];
+    const float a = m + s * z;
+    const float d = a - m;
+    term = -(d * d) / (2.0f * (s * s)) - logf(s) - c;
+    act_out[(size_t)e * A + j] = a;
+    mu_out[(size_t)e * A + j] = m;
+    sigma_out[(size_t)e * A + j] = s;
+  }
+  float lp = 0.f;
+  for (int jj = 0; jj < A; jj++) lp += __shfl(term, jj, ACT_LANES);
+  if (j == 0) {
+    logp_out[e] = lp;
+    if (value) value_out[e] = value[e];
+  }
+}
+
+// observation rows -> storage slot: one wave per (table, row), lanes along the row; source rows
+// strided (the env's stacks are column slices of its history windows), storage rows packed.  Wave
+// w0 of the copy waves (nw of them) takes rows w0, w0 + nw, ..
+template <typename OT>
+__device__ __forceinline__ void act_copy_obs(int64_t w0, int64_t nw, const float* __restrict__ obs,
+                                             const float* __restrict__ cobs, int n, int64_t obs_w, int64_t cobs_w,
+                                             int64_t obs_ld, int64_t obs_c0, int64_t cobs_ld, int64_t obs_out_ld,
+                                             OT* __restrict__ obs_out, OT* __restrict__ cobs_out) {
+  const int64_t rows = cobs_w > 0 ? 2 * (int64_t)n : n;
+  const int lane = threadIdx.x & 63;
+  for (int64_t q = w0; q < rows; q += nw) {
+    const bool o = q < n;
+    const int64_t r = o ? q : q - n;
+    const int64_t w = o ? obs_w : cobs_w;
+    const float* __restrict__ src = o ? obs + r * obs_ld + obs_c0 : cobs + r * cobs_ld;
+    OT* __restrict__ dst = o ? obs_out + r * obs_out_ld : cobs_out + r * w;
+    int64_t c = lane;
+    for (; c + 192 < w; c += 256) {
+      const float a = src[c], b = src[c + 64], d = src[c + 128], e = src[c + 192];
+      store_obs<OT>(dst + c, a);
+      store_obs<OT>(dst + c + 64, b);
+      store_obs<OT>(dst + c + 128, d);
+      store_obs<OT>(dst + c + 192, e);
+    }
+    for (; c < w; c += 64) store_obs<OT>(dst + c, src[c]);
+  }
+}
+
 template <typename OT, bool HEAD>
 __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, ActHead hd, const float* __restrict__ std,
                                             const float* __restrict__ value, const float* __restrict__ obs,
@@ -60,60 +145,16 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, Act
                                             OT* __restrict__ cobs_out, int row_offset, uint64_t seed,
                                             uint64_t counter, int env_blocks) {
   if ((int)blockIdx.x < env_blocks) {
-    const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
     if (A <= ACT_LANES) {
-      // one 16-lane group per env, one lane per action (its Philox block computed by each of the
-      // block's lanes); the log-prob terms are summed in action order by every lane of the group
-      // (the same additions as the one-thread-per-env loop below)
       const int e = (int)(((int64_t)blockIdx.x * TPB + threadIdx.x) / ACT_LANES);
       const int j = threadIdx.x % ACT_LANES;
       if (e >= n) return;  // whole groups leave together
-      float term = 0.f;
-      float mh = 0.f;
-      if (HEAD) {
-        // mean of row e = W h_e + b, as k_skinny_fwd<12> computes it (same fma chain, the same
-        // xor-shuffle tree, the bias added last), so bitwise the two-launch result
-        const int k0 = 8 * j;
-        const float4 xa = *reinterpret_cast<const float4*>(hd.h + (int64_t)e * hd.ld + k0);
-        const float4 xb = *reinterpret_cast<const float4*>(hd.h + (int64_t)e * hd.ld + k0 + 4);
-        const float v[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-        float out = 0.f;
-#pragma unroll
-        for (int q = 0; q < HEAD_N; q++) {
-          const float4 wa = *reinterpret_cast<const float4*>(hd.W + q * HEAD_K + k0);
-          const float4 wb = *reinterpret_cast<const float4*>(hd.W + q * HEAD_K + k0 + 4);
-          const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-          float s = 0.f;
-#pragma unroll
-          for (int i = 0; i < 8; i++) s = fmaf(v[i], w[i], s);
-          s += __shfl_xor(s, 8, 16);
-          s += __shfl_xor(s, 4, 16);
-          s += __shfl_xor(s, 2, 16);
-          s += __shfl_xor(s, 1, 16);
-          out = (j == q) ? s : out;
-        }
-        mh = out + (j < HEAD_N ? hd.b[j] : 0.f);
-      }
-      if (j < A) {
-        float z4[4];
-        normals4(philox_key(seed, (uint32_t)(e + row_offset), counter, (uint32_t)(j >> 2)), z4);
-        const float z = (j & 3) == 0 ? z4[0] : (j & 3) == 1 ? z4[1] : (j & 3) == 2 ? z4[2] : z4[3];
-        const float m = HEAD ? mh : mean[(size_t)e * A + j], s = std[j];
-        const float a = m + s * z;
-        const float d = a - m;
-        term = -(d * d) / (2.0f * (s * s)) - logf(s) - c;
-        act_out[(size_t)e * A + j] = a;
-        mu_out[(size_t)e * A + j] = m;
-        sigma_out[(size_t)e * A + j] = s;
-      }
-      float lp = 0.f;
-      for (int jj = 0; jj < A; jj++) lp += __shfl(term, jj, ACT_LANES);
-      if (j == 0) {
-        logp_out[e] = lp;
-        if (value) value_out[e] = value[e];
-      }
+      const float m = HEAD ? act_head_mean(hd.h + (int64_t)e * hd.ld, hd.W, hd.b, j)
+                           : (j < A ? mean[(size_t)e * A + j] : 0.f);
+      act_env16(e, j, A, m, std, value, act_out, logp_out, mu_out, sigma_out, value_out, row_offset, seed, counter);
       return;
     }
+    const float c = 0.91893853320467274178f;  // log(sqrt(2 pi))
     const int e = blockIdx.x * TPB + threadIdx.x;
     if (e >= n) return;
     float lp = 0.f;
@@ -132,27 +173,72 @@ __global__ void __launch_bounds__(TPB) k_act(const float* __restrict__ mean, Act
     if (value) value_out[e] = value[e];
     return;
   }
-  // observation rows -> storage slot: one wave per (table, row), lanes along the row; source rows
-  // strided (the env's stacks are column slices of its history windows), storage rows packed
-  const int64_t rows = cobs_w > 0 ? 2 * (int64_t)n : n;
-  const int64_t wstride = (int64_t)(gridDim.x - env_blocks) * (TPB / 64);
-  const int lane = threadIdx.x & 63;
-  for (int64_t q = (int64_t)(blockIdx.x - env_blocks) * (TPB / 64) + (threadIdx.x >> 6); q < rows; q += wstride) {
-    const bool o = q < n;
-    const int64_t r = o ? q : q - n;
-    const int64_t w = o ? obs_w : cobs_w;
-    const float* __restrict__ src = o ? obs + r * obs_ld + obs_c0 : cobs + r * cobs_ld;
-    OT* __restrict__ dst = o ? obs_out + r * obs_out_ld : cobs_out + r * w;
-    int64_t c = lane;
-    for (; c + 192 < w; c += 256) {
-      const float a = src[c], b = src[c + 64], d = src[c + 128], e = src[c + 192];
-      store_obs<OT>(dst + c, a);
-      store_obs<OT>(dst + c + 64, b);
-      store_obs<OT>(dst + c + 128, d);
-      store_obs<OT>(dst + c + 192, e);
+  act_copy_obs<OT>((int64_t)(blockIdx.x - env_blocks) * (TPB / 64) + (threadIdx.x >> 6),
+                   (int64_t)(gridDim.x - env_blocks) * (TPB / 64), obs, cobs, n, obs_w, cobs_w, obs_ld, obs_c0,
+                   cobs_ld, obs_out_ld, obs_out, cobs_out);
+}
+
+// The actor's last hidden layer and its output layer in the sampling launch
+// (hg_rollout_act_tail): a block of TAIL_WAVES waves owns 16 rows — wave w computes the 16 x 16
+// tile of columns 16 w .. 16 w + 15 of y = elu(x W3^T + b3) exactly as k_linear_act16 does
+// (hg_lin16_acc, the same epilogue) into LDS, and the block's first 256 threads then run the
+// head and the sampling of its 16 envs from those rows (k_act's HEAD path).  Bitwise the
+// linear_act + hg_rollout_act_head pair; one launch and no global round trip of the hidden row.
+constexpr int TAIL_WAVES = HEAD_K / 16;
+struct ActTail {
+  const float* x;
+  int64_t ldx;
+  const float* W3;
+  const float* b3;
+  int K;
+  const float* W;
+  const float* b;
+};
+
+template <typename OT>
+__global__ void __launch_bounds__(64 * TAIL_WAVES) k_act_tail(ActTail tl, const float* __restrict__ std,
+                                                              const float* __restrict__ value,
+                                                              const float* __restrict__ obs,
+                                                              const float* __restrict__ cobs, int n, int A,
+                                                              int64_t obs_w, int64_t cobs_w, int64_t obs_ld,
+                                                              int64_t obs_c0, int64_t cobs_ld,
+                                                              float* __restrict__ act_out, float* __restrict__ logp_out,
+                                                              float* __restrict__ mu_out, float* __restrict__ sigma_out,
+                                                              float* __restrict__ value_out, int64_t obs_out_ld,
+                                                              OT* __restrict__ obs_out, OT* __restrict__ cobs_out,
+                                                              int row_offset, uint64_t seed, uint64_t counter,
+                                                              int env_blocks) {
+  if ((int)blockIdx.x < env_blocks) {
+    __shared__ __attribute__((aligned(16))) float hs[16][HEAD_K + 4];  // 528-byte rows: 16-byte aligned
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int64_t r0 = (int64_t)blockIdx.x * 16;
+    const int c = wv * 16 + i;
+    {
+      const float* xr = tl.x + (int64_t)min((int)r0 + i, n - 1) * tl.ldx + 8 * g;
+      const float* wr = tl.W3 + (int64_t)c * tl.K + 8 * g;
+      hg_f32x4 acc0, acc1;
+      hg_lin16_acc<true>(xr, wr, tl.K, g, acc0, acc1);
+      const float bc = tl.b3[c];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        float v = acc0[q] + acc1[q] + bc;
+        v = v > 0.f ? v : expm1f(v);
+        hs[4 * g + q][c] = v;
+      }
     }
-    for (; c < w; c += 64) store_obs<OT>(dst + c, src[c]);
+    __syncthreads();
+    if (threadIdx.x >= 16 * ACT_LANES) return;
+    const int el = threadIdx.x / ACT_LANES, j = threadIdx.x % ACT_LANES;
+    const int e = (int)r0 + el;
+    if (e >= n) return;  // whole groups leave together
+    const float m = act_head_mean(&hs[el][0], tl.W, tl.b, j);
+    act_env16(e, j, A, m, std, value, act_out, logp_out, mu_out, sigma_out, value_out, row_offset, seed, counter);
+    return;
   }
+  act_copy_obs<OT>((int64_t)(blockIdx.x - env_blocks) * TAIL_WAVES + (threadIdx.x >> 6),
+                   (int64_t)(gridDim.x - env_blocks) * TAIL_WAVES, obs, cobs, n, obs_w, cobs_w, obs_ld, obs_c0,
+                   cobs_ld, obs_out_ld, obs_out, cobs_out);
 }
 
 __global__ void __launch_bounds__(TPB) k_env(const float* __restrict__ rew, const uint8_t* __restrict__ reset,
@@ -168,9 +254,6 @@ __global__ void __launch_bounds__(TPB) k_env(const float* __restrict__ rew, cons
   if (time_out_out) time_out_out[e] = time_out ? time_out[e] : (uint8_t)0;
 }
 
-}  // namespace
-
-namespace {
 int launch_act(const float* mean, ActHead hd, const float* std, const float* value, const float* obs,
                const float* critic_obs, int num_envs, int num_actions, int64_t obs_width, int64_t critic_obs_width,
                int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld, float* actions_out, float* logp_out,
@@ -204,6 +287,32 @@ int launch_act(const float* mean, ActHead hd, const float* std, const float* val
 #undef HG_ACT
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
+
+int launch_act_tail(ActTail tl, const float* std, const float* value, const float* obs, const float* critic_obs,
+                    int num_envs, int num_actions, int64_t obs_width, int64_t critic_obs_width, int64_t obs_ld,
+                    int64_t obs_col0, int64_t critic_obs_ld, float* actions_out, float* logp_out, float* mu_out,
+                    float* sigma_out, float* value_out, void* obs_out, int64_t obs_out_ld, void* critic_obs_out,
+                    int obs_fp16, int row_offset, uint64_t seed, uint64_t counter, void* stream) {
+  if (!std || (value && !value_out) || !obs || !actions_out || !logp_out || !mu_out || !sigma_out || !obs_out ||
+      num_envs <= 0 || num_actions != HEAD_N || obs_width <= 0 || obs_col0 < 0 ||
+      (obs_out_ld != 0 && obs_out_ld < obs_width) || obs_ld < obs_col0 + obs_width ||
+      (critic_obs_width > 0 && (!critic_obs || !critic_obs_out || critic_obs_ld < critic_obs_width)))
+    return HG_ERR_ARG;
+  const int env_blocks = (num_envs + 15) / 16;
+  const int64_t copy_rows = critic_obs_width > 0 ? 2 * (int64_t)num_envs : num_envs;
+  const int copy_blocks = (int)std::min<int64_t>((copy_rows + TAIL_WAVES - 1) / TAIL_WAVES, 1024);
+  const int64_t cw = critic_obs_width > 0 ? critic_obs_width : 0;
+  const int64_t old = obs_out_ld ? obs_out_ld : obs_width;
+  hipStream_t s = (hipStream_t)stream;
+#define HG_ACTT(OT) hipLaunchKernelGGL((k_act_tail<OT>), dim3(env_blocks + copy_blocks), dim3(64 * TAIL_WAVES), 0, s, tl, \
+                                       std, value, obs, critic_obs, num_envs, num_actions, obs_width, cw, obs_ld,        \
+                                       obs_col0, critic_obs_ld, actions_out, logp_out, mu_out, sigma_out, value_out, old, \
+                                       (OT*)obs_out, (OT*)critic_obs_out, row_offset, seed, counter, env_blocks)
+  if (obs_fp16) HG_ACTT(__half);
+  else HG_ACTT(float);
+#undef HG_ACTT
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
 }  // namespace
 
 extern "C" int hg_rollout_act(const float* mean, const float* std, const float* value, const float* obs,
@@ -234,6 +343,26 @@ extern "C" int hg_rollout_act_head(const float* h, int64_t h_ld, const float* W,
                     value_out, obs_out, obs_out_ld, critic_obs_out, obs_fp16, row_offset, seed, counter, stream);
 }
 
+// hg_rollout_act_head with the actor's last hidden layer folded in (k_act_tail): x [num_envs, tail_k]
+// (row stride x_ld) is that layer's input, W3 [HEAD_K, tail_k] / b3 its weight and bias (ELU), W / b
+// the output layer.  Bitwise hg_linear_act_forward (16 x 16 tile, hg_linear_act_tile's choice at the
+// rollout's row counts) followed by hg_rollout_act_head.  16-byte aligned rows required.
+extern "C" int hg_rollout_act_tail(const float* x, int64_t x_ld, const float* W3, const float* b3, int tail_k,
+                                   const float* W, const float* b, const float* std, const float* value,
+                                   const float* obs, const float* critic_obs, int num_envs, int num_actions,
+                                   int64_t obs_width, int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0,
+                                   int64_t critic_obs_ld, float* actions_out, float* logp_out, float* mu_out,
+                                   float* sigma_out, float* value_out, void* obs_out, int64_t obs_out_ld,
+                                   void* critic_obs_out, int obs_fp16, int row_offset, uint64_t seed, uint64_t counter,
+                                   void* stream) {
+  if (!x || !W3 || !b3 || !W || !b || tail_k <= 0 || tail_k % 4 != 0 || x_ld < tail_k || x_ld % 4 != 0 ||
+      (uintptr_t)x % 16 != 0 || (uintptr_t)W3 % 16 != 0 || (uintptr_t)W % 16 != 0)
+    return HG_ERR_ARG;
+  return launch_act_tail(ActTail{x, x_ld, W3, b3, tail_k, W, b}, std, value, obs, critic_obs, num_envs, num_actions,
+                         obs_width, critic_obs_width, obs_ld, obs_col0, critic_obs_ld, actions_out, logp_out, mu_out,
+                         sigma_out, value_out, obs_out, obs_out_ld, critic_obs_out, obs_fp16, row_offset, seed, counter,
+                         stream);
+}
 extern "C" int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs,
                               const float* values, int num_envs, float gamma, float* rewards_out,
                               uint8_t* dones_out, uint8_t* time_outs_out, void* stream) {

@@ -780,6 +780,39 @@ def mlp_infer_hidden(net, x):
     return h
 
 
+# the actor's last hidden layer folded into the sampling launch as well (hg_rollout_act_tail)
+TAIL_FUSED = os.environ.get("HG_ACT_TAIL", "1") != "0"
+
+
+def mlp_infer_tail(net, x):
+    """For hg_rollout_act_tail: the hidden layers of ``net`` but its last one, as mlp_infer_hidden
+    runs them, and that last hidden layer's (W, b) -> (h, W, b); None (nothing computed) unless
+    that layer is 128 wide and its separate route would be linear_act's 16 x 16 tile on aligned
+    rows — so the fused launch gives the separate launches' bits."""
+    if not (TAIL_FUSED and fusable(net)):
+        return None
+    mods = list(net)
+    if len(mods) < 5:
+        return None
+    lin = mods[-3]
+    W, b = lin.weight, lin.bias
+    rows, K = x.shape[0], W.shape[1]
+    if (W.device != x.device or not x.is_cuda or x.dim() != 2 or x.dtype != torch.float32
+            or W.shape[0] != 128 or K % 4 or not W.is_contiguous() or W.data_ptr() % 16 or not b.is_contiguous()
+            or _route(_GEMM_FWD, rows, K, 128) or (K, 128) in _GEMM_FWD_SPLITK or not FUSED_FORWARD
+            or rows > _FUSED_FWD_ROWS.get((K, 128), 0) or int(N.lib().hg_linear_act_tile(rows, 128, K)) != 5):
+        return None
+    params = _params(net)
+    fimg = _forward_images(params, len(params) // 2, rows, x.device, False)[0]
+    h = x
+    for j in range(0, len(mods) - 3, 2):
+        h = _hidden_forward(h, mods[j].weight, mods[j].bias, fimg, j // 2)
+    if not (h.dim() == 2 and h.dtype == torch.float32 and h.stride(1) == 1 and h.stride(0) % 4 == 0
+            and h.data_ptr() % 16 == 0 and h.shape[1] == K):
+        h = h.contiguous()
+    return h, W, b
+
+
 def head_fusable(h, W):
     """The output layer W applied to h can run inside hg_rollout_act_head (12 x 128, aligned rows)."""
     return (h is not None and tuple(W.shape) == (12, 128) and W.is_contiguous() and h.dim() == 2

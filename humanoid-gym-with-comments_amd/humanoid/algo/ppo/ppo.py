@@ -236,16 +236,22 @@ class PPO:
         t = st.step
         # the actor's output layer runs inside the sampling launch when it is the 12 x 128 head
         # (hg_rollout_act_head: bitwise the separate output-layer launch); the mean lands in mu
-        mean = head = None
+        mean = head = tail = None
         last = ac.actor[-1]
         if (HEAD_FUSED and ac.policy_dtype == "fp32" and ac.fused_mlp and not torch.is_grad_enabled()
                 and isinstance(last, torch.nn.Linear) and tuple(last.weight.shape) == (12, 128)
                 and last.bias is not None and last.bias.is_contiguous() and hg_mlp.fusable(ac.actor)):
-            h = hg_mlp.mlp_infer_hidden(ac.actor, obs)
-            if hg_mlp.head_fusable(h, last.weight):
-                head = (h, last.weight, last.bias)
+            # the last hidden layer too when its route allows (hg_rollout_act_tail), else the head only
+            if last.weight.is_contiguous() and last.weight.data_ptr() % 16 == 0:
+                tail = hg_mlp.mlp_infer_tail(ac.actor, obs)
+            if tail is not None:
+                head = tail
             else:
-                mean = last(h).contiguous()
+                h = hg_mlp.mlp_infer_hidden(ac.actor, obs)
+                if hg_mlp.head_fusable(h, last.weight):
+                    head = (h, last.weight, last.bias)
+                else:
+                    mean = last(h).contiguous()
         else:
             mean = ac._mlp(ac.actor, obs).contiguous()
         defer = self._defer_values()
@@ -265,7 +271,12 @@ class PPO:
             w, c0 = st.frame_width, obs.shape[1] - st.frame_width
         else:
             w, c0 = obs.shape[1], 0
-        if head is not None:
+        if tail is not None:
+            x3, W3, b3 = tail
+            W, b = last.weight, last.bias
+            fn = N.lib().hg_rollout_act_tail
+            lead = (p(x3), ctypes.c_int64(x3.stride(0)), p(W3), p(b3), W3.shape[1], p(W), p(b), p(std))
+        elif head is not None:
             h, W, b = head
             fn = N.lib().hg_rollout_act_head
             lead = (p(h), ctypes.c_int64(h.stride(0)), p(W), p(b), W.shape[1], p(std))

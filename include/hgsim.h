@@ -292,6 +292,21 @@ int hg_rollout_act_head(const float* h, int64_t h_ld, const float* W, const floa
                         int64_t critic_obs_ld, float* actions_out, float* logp_out, float* mu_out, float* sigma_out,
                         float* value_out, void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16,
                         int row_offset, uint64_t seed, uint64_t counter, void* stream);
+/* hg_rollout_act_head with the actor's last hidden layer folded in as well (one launch instead of
+ * hg_linear_act_forward + hg_rollout_act_head): h = elu(x W3^T + b3) for x [N, tail_k] rows x_ld
+ * apart, W3 [128, tail_k], b3 [128], computed as hg_linear_act_forward's 16 x 16 tile computes it
+ * (the tile hg_linear_act_tile picks for the rollout's row counts: bitwise that launch pair's
+ * result), kept on chip, then the head W [12, 128], b [12] and the sampling as in
+ * hg_rollout_act_head.  16-byte aligned x / W3 / W, x_ld and tail_k multiples of 4, A == 12 (else
+ * HG_ERR_ARG: run the two launches).  Replaces, with hg_rollout_act_head, ActorCritic.act's last
+ * hidden layer + output layer (reference actor_critic.py:53-89, 111-121). */
+int hg_rollout_act_tail(const float* x, int64_t x_ld, const float* W3, const float* b3, int tail_k, const float* W,
+                        const float* b, const float* std, const float* value, const float* obs,
+                        const float* critic_obs, int num_envs, int num_actions, int64_t obs_width,
+                        int64_t critic_obs_width, int64_t obs_ld, int64_t obs_col0, int64_t critic_obs_ld,
+                        float* actions_out, float* logp_out, float* mu_out, float* sigma_out, float* value_out,
+                        void* obs_out, int64_t obs_out_ld, void* critic_obs_out, int obs_fp16, int row_offset,
+                        uint64_t seed, uint64_t counter, void* stream);
 int hg_rollout_env(const float* rewards, const uint8_t* reset, const uint8_t* time_outs, const float* values,
                    int num_envs, float gamma, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out,
                    void* stream);

@@ -986,6 +986,46 @@ def test_fused_head_matches_two_launches():
         torch.testing.assert_close(out[True]["mu"], ac.actor(obs), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("n", [4096, 1000])
+def test_fused_tail_matches_head_and_two_launches(n):
+    """hg_rollout_act_tail (the actor's last hidden layer 256 -> 128 + ELU and its 12 x 128 output
+    layer inside the sampling launch) writes bitwise what the head-only fused launch
+    (linear_act, then hg_rollout_act_head) and the two-launch form write, at the bench's row count
+    and at a ragged one (a partial 16-row block)."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO, hg_mlp
+    from humanoid.algo.ppo import ppo as ppo_mod
+    torch.manual_seed(7)
+    ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                     init_noise_std=0.8).to("cuda:0")
+    big = torch.randn(n, 705 + 47, device="cuda:0")
+    obs, cobs = big[:, 47:], torch.randn(n, 219, device="cuda:0")
+    with torch.inference_mode():
+        assert hg_mlp.mlp_infer_tail(ac.actor, obs) is not None  # the tail route is the one taken
+        assert hg_mlp.mlp_infer_tail(ac.actor, obs.cpu()) is None  # never a host tensor's address
+    out = {}
+    try:
+        for mode in ("two", "head", "tail"):
+            ppo_mod.HEAD_FUSED = mode != "two"
+            hg_mlp.TAIL_FUSED = mode == "tail"
+            ppo = PPO(ac, device="cuda:0")
+            ppo._rollout_seed = 777
+            ppo.init_storage(n, 2, [705], [219], [12])
+            with torch.inference_mode():
+                ppo.act(obs, cobs)
+            st = ppo.storage
+            out[mode] = {k: getattr(st, k)[0].clone() for k in
+                         ("actions", "actions_log_prob", "mu", "sigma", "observations", "privileged_observations")}
+    finally:
+        ppo_mod.HEAD_FUSED = True
+        hg_mlp.TAIL_FUSED = True
+    for mode in ("head", "tail"):
+        for k in out[mode]:
+            assert torch.equal(out[mode][k], out["two"][k]), (mode, k)
+    with torch.inference_mode():
+        torch.testing.assert_close(out["tail"]["mu"], ac.actor(obs), rtol=1e-5, atol=1e-5)
+
+
 def test_set_root_state_and_env_props(env):
     """hg_set_root_state (all envs, clears contact warm-starts) and hg_set_env_props (DR
     friction / base mass) through the C ABI."""
