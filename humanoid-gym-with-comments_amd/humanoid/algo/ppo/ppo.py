@@ -635,24 +635,32 @@ class PPO:
         torch.cuda.synchronize(dev)
         if self._flat_grad is None:
             self.optimizer.zero_grad(set_to_none=True)  # backward allocates the grads in the graph pool
-        # minibatch rows land in static buffers: the three row gathers are one HIP launch
-        self._mb_obs = torch.empty(mb, st.obs_shape[0], dtype=mb_dtype or st.obs_dtype, device=dev)
-        self._mb_critic = (torch.empty(mb, critic.shape[1], dtype=mb_dtype or critic.dtype, device=dev)
-                           if critic is not obs else self._mb_obs)
-        self._mb_packed = torch.empty(mb, self._packed.shape[1], dtype=torch.float32, device=dev)
-        tables = [(self._packed, self._mb_packed)]
-        if not frames:
-            tables.insert(0, (obs, self._mb_obs))
-        if critic is not obs:
-            tables.insert(1 if not frames else 0, (critic, self._mb_critic))
-        self._mb_tables, self._mb_widths = tables, widths
+        self._whole = (not self._dp and self._flat_grad is None) or self._collective_in_graph()
+        # minibatch rows land in static buffers: the three row gathers are one HIP launch.  The
+        # reference draws ONE permutation per update and walks the same minibatches in every epoch
+        # (rollout_storage.py:153-177), so the one-graph form keeps one buffer set per minibatch and
+        # gathers only in the first epoch (380 MB at the bench's size); the two-graph form re-gathers
+        reuse = self._whole and self.num_learning_epochs > 1 and os.environ.get("HG_MB_REUSE", "1") != "0"
+        nsets = self.num_mini_batches if reuse else 1
+        self._mb_sets = []
+        for _ in range(nsets):
+            m_obs = torch.empty(mb, st.obs_shape[0], dtype=mb_dtype or st.obs_dtype, device=dev)
+            m_critic = (torch.empty(mb, critic.shape[1], dtype=mb_dtype or critic.dtype, device=dev)
+                        if critic is not obs else m_obs)
+            m_packed = torch.empty(mb, self._packed.shape[1], dtype=torch.float32, device=dev)
+            tables = [(self._packed, m_packed)]
+            if not frames:
+                tables.insert(0, (obs, m_obs))
+            if critic is not obs:
+                tables.insert(1 if not frames else 0, (critic, m_critic))
+            self._mb_sets.append((m_obs, m_critic, m_packed, tables))
+        self._mb_widths = widths
         # the whole update (epochs x minibatches, each with its LR rule and Adam step) is ONE graph
         # reading its row indices from a static permutation buffer at world size 1.  Data parallel,
         # the default is two graphs per minibatch with the eager gradient all-reduce between their
         # replays (RCCL or gloo; timed by comm_timer).  On request (HG_DP_GRAPH_COLLECTIVE=1, RCCL
         # only) the all-reduce is captured inside the one graph between each backward and its step;
         # a rank whose capture fails pulls every rank back to the two-graph form in this process.
-        self._whole = (not self._dp and self._flat_grad is None) or self._collective_in_graph()
         if self._whole:
             nmb = self.num_mini_batches
             self._perm = torch.zeros(nmb * mb, dtype=torch.int64, device=dev)
@@ -661,11 +669,13 @@ class PPO:
             try:
                 # thread_local: the process group's watchdog thread may query its events meanwhile
                 with _capturing(g, "thread_local" if self._dp else "global"):
-                    for _ in range(self.num_learning_epochs):
+                    for ep in range(self.num_learning_epochs):
                         for i in range(nmb):
                             if self._flat_grad is None:
                                 self.optimizer.zero_grad(set_to_none=True)  # fresh gradients from each backward
-                            self._mb_backward(self._perm[i * mb:(i + 1) * mb])  # zeroes the flat buffer (dp)
+                            k = i if len(self._mb_sets) > 1 else 0
+                            # zeroes the flat buffer (dp); gathers minibatch i's rows in the first epoch only
+                            self._mb_backward(self._perm[i * mb:(i + 1) * mb], k, ep == 0 or len(self._mb_sets) == 1)
                             if self._dp:
                                 dist.all_reduce(self._flat_grad)  # gradients + the KL slot, in the graph
                             self._mb_step()
@@ -724,18 +734,21 @@ class PPO:
             return 0
         return self.num_learning_epochs * self.num_mini_batches + 1
 
-    def _mb_backward(self, idx):
-        """Captured minibatch body: gather rows -> losses -> backward (+ KL mean, loss sums)."""
+    def _mb_backward(self, idx, k=0, gather=True):
+        """Captured minibatch body: gather rows (into buffer set k; ``gather`` False: the set
+        already holds these rows) -> losses -> backward (+ KL mean, loss sums)."""
         if self._flat_grad is not None:
             self._flat_grad.zero_()
-        if self.storage.obs_frames is not None:
-            # frame-only storage: the stacked obs rows and the plain tables in one launch
-            self.storage.gather_stacked(idx, self._mb_obs, self._mb_tables, use_prepared=True)
-        else:
-            gather_rows(idx, self._mb_tables)
-        crit_b = self._mb_critic
-        b = {"obs": self._mb_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
-        pk = self._mb_packed
+        m_obs, m_critic, m_packed, tables = self._mb_sets[k]
+        if gather:
+            if self.storage.obs_frames is not None:
+                # frame-only storage: the stacked obs rows and the plain tables in one launch
+                self.storage.gather_stacked(idx, m_obs, tables, use_prepared=True)
+            else:
+                gather_rows(idx, tables)
+        crit_b = m_critic
+        b = {"obs": m_obs, "critic": crit_b, "lin_vel": crit_b[:, 53:56]}
+        pk = m_packed
         for name, part in zip(("actions", "values", "returns", "logp", "adv", "mu", "sigma", "lin_vel"),
                               pk.split(self._mb_widths, dim=1)):
             b[name] = part
