@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0
 # (actions, rigid 13x13, contacts 13x3, root, dof pos / vel, torques, 144 warm-start impulses, and
 # the next post launch's 48 observation-noise normals)
 KSTEP_BYTES_PER_ENV = 828 + 1844
-PROFILE_DIR = "r6_v2"  # the committed rocprofv3 summaries of the current kernels
+PROFILE_DIR = "r6_v3"  # the committed rocprofv3 summaries of the current kernels
 PMC_SUMMARY = os.path.join(REPO, "profiles", PROFILE_DIR, "pmc_summary.json")
 
 
