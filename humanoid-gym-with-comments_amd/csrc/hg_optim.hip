@@ -313,12 +313,17 @@ __global__ void __launch_bounds__(LOSS_TPB) k_ppo_loss_rows(hg_ppo_batch Bt, int
 }
 
 constexpr int FIN_WAVES = 16;
+struct LrRule {  // the adaptive-KL rule folded into the loss's final launch (lr64 NULL: none)
+  double* lr64;
+  float* lr32;
+  double desired, lr_min, lr_max;
+};
 __global__ void __launch_bounds__(64 * FIN_WAVES) k_ppo_loss_final(const double* __restrict__ partial, int nb,
                                                                   int64_t rows, int A, const float* __restrict__ std,
                                                                   float c_v, float c_e, float c_l,
                                                                   float* __restrict__ loss_out,
                                                                   float* __restrict__ stats, int accum,
-                                                                  float* __restrict__ g_std) {
+                                                                  float* __restrict__ g_std, LrRule rule) {
   // one wave per column (columns w, w + 16, ..): lane l sums blocks l, l + 64, .. in order (all
   // its loads in flight at once), then one fixed-order wave reduction — deterministic, and the
   // column chains run side by side instead of one after another in a single block's threads
@@ -352,6 +357,15 @@ __global__ void __launch_bounds__(64 * FIN_WAVES) k_ppo_loss_final(const double*
     stats[1] = accum ? stats[1] + (float)surr : (float)surr;
     stats[2] = accum ? stats[2] + (float)lv : (float)lv;
     stats[3] = (float)kl;
+    if (rule.lr64) {
+      // the adaptive schedule on this minibatch's KL mean, as k_lr_rule reads it (float -> fp64)
+      const double k = (double)(float)kl;
+      double lr = *rule.lr64;
+      if (k > rule.desired * 2.0) lr = fmax(lr / 1.5, rule.lr_min);
+      else if (k < rule.desired / 2.0 && k > 0.0) lr = fmin(lr * 1.5, rule.lr_max);
+      *rule.lr64 = lr;
+      *rule.lr32 = (float)lr;
+    }
   }
 }
 
@@ -374,11 +388,11 @@ extern "C" int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions) {
   return ((rows + LOSS_TPB - 1) / LOSS_TPB) * (4 + (int64_t)num_actions);
 }
 
-extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float clip_lo, float clip_hi, float value_clip,
-                           int clipped_value_loss, float value_loss_coef, float entropy_coef, float lin_vel_coef,
-                           float* loss_out, float* stats_out, int accumulate_stats, float* grad_mu, float* grad_std,
-                           float* grad_value,
-                           float* grad_lin_vel, double* scratch, void* stream) {
+namespace {
+int launch_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float clip_lo, float clip_hi, float value_clip,
+                    int clipped_value_loss, float value_loss_coef, float entropy_coef, float lin_vel_coef,
+                    float* loss_out, float* stats_out, int accumulate_stats, float* grad_mu, float* grad_std,
+                    float* grad_value, float* grad_lin_vel, double* scratch, LrRule rule, void* stream) {
   if (!B || rows <= 0 || A <= 0 || A > LOSS_MAX_A || !loss_out || !stats_out || !grad_mu || !grad_std ||
       !grad_value || !grad_lin_vel || !scratch || !B->mu || !B->std || !B->value || !B->lin_vel ||
       !B->lin_vel_target || !B->actions || !B->old_logp || !B->advantages || !B->returns || !B->old_mu ||
@@ -394,8 +408,30 @@ extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float cli
   hipLaunchKernelGGL(k_ppo_loss_rows, dim3(nb), dim3(LOSS_TPB), 0, s, *B, rows, A, clip_lo, clip_hi, value_clip,
                      clipped_value_loss, c_s, c_v, c_l, grad_mu, grad_value, grad_lin_vel, scratch);
   hipLaunchKernelGGL(k_ppo_loss_final, dim3(1), dim3(64 * FIN_WAVES), 0, s, scratch, nb, rows, A, B->std, value_loss_coef,
-                     entropy_coef, lin_vel_coef, loss_out, stats_out, accumulate_stats, grad_std);
+                     entropy_coef, lin_vel_coef, loss_out, stats_out, accumulate_stats, grad_std, rule);
   return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+}  // namespace
+
+extern "C" int hg_ppo_loss(const hg_ppo_batch* B, int64_t rows, int A, float clip_lo, float clip_hi, float value_clip,
+                           int clipped_value_loss, float value_loss_coef, float entropy_coef, float lin_vel_coef,
+                           float* loss_out, float* stats_out, int accumulate_stats, float* grad_mu, float* grad_std,
+                           float* grad_value, float* grad_lin_vel, double* scratch, void* stream) {
+  return launch_ppo_loss(B, rows, A, clip_lo, clip_hi, value_clip, clipped_value_loss, value_loss_coef, entropy_coef,
+                         lin_vel_coef, loss_out, stats_out, accumulate_stats, grad_mu, grad_std, grad_value,
+                         grad_lin_vel, scratch, LrRule{nullptr, nullptr, 0.0, 0.0, 0.0}, stream);
+}
+
+extern "C" int hg_ppo_loss_lr(const hg_ppo_batch* B, int64_t rows, int A, float clip_lo, float clip_hi,
+                              float value_clip, int clipped_value_loss, float value_loss_coef, float entropy_coef,
+                              float lin_vel_coef, float* loss_out, float* stats_out, int accumulate_stats,
+                              float* grad_mu, float* grad_std, float* grad_value, float* grad_lin_vel, double* scratch,
+                              double* lr64, float* lr32, double desired_kl, double lr_min, double lr_max,
+                              void* stream) {
+  if (!lr64 || !lr32) return HG_ERR_ARG;
+  return launch_ppo_loss(B, rows, A, clip_lo, clip_hi, value_clip, clipped_value_loss, value_loss_coef, entropy_coef,
+                         lin_vel_coef, loss_out, stats_out, accumulate_stats, grad_mu, grad_std, grad_value,
+                         grad_lin_vel, scratch, LrRule{lr64, lr32, desired_kl, lr_min, lr_max}, stream);
 }
 
 extern "C" int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int A, float* grad_mu, float* grad_std,

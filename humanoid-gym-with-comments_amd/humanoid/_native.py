@@ -100,7 +100,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_post", "hg_ep_stats_slot", "hg_obs_head", "hg_obs_window_advance", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_stats_len", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
-           "hg_rollout_act", "hg_rollout_act_head", "hg_rollout_act_tail", "hg_rollout_env", "hg_gather_rows", "hg_gather_rows_ex", "hg_gather_stacked", "hg_ppo_loss", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
+           "hg_rollout_act", "hg_rollout_act_head", "hg_rollout_act_tail", "hg_rollout_env", "hg_gather_rows", "hg_gather_rows_ex", "hg_gather_stacked", "hg_ppo_loss", "hg_ppo_loss_lr", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
            "hg_mlp_act_backward", "hg_mlp_act_backward_scratch", "hg_colsum_jobs", "hg_linear_skinny_supported",
            "hg_linear_skinny_forward", "hg_linear_skinny_backward", "hg_linear_skinny_backward_scratch",
            "hg_mlp_act_backward_bf16", "hg_linear_skinny_forward_bf16", "hg_linear_skinny_backward_bf16",
@@ -226,6 +226,9 @@ def load_library(path=LIB_PATH):
     L.hg_ppo_loss.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp, ctypes.c_int] + \
         [vp] * 6
+    L.hg_ppo_loss_lr.restype = ctypes.c_int
+    L.hg_ppo_loss_lr.argtypes = L.hg_ppo_loss.argtypes[:13] + [vp] * 5 + [vp, vp, ctypes.c_double, ctypes.c_double,
+                                                                          ctypes.c_double, vp]
     L.hg_ppo_loss_scratch.restype = ctypes.c_int64
     L.hg_ppo_loss_scratch.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.hg_ppo_loss_backward.restype = ctypes.c_int

@@ -71,11 +71,18 @@ class _PPOLoss(torch.autograd.Function):
         g_p = torch.empty(rows, 3, dtype=torch.float32, device=dev)
         scratch = torch.empty(int(L.hg_ppo_loss_scratch(rows, A)), dtype=torch.float64, device=dev)
         clip, vcoef, ecoef, lcoef, clipped = params[:5]
+        lr_rule = params[7]
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        rc = L.hg_ppo_loss(ctypes.byref(b), rows, A, float(1.0 - clip), float(1.0 + clip), float(clip),
-                           int(bool(clipped)), float(vcoef), float(ecoef), float(lcoef), loss.data_ptr(),
-                           stats.data_ptr(), int(bool(accumulate)), g_mu.data_ptr(), g_std.data_ptr(), g_v.data_ptr(), g_p.data_ptr(),
-                           scratch.data_ptr(), s)
+        head = (ctypes.byref(b), rows, A, float(1.0 - clip), float(1.0 + clip), float(clip), int(bool(clipped)),
+                float(vcoef), float(ecoef), float(lcoef), loss.data_ptr(), stats.data_ptr(), int(bool(accumulate)),
+                g_mu.data_ptr(), g_std.data_ptr(), g_v.data_ptr(), g_p.data_ptr(), scratch.data_ptr())
+        if lr_rule is None:
+            rc = L.hg_ppo_loss(*head, s)
+        else:
+            # the adaptive-KL rule on this minibatch's KL mean in the same launch (hg_ppo_loss_lr)
+            lr64, lr32, desired, lr_min, lr_max = lr_rule
+            rc = L.hg_ppo_loss_lr(*head, lr64.data_ptr(), lr32.data_ptr(), float(desired), float(lr_min),
+                                  float(lr_max), s)
         if rc != 0:
             raise RuntimeError(f"hg_ppo_loss failed ({rc})")
         ctx.save_for_backward(g_mu, g_std, g_v, g_p)
@@ -125,7 +132,7 @@ def release_unit_seed(t):
 
 
 def ppo_loss(mu, std, value, lin_vel, data, clip_param, value_loss_coef, entropy_coef, lin_vel_coef,
-             use_clipped_value_loss=True, stats_out=None, accumulate=False):
+             use_clipped_value_loss=True, stats_out=None, accumulate=False, lr_rule=None):
     """(loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean] (detached).
     With ``stats_out`` (a float32 [4] device buffer) the statistics are written there instead —
     ``accumulate`` adds the three losses to its first entries — and only the loss is returned.
@@ -133,7 +140,9 @@ def ppo_loss(mu, std, value, lin_vel, data, clip_param, value_loss_coef, entropy
     ``mu`` [B, A] actor mean, ``std`` [A] the policy's std parameter, ``value`` [B, 1] critic
     output, ``lin_vel`` [B, 3] lin-vel estimate; ``data``: dict of the minibatch's stored
     tensors ``actions``, ``old_logp``, ``advantages``, ``target_values``, ``returns``,
-    ``old_mu``, ``old_sigma`` and ``lin_vel_target`` (row views with unit column stride)."""
+    ``old_mu``, ``old_sigma`` and ``lin_vel_target`` (row views with unit column stride).
+    ``lr_rule`` = (lr64 [1] float64, lr32 [1] float32, desired_kl, lr_min, lr_max) device scalars and
+    bounds: the adaptive schedule's rule applied to this minibatch's KL mean in the same launch."""
     return _PPOLoss.apply(mu, std, value, lin_vel, data,
                           (clip_param, value_loss_coef, entropy_coef, lin_vel_coef, use_clipped_value_loss,
-                           stats_out, accumulate))
+                           stats_out, accumulate, lr_rule))

@@ -36,6 +36,8 @@ from .rollout_storage import RolloutStorage, gather_rows
 
 # the actor's 12 x 128 output layer fused into the rollout's sampling launch (hg_rollout_act_head)
 HEAD_FUSED = os.environ.get("HG_HEAD_FUSED", "1") != "0"
+# the adaptive-KL learning-rate rule inside the loss's final launch (hg_ppo_loss_lr), one process
+FUSED_LR_RULE = os.environ.get("HG_FUSED_LR_RULE", "1") != "0"
 
 
 def _world():
@@ -453,7 +455,7 @@ class PPO:
         return self._on_device and self.use_fused_loss and not self.sym_loss
 
     def _losses_fused(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b,
-                      old_mu_b, old_sigma_b, stats_out=None):
+                      old_mu_b, old_sigma_b, stats_out=None, lr_rule=None):
         """The loss of _losses (and the adaptive schedule's KL mean) from the three network
         outputs in one fused HIP forward launch pair and one backward launch (hg_loss.py).
         Returns (loss, stats) with stats = [value_loss, surrogate_loss, lin_vel_loss, kl_mean]."""
@@ -480,7 +482,7 @@ class PPO:
                 "lin_vel_target": lin_vel_b if lin_vel_b.dtype == torch.float32 else lin_vel_b.float()}
         return ppo_loss(mu, ac.std, value_b, est_lin_vel, data, self.clip_param, self.value_loss_coef,
                         self.entropy_coef, self.base_lin_vel_coef, self.use_clipped_value_loss,
-                        stats_out=stats_out, accumulate=stats_out is not None)
+                        stats_out=stats_out, accumulate=stats_out is not None, lr_rule=lr_rule)
 
     def _losses(self, obs_b, critic_b, lin_vel_b, actions_b, target_values_b, adv_b, returns_b, old_logp_b):
         """Minibatch loss (ppo.py:155-214).  The reference calls actor_critic.act() here and
@@ -755,7 +757,7 @@ class PPO:
         if self._fused_loss:
             loss = self._losses_fused(b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"],
                                       b["adv"], b["returns"], b["logp"], b["mu"], b["sigma"],
-                                      stats_out=self._stats4)
+                                      stats_out=self._stats4, lr_rule=self._fused_lr_rule())
         else:
             loss, value_loss, surrogate_loss, lin_vel_loss, _ = self._losses(
                 b["obs"], b["critic"], b["lin_vel"], b["actions"], b["values"], b["adv"], b["returns"],
@@ -769,6 +771,14 @@ class PPO:
         # d loss / d loss = 1 from a persistent tensor: no fill launch per minibatch in the graph
         loss.backward(gradient=self._one_grad)
 
+    def _fused_lr_rule(self):
+        """The adaptive rule's device state for hg_ppo_loss_lr (the rule inside the loss launch):
+        one process with the device learning rate; None otherwise (data parallel: the rule needs
+        the all-reduced KL mean, _mb_step applies it)."""
+        if FUSED_LR_RULE and self._adaptive and not self._dp and self._lr_t is not None and self._fused_loss:
+            return (self._lr_t, self._lr_f32, self.desired_kl, 1e-5, 1e-2)
+        return None
+
     def _mb_step(self):
         """Captured minibatch step: adaptive learning rate, global-norm clip, fused Adam."""
         kl = self._kl
@@ -776,7 +786,7 @@ class PPO:
             # gradients and the KL mean were summed over ranks in ONE all-reduce
             self._flat_grad.div_(self.world_size)
             kl = self._kl_slot
-        if self._adaptive:
+        if self._adaptive and self._fused_lr_rule() is None:  # else applied by the loss launch
             self._lr_rule_device(kl)
         self._clip_and_step()
 

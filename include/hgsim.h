@@ -415,6 +415,16 @@ int hg_ppo_loss(const hg_ppo_batch* batch, int64_t rows, int num_actions, float 
                 float* grad_std,
                 float* grad_value, float* grad_lin_vel, double* scratch /* >= hg_ppo_loss_scratch() doubles */,
                 void* stream);
+/* hg_ppo_loss with the adaptive-KL learning-rate rule (hg_kl_lr_rule, reference ppo.py:162-176)
+ * applied in its final launch to this minibatch's KL mean (stats_out[3], read as hg_kl_lr_rule
+ * reads it): lr64 / lr32 updated before the optimizer step of the same minibatch, one launch
+ * fewer.  Single-process form: a data-parallel update applies hg_kl_lr_rule to the all-reduced
+ * KL mean instead. */
+int hg_ppo_loss_lr(const hg_ppo_batch* batch, int64_t rows, int num_actions, float clip_lo, float clip_hi,
+                   float value_clip, int clipped_value_loss, float value_loss_coef, float entropy_coef,
+                   float lin_vel_coef, float* loss_out, float* stats_out, int accumulate_stats, float* grad_mu,
+                   float* grad_std, float* grad_value, float* grad_lin_vel, double* scratch, double* lr64,
+                   float* lr32, double desired_kl, double lr_min, double lr_max, void* stream);
 int64_t hg_ppo_loss_scratch(int64_t rows, int num_actions);
 int hg_ppo_loss_backward(const float* grad_loss, int64_t rows, int num_actions, float* grad_mu, float* grad_std,
                          float* grad_value, float* grad_lin_vel, void* stream);
