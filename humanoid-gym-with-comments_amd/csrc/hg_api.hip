@@ -13,7 +13,7 @@ extern "C" int hg_launch_step(const HgState* S, const hg_cfg* hcfg, const float*
                                hipStream_t stream);
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
                               float* frame_obs, float* frame_priv, HgWindow obs, HgWindow priv, float inv_len_s,
-                              int ep_slot, hipStream_t stream);
+                              int ep_slot, HgSink sink, hipStream_t stream);
 
 namespace {
 
@@ -118,6 +118,7 @@ struct Sim {
   int head;    // first window slot of the current observation stack
   uint64_t post_seq = 0;  // post/reset launches so far: EP_STATS ring row of the next one
   int ep_slot = 0;        // ring row written by the latest one
+  HgSink sink{nullptr, nullptr, nullptr};  // one-shot: consumed by the next hg_post
   std::string err;
 };
 
@@ -342,8 +343,11 @@ static int do_post(Sim* s, uint64_t counter, int mode, const uint8_t* mask, void
   const HgWindow wp = {(float*)(s->arena + s->L.priv_buf),
                        (int64_t)win_frames(s->cfg.c_frame_stack, &s->cfg) * HG_PRIV1, HG_PRIV1, s->cfg.c_frame_stack,
                        head, shift ? old + 1 : -1};
+  // a step's post launch takes the pending rollout sink (reset launches leave it pending)
+  const HgSink sink = mode == 0 ? s->sink : HgSink{nullptr, nullptr, nullptr};
+  if (mode == 0) s->sink = HgSink{nullptr, nullptr, nullptr};
   int rc = hg_launch_post(&s->S, &s->cfg, counter, mode, mask, (float*)(s->arena + s->L.frame_obs),
-                          (float*)(s->arena + s->L.frame_priv), wo, wp, inv_len_s, slot, (hipStream_t)stream);
+                          (float*)(s->arena + s->L.frame_priv), wo, wp, inv_len_s, slot, sink, (hipStream_t)stream);
   if (rc != 0) return fail(s, HG_ERR_HIP, "k_post launch failed");
   s->ep_slot = slot;
   s->post_seq++;
@@ -364,6 +368,13 @@ int hg_obs_window_advance(void* sim) {
 int hg_ep_stats_slot(void* sim) {
   Sim* s = (Sim*)sim;
   return s ? s->ep_slot : -1;
+}
+
+int hg_set_rollout_sink(void* sim, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out) {
+  Sim* s = (Sim*)sim;
+  if (!s || (!rewards_out) != (!dones_out) || (time_outs_out && !rewards_out)) return HG_ERR_ARG;
+  s->sink = HgSink{rewards_out, dones_out, time_outs_out};
+  return HG_OK;
 }
 
 int hg_post(void* sim, uint64_t common_step_counter, void* stream) {

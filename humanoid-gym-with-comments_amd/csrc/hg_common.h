@@ -66,6 +66,15 @@ struct HgState {
   const hg_model* model;  // device copy
 };
 
+// the rollout-storage slot a step's post launch also fills (hg_set_rollout_sink): rewards [n] f32,
+// dones [n] u8 and (optional) time-out flags [n] u8 — what hg_rollout_env writes with the value
+// bootstrap deferred; all NULL: no sink
+struct HgSink {
+  float* rew;
+  uint8_t* dones;
+  uint8_t* time_outs;
+};
+
 // one observation history window table for the post launch: row e = win + e * rowlen, frame slots of
 // `width` floats; this launch writes the new frame into slot head + frames - 1, zeroes slots
 // head .. head + frames - 2 of reset envs and, when shift_src >= 0, first moves slots

@@ -1131,12 +1131,25 @@ __global__ void __launch_bounds__(64 * WIN_ROWS) k_window_stats(HgWindow A, HgWi
                                                       const uint8_t* __restrict__ reset, int n, float* ep_stats,
                                                       float inv_len_s, int ring_slot,
                                                       const int32_t* __restrict__ env_rows,
-                                                      int32_t* __restrict__ env_order, int nsort) {
+                                                      int32_t* __restrict__ env_order, int nsort, HgSink sink,
+                                                      const float* __restrict__ rew,
+                                                      const uint8_t* __restrict__ time_out, int nsink) {
   static_assert(64 * WIN_ROWS == HG_ORD_T, "the order blocks use the window block's threads");
   // blocks 0 .. nsort - 1: the next K_step's env order (hg_common.h), first so that they start
   // with the launch and run beside the window rows
   if ((int)blockIdx.x < nsort) {
     hg_env_order_block(env_rows, env_order, n, blockIdx.x);
+    return;
+  }
+  // blocks nsort .. nsort + nsink - 1: the step's rewards / dones / time-outs into the rollout
+  // storage slot (hg_set_rollout_sink; hg_rollout_env's writes with the bootstrap deferred)
+  if ((int)blockIdx.x < nsort + nsink) {
+    const int e = ((int)blockIdx.x - nsort) * (64 * WIN_ROWS) + (int)threadIdx.x;
+    if (e < n) {
+      sink.rew[e] = rew[e];
+      sink.dones[e] = reset[e];
+      if (sink.time_outs) sink.time_outs[e] = time_out[e];
+    }
     return;
   }
   if (blockIdx.x == gridDim.x - 1) {
@@ -1157,7 +1170,7 @@ __global__ void __launch_bounds__(64 * WIN_ROWS) k_window_stats(HgWindow A, HgWi
     return;
   }
   // one wave per (env, table) row, WIN_ROWS rows per block
-  const int b = (blockIdx.x - nsort) * WIN_ROWS + (threadIdx.x >> 6);
+  const int b = (blockIdx.x - nsort - nsink) * WIN_ROWS + (threadIdx.x >> 6);
   if (b >= 2 * n) return;
   const int lane = threadIdx.x & 63;
   const bool a = b < n;
@@ -1179,7 +1192,7 @@ __global__ void __launch_bounds__(64 * WIN_ROWS) k_window_stats(HgWindow A, HgWi
 
 extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t counter, int mode, const uint8_t* mask,
                               float* frame_obs, float* frame_priv, HgWindow obs, HgWindow priv, float inv_len_s,
-                              int ep_slot, hipStream_t stream) {
+                              int ep_slot, HgSink sink, hipStream_t stream) {
   const int n = S->n;
   if (mode == 0)
     hipLaunchKernelGGL(k_post_step, dim3((n + PEB - 1) / PEB), dim3(64 * PWAVES), 0, stream, *S, *hcfg, counter,
@@ -1190,8 +1203,10 @@ extern "C" int hg_launch_post(const HgState* S, const hg_cfg* hcfg, uint64_t cou
   // the env-order blocks (K_step's wave balancing), WIN_ROWS (env, table) rows per block, the
   // statistics block
   const int nsort = S->balance ? 8 : 0;
-  const int g = nsort + (2 * n + WIN_ROWS - 1) / WIN_ROWS + 1;
+  const int nsink = sink.rew ? (n + 64 * WIN_ROWS - 1) / (64 * WIN_ROWS) : 0;
+  const int g = nsort + nsink + (2 * n + WIN_ROWS - 1) / WIN_ROWS + 1;
   hipLaunchKernelGGL(k_window_stats, dim3(g), dim3(64 * WIN_ROWS), 0, stream, obs, priv, frame_obs, frame_priv,
-                     S->reset_buf, n, S->ep_stats, inv_len_s, ep_slot, S->env_rows, S->env_order, nsort);
+                     S->reset_buf, n, S->ep_stats, inv_len_s, ep_slot, S->env_rows, S->env_order, nsort, sink, S->rew,
+                     S->time_out, nsink);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -97,7 +97,7 @@ T = {name: i for i, name in enumerate(TENSOR_IDS)}
 
 # every symbol include/hgsim.h declares (checked by tests/test_boundary.py)
 EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_tensor", "hg_step",
-           "hg_post", "hg_ep_stats_slot", "hg_obs_head", "hg_obs_window_advance", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
+           "hg_post", "hg_set_rollout_sink", "hg_ep_stats_slot", "hg_obs_head", "hg_obs_window_advance", "hg_update_cfg", "hg_reset_masked", "hg_set_dof_state_indexed", "hg_set_root_state_indexed",
            "hg_set_root_state", "hg_set_env_props",
            "hg_measure_heights", "hg_gae_scan", "hg_gae_stats_len", "hg_gae_normalize", "hg_adam_step", "hg_adam_chunk", "hg_kl_mean", "hg_kl_lr_rule",
            "hg_rollout_act", "hg_rollout_act_head", "hg_rollout_act_tail", "hg_rollout_env", "hg_gather_rows", "hg_gather_rows_ex", "hg_gather_stacked", "hg_ppo_loss", "hg_ppo_loss_lr", "hg_ppo_loss_scratch", "hg_ppo_loss_backward",
@@ -170,6 +170,8 @@ def load_library(path=LIB_PATH):
     L.hg_step.argtypes = [vp, vp, ctypes.c_uint64, vp]
     L.hg_post.restype = ctypes.c_int
     L.hg_post.argtypes = [vp, ctypes.c_uint64, vp]
+    L.hg_set_rollout_sink.restype = ctypes.c_int
+    L.hg_set_rollout_sink.argtypes = [vp, vp, vp, vp]
     L.hg_update_cfg.restype = ctypes.c_int
     L.hg_update_cfg.argtypes = [vp, ctypes.POINTER(HgCfg), vp]
     L.hg_reset_masked.restype = ctypes.c_int

@@ -125,9 +125,14 @@ class OnPolicyRunner:
                 # phase times from HIP events: no host synchronisation between collection and learning
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 ev[0].record()
+            sink_ok = hasattr(self.env, "set_rollout_sink") and hasattr(self.alg, "rollout_sink")
             with torch.inference_mode():
                 for step in range(self.num_steps_per_env):
                     actions = self.alg.act(obs, critic_obs)
+                    if sink_ok:
+                        sink = self.alg.rollout_sink()
+                        if sink is not None:  # the env's post launch fills the storage slot
+                            self.env.set_rollout_sink(*sink)
                     obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
                     critic_obs = privileged_obs if privileged_obs is not None else obs
                     obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)

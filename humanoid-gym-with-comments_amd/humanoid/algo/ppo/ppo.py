@@ -36,6 +36,8 @@ from .rollout_storage import RolloutStorage, gather_rows
 
 # the actor's 12 x 128 output layer fused into the rollout's sampling launch (hg_rollout_act_head)
 HEAD_FUSED = os.environ.get("HG_HEAD_FUSED", "1") != "0"
+# the env's post launch writes the rollout slot's rewards / dones / time-outs (set_rollout_sink)
+ROLLOUT_SINK = os.environ.get("HG_ROLLOUT_SINK", "1") != "0"
 # the adaptive-KL learning-rate rule inside the loss's final launch (hg_ppo_loss_lr), one process
 FUSED_LR_RULE = os.environ.get("HG_FUSED_LR_RULE", "1") != "0"
 
@@ -326,6 +328,20 @@ class PPO:
                                  else critic_obs)
         return t.actions
 
+    def rollout_sink(self):
+        """(rewards, dones, time_outs) views of the rollout storage slot the current transition
+        fills, for an env that writes them inside its step (set_rollout_sink: the post launch fills
+        the slot, process_env_step then launches nothing); None unless the fused device rollout
+        with the deferred value pass is active."""
+        t = self.transition
+        st = self.storage
+        if not (ROLLOUT_SINK and getattr(t, "fused_slot", None) is not None and self._defer_values()):
+            return None
+        if st.time_outs is None:
+            st.time_outs = torch.zeros_like(st.dones)
+        k = t.fused_slot
+        return st.rewards[k].view(-1), st.dones[k].view(-1), st.time_outs[k].view(-1)
+
     def process_env_step(self, rewards, dones, infos):
         t = self.transition
         if getattr(t, "fused_slot", None) is not None:
@@ -344,11 +360,15 @@ class PPO:
                 # time-out bootstrap deferred to the batched value pass in compute_returns
                 if st.time_outs is None:
                     st.time_outs = torch.zeros_like(st.dones)
-                if "p_time_outs" not in sl:
-                    sl["p_time_outs"] = ctypes.c_void_p(st.time_outs[k].data_ptr())
-                N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, None, r.shape[0],
-                                               ctypes.c_float(self.gamma), sl["p_rewards"], sl["p_dones"],
-                                               sl["p_time_outs"], s))
+                sink = infos.get("rollout_sink")
+                written = (sink is not None and sink[0].data_ptr() == sl["rewards"].data_ptr()
+                           and sink[2] is not None and sink[2].data_ptr() == st.time_outs[k].data_ptr())
+                if not written:  # else the env's post launch already filled this slot
+                    if "p_time_outs" not in sl:
+                        sl["p_time_outs"] = ctypes.c_void_p(st.time_outs[k].data_ptr())
+                    N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, None, r.shape[0],
+                                                   ctypes.c_float(self.gamma), sl["p_rewards"], sl["p_dones"],
+                                                   sl["p_time_outs"], s))
                 st.values_deferred = True
             else:
                 N.check(N.lib().hg_rollout_env(p(r), p(d), p(to) if to is not None else None, sl["p_values"],

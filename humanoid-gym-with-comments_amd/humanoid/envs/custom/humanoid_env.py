@@ -527,11 +527,34 @@ class XBotLFreeEnv(BaseTask):
             N.check(self.hg.hg_measure_heights(self.sim, ctypes.c_void_p(self._height_xy.data_ptr()),
                                                self.num_height_points, ctypes.c_void_p(self.measured_heights.data_ptr()),
                                                s), self.sim)
+        sink, self._rollout_sink = self._rollout_sink, None
+        if sink is not None:
+            # this step's post launch also writes the rollout storage slot (hg_set_rollout_sink)
+            vp = ctypes.c_void_p
+            N.check(self.hg.hg_set_rollout_sink(self.sim, *[vp(t.data_ptr()) if t is not None else None
+                                                             for t in sink]), self.sim)
         N.check(self.hg.hg_post(self.sim, ctypes.c_uint64(self.common_step_counter), s), self.sim)
         if kt is not None:
             kt.stop("k_post")
         self._publish_extras()
+        if sink is not None:
+            self.extras["rollout_sink"] = sink  # the slot tensors this step's post launch filled
         return self.get_observations(), self.get_privileged_observations(), self.rew_buf, self.reset_buf, self.extras
+
+    _rollout_sink = None
+
+    def set_rollout_sink(self, rewards, dones, time_outs=None):
+        """The next step() also writes its rewards (float32), reset flags and time-out flags (uint8)
+        into these [num_envs] device tensors — a PPO rollout-storage slot — inside its post launch
+        (hg_set_rollout_sink), so the algorithm's storage write needs no launch of its own.  The
+        step reports the tensors in extras["rollout_sink"]."""
+        checks = [(rewards, torch.float32), (dones, torch.uint8)] + ([(time_outs, torch.uint8)] if time_outs is not None else [])
+        for t, dt in checks:
+            if (t is None or t.dtype != dt or t.device != self.device or t.numel() != self.num_envs
+                    or not t.is_contiguous()):
+                raise ValueError("set_rollout_sink: contiguous [num_envs] device tensors (float32 rewards, "
+                                 "uint8 dones / time-outs)")
+        self._rollout_sink = (rewards, dones, time_outs)
 
     def get_observations(self):
         return self.obs_buf.clone() if self.stable_observations else _live(self.obs_buf)

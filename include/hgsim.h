@@ -209,6 +209,13 @@ int hg_step(void* sim, const float* actions, uint64_t step_counter, void* stream
 /* ring row of HG_T_EP_STATS_RING written by the latest hg_post / hg_reset_masked launch (host-side
  * bookkeeping, no device access) */
 int hg_ep_stats_slot(void* sim);
+/* The rollout-storage slot the NEXT hg_post also fills: rewards_out[e] = the step's reward,
+ * dones_out[e] = its reset flag, time_outs_out[e] (optional) = its time-out flag, e < num_envs —
+ * what hg_rollout_env writes with the value bootstrap deferred (values == NULL), in extra blocks
+ * of the post launch instead of a launch of its own (PPO.process_env_step, reference
+ * ppo.py:127-138, then skips it).  One-shot: consumed by the next hg_post (hg_reset_masked leaves
+ * it pending); all NULL clears it.  float32 / uint8 device arrays. */
+int hg_set_rollout_sink(void* sim, float* rewards_out, uint8_t* dones_out, uint8_t* time_outs_out);
 int hg_post(void* sim, uint64_t common_step_counter, void* stream);
 /* first frame slot h of the current observation stacks in the HG_T_OBS_BUF / HG_T_PRIV_BUF
  * windows (host-side bookkeeping): every hg_post / hg_reset_masked advances it by one and writes

@@ -1026,6 +1026,59 @@ def test_fused_tail_matches_head_and_two_launches(n):
         torch.testing.assert_close(out["tail"]["mu"], ac.actor(obs), rtol=1e-5, atol=1e-5)
 
 
+def test_rollout_sink_matches_the_env_launch():
+    """With the rollout sink (the env's post launch writes the storage slot's rewards, dones and
+    time-outs: hg_set_rollout_sink) a collection leaves bit-for-bit the storage the separate
+    hg_rollout_env launch leaves, on short episodes (resets and time-outs within the rollout); and
+    the slot equals the env's own step outputs."""
+    _need_gpu()
+    from humanoid.algo.ppo import ActorCritic, PPO
+    from humanoid.algo.ppo import ppo as ppo_mod
+    from humanoid.envs import XBotLCfg
+    from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
+    from humanoid.utils.helpers import SimParams
+    T, n = 12, 128
+    out = {}
+    try:
+        for mode in (False, True):
+            ppo_mod.ROLLOUT_SINK = mode
+            cfg = XBotLCfg()
+            cfg.env.num_envs = n
+            cfg.env.episode_length_s = 0.05  # 5 policy steps: time-outs inside the rollout
+            cfg.seed = 3
+            env = XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
+            torch.manual_seed(4)
+            ac = ActorCritic(705, 219, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[768, 256, 128],
+                             init_noise_std=1.0)
+            ppo = PPO(ac, device="cuda:0")
+            ppo._rollout_seed = 99
+            ppo.init_storage(n, T, [705], [219], [12])
+            obs, cobs = env.get_observations(), env.get_privileged_observations()
+            used = 0
+            with torch.inference_mode():
+                for _ in range(T):
+                    a = ppo.act(obs, cobs)
+                    sink = ppo.rollout_sink()
+                    assert (sink is not None) == mode
+                    if sink is not None:
+                        env.set_rollout_sink(*sink)
+                    obs, cobs, rew, dones, infos = env.step(a)
+                    used += "rollout_sink" in infos
+                    ppo.process_env_step(rew, dones, infos)
+                    k = ppo.storage.step - 1
+                    st = ppo.storage
+                    assert torch.equal(st.rewards[k, :, 0], rew) and torch.equal(st.dones[k, :, 0], dones.to(torch.uint8))
+                    assert torch.equal(st.time_outs[k, :, 0], infos["time_outs"].to(torch.uint8))
+            assert used == (T if mode else 0)
+            st = ppo.storage
+            out[mode] = (st.rewards.clone(), st.dones.clone(), st.time_outs.clone())
+            assert st.time_outs.any() and st.dones.any()
+    finally:
+        ppo_mod.ROLLOUT_SINK = True
+    for a, b in zip(out[True], out[False]):
+        assert torch.equal(a, b)
+
+
 def test_set_root_state_and_env_props(env):
     """hg_set_root_state (all envs, clears contact warm-starts) and hg_set_env_props (DR
     friction / base mass) through the C ABI."""
