@@ -606,7 +606,8 @@ __device__ __forceinline__ void gemm_x6_body(const GemmX6Args& xa) {
   constexpr bool AKC = MODE != 2, BKC = MODE == 0 || MODE == 3 || MODE == 4;
   constexpr int SCA = (AKC || (IMG & 2)) ? 0 : X6StageT<BM, KG, 64 * WGM * WGN>::SCRATCH;
   constexpr bool AIMG = (IMG & 2) != 0, BIMG = (IMG & 1) != 0;
-  static_assert(IMG == 0 || MODE == 0 || MODE == 1 || MODE == 2, "images: forward, input-grad, split-K epilogues");
+  static_assert(IMG == 0 || MODE == 0 || MODE == 1 || MODE == 2 || (MODE == 4 && IMG == 1),
+                "images: forward, input-grad, split-K epilogues (the split-K forward: B only)");
   static_assert(MODE != 2 || IMG == 0 || IMG == 3, "split-K: both operands as images");
   constexpr int SCB = (BKC || BIMG) ? 0 : X6StageT<BN, KG, 64 * WGM * WGN>::SCRATCH;
   constexpr int SCS = (SCA + SCB + 3) / 4;  // scratch in 16-byte slots, after the two stages
@@ -891,7 +892,7 @@ int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStrea
   g.tiles_n = (g.N + BN - 1) / BN;
   const int64_t tiles_m = (g.M + BM - 1) / BM;
   g.tiles = tiles_m * g.tiles_n;
-  if (mode != 2) xa.slices = 1;
+  if (mode != 2 && mode != 4) xa.slices = 1;
   if (g.tiles * xa.slices > 0x7fffffff) return HG_ERR_ARG;
   const dim3 grid((unsigned)(g.tiles * xa.slices)), block(64 * WGM * WGN);
 #define HG_X6I(V, MD, E, I)                                                                                      \
@@ -901,6 +902,9 @@ int launch_x6_img(int mode, int img, GemmX6Args xa, bool vec, bool elu, hipStrea
   } while (0)
   if (mode == 2) {
     HG_X6I(false, 2, false, 3);
+  } else if (mode == 4) {  // the split-K forward's slices with W as the image
+    if (vec) HG_X6I(true, 4, false, 1);
+    else HG_X6I(false, 4, false, 1);
   } else if (img == 3) {
     if (mode == 0) {
       if (elu) HG_X6I(false, 0, true, 3);
@@ -1523,6 +1527,27 @@ __global__ void __launch_bounds__(256) k_splitk_finish(const float* __restrict__
     }
   }
 }
+
+// the fixed-order sum of the slices + bias (+ ELU): one thread per 4 columns of a row
+int splitk_finish(const float* ws, const float* bias, float* C, int64_t ldc, int64_t M, int N, int slices, bool elu,
+                  hipStream_t s) {
+  const int64_t threads = M * ((N + 3) / 4);
+  const bool fvec = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)bias % 16 == 0;
+  const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+#define HG_FIN(E, SC) hipLaunchKernelGGL((k_splitk_finish<E, SC>), grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, \
+                                         slices, fvec)
+  if (elu) {
+    if (slices == 4) HG_FIN(true, 4);
+    else if (slices == 2) HG_FIN(true, 2);
+    else HG_FIN(true, 0);
+  } else {
+    if (slices == 4) HG_FIN(false, 4);
+    else if (slices == 2) HG_FIN(false, 2);
+    else HG_FIN(false, 0);
+  }
+#undef HG_FIN
+  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
 }  // namespace
 
 extern "C" int64_t hg_gemm_splitk_kslice(int K, int slices) {
@@ -1562,19 +1587,32 @@ extern "C" int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, i
     default: rc = launch_x6<64, 256, 2, 4, 1>(md, xa, vec, elu, s); break;
   }
   if (rc != HG_OK) return rc;
-  const bool fvec = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0 && (uintptr_t)bias % 16 == 0;
-  const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
-#define HG_FIN(E, SC) hipLaunchKernelGGL((k_splitk_finish<E, SC>), grid, block, 0, s, ws, M * (int64_t)N, bias, C, ldc, M, N, \
-                                         slices, fvec)
-  if (elu) {
-    if (slices == 4) HG_FIN(true, 4);
-    else if (slices == 2) HG_FIN(true, 2);
-    else HG_FIN(true, 0);
-  } else {
-    if (slices == 4) HG_FIN(false, 4);
-    else if (slices == 2) HG_FIN(false, 2);
-    else HG_FIN(false, 0);
-  }
-#undef HG_FIN
-  return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+  return splitk_finish(ws, bias, C, ldc, M, N, slices, elu, s);
+}
+
+// The same split-K forward with W as the operand image hg_gemm_x6_image_jobs builds (trans 0, N
+// rows, K deep): the slices DMA B's three planes into LDS instead of splitting W per block.  The
+// products and their order are those of hg_gemm_f32_splitk (bitwise the same output).  Tiles with
+// one 16-deep chunk per stage only (a slice's chunks then never reach past the image's K).
+extern "C" int hg_gemm_f32_splitk_img(const float* A, int64_t lda, const void* Bimg, int64_t bimg_bytes,
+                                      const float* bias, float* C, int64_t ldc, float* ws, int64_t ws_floats,
+                                      int64_t M, int N, int K, int act, int tile, int slices, void* stream) {
+  if (!A || !Bimg || !bias || !C || !ws || M <= 0 || N <= 0 || K <= 0 || lda < K || ldc < N || act < 0 || act > 1 ||
+      tile < 19 || tile > NTILES_IMG || tile == 24 || tile == 26 || tile == 29 || slices < 2 || slices > 16)
+    return HG_ERR_ARG;
+  if (bimg_bytes != hg_gemm_x6_image_bytes(N, K)) return HG_ERR_ARG;
+  const int64_t kslice = hg_gemm_splitk_kslice(K, slices);
+  if ((slices - 1) * kslice >= K) return HG_ERR_ARG;
+  if (ws_floats < slices * M * (int64_t)N) return HG_ERR_ARG;
+  if ((uintptr_t)A % 4 || (uintptr_t)Bimg % 16 || (uintptr_t)C % 4 || (uintptr_t)bias % 4 || (uintptr_t)ws % 16)
+    return HG_ERR_ARG;
+  if ((M * ((N + 3) / 4) + 255) / 256 > 0x7fffffff) return HG_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  GemmArgs g{A, lda, reinterpret_cast<const float*>(Bimg), img_rows(N) * 2, nullptr, nullptr, 0, ws, N, nullptr, M, N,
+             K, 0, 0};
+  GemmX6Args xa{g, kslice, M * (int64_t)N, slices};
+  const bool vec = lda % 4 == 0 && (uintptr_t)A % 16 == 0;
+  const int rc = x6_img_dispatch(tile, 4, 1, xa, vec, false, s);
+  if (rc != HG_OK) return rc;
+  return splitk_finish(ws, bias, C, ldc, M, N, slices, act == 1, s);
 }

@@ -106,7 +106,7 @@ EXPORTS = ["hg_arena_bytes", "hg_create", "hg_destroy", "hg_last_error", "hg_ten
            "hg_mlp_act_backward_bf16", "hg_linear_skinny_forward_bf16", "hg_linear_skinny_backward_bf16",
            "hg_cast_bf16_jobs", "hg_linear_act_forward", "hg_linear_act_tile", "hg_gemm_f32", "hg_gemm_tile",
            "hg_gemm_colpart_rows", "hg_gemm_f32_wgrad", "hg_gemm_x6_image_bytes", "hg_gemm_x6_image_jobs", "hg_gemm_x6_image_jobs_pitched", "hg_gemm_wgrad_img",
-           "hg_gemm_f32_img", "hg_gemm_f32_img_split", "hg_gemm_splitk_kslice", "hg_gemm_f32_splitk", "hg_linear_skinny_backward_act", "hg_linear_skinny_colpart_rows", "hg_version",
+           "hg_gemm_f32_img", "hg_gemm_f32_img_split", "hg_gemm_splitk_kslice", "hg_gemm_f32_splitk", "hg_gemm_f32_splitk_img", "hg_linear_skinny_backward_act", "hg_linear_skinny_colpart_rows", "hg_version",
            "hg_source_hash"]
 
 _LIB = None
@@ -295,6 +295,10 @@ def load_library(path=LIB_PATH):
     L.hg_gemm_f32_splitk.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp, ctypes.c_int64,
                                      ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      vp]
+    L.hg_gemm_f32_splitk_img.restype = ctypes.c_int
+    L.hg_gemm_f32_splitk_img.argtypes = [vp, ctypes.c_int64, vp, ctypes.c_int64, vp, vp, ctypes.c_int64, vp,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, vp]
     L.hg_gemm_f32_img.restype = ctypes.c_int
     L.hg_gemm_f32_img.argtypes = [ctypes.c_int, vp, ctypes.c_int64, vp, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int64,
                                   vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,

@@ -590,6 +590,13 @@ int64_t hg_gemm_splitk_kslice(int K, int slices);
 int hg_gemm_f32_splitk(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, float* C,
                        int64_t ldc, float* ws, int64_t ws_floats, int64_t M, int N, int K, int act, int tile,
                        int slices, void* stream);
+/* hg_gemm_f32_splitk with W as its operand image (Bimg: hg_gemm_x6_image_jobs trans 0 of W [N, K],
+ * bimg_bytes = hg_gemm_x6_image_bytes(N, K)): the slices read W's bf16 planes instead of splitting
+ * W per block; bitwise the same C as hg_gemm_f32_splitk on the same tile.  Tiles 19..32 except 24,
+ * 26, 29 (one 16-deep chunk per stage).  The rollout builds the image once per weight update. */
+int hg_gemm_f32_splitk_img(const float* A, int64_t lda, const void* Bimg, int64_t bimg_bytes, const float* bias,
+                           float* C, int64_t ldc, float* ws, int64_t ws_floats, int64_t M, int N, int K, int act,
+                           int tile, int slices, void* stream);
 
 /* library build info; hg_source_hash: first 16 hex digits of the sha256 of the sources the
  * library was built from (the Makefile's SRCS, csrc/hg_common.h, include/hgsim.h, concatenated) */

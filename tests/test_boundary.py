@@ -163,3 +163,29 @@ def test_splitk_forward_rejects_bad_arguments():
     assert call(bias=None) != 0
     assert call(ldc=500) != 0
     assert call(act=2) != 0
+
+
+def test_splitk_img_forward_rejects_bad_arguments():
+    """hg_gemm_f32_splitk_img refuses before any device work: an image built for another shape, the
+    tiles with two chunks per stage (24, 26, 29), f32 tiles, an empty slice, a short workspace."""
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("libhgsim.so not built")
+    L = N.load_library()
+    fake = ctypes.c_void_p(0x10000)
+    nbytes = int(L.hg_gemm_x6_image_bytes(512, 705))
+    args = dict(A=fake, lda=705, img=fake, nb=nbytes, bias=fake, C=fake, ldc=512, ws=fake, wsf=4 * 4096 * 512,
+                M=4096, N=512, K=705, act=1, tile=25, slices=4)
+
+    def call(**kw):
+        a = dict(args, **kw)
+        return L.hg_gemm_f32_splitk_img(a["A"], a["lda"], a["img"], a["nb"], a["bias"], a["C"], a["ldc"], a["ws"],
+                                        a["wsf"], a["M"], a["N"], a["K"], a["act"], a["tile"], a["slices"], None)
+    assert call(nb=nbytes - 16) != 0               # image built for another shape
+    for t in (24, 26, 29, 5, 18, 33):
+        assert call(tile=t) != 0
+    assert call(img=ctypes.c_void_p(0x10004)) != 0  # image not 16-byte aligned
+    assert call(K=16, lda=16, nb=int(L.hg_gemm_x6_image_bytes(512, 16))) != 0  # an empty slice
+    assert call(wsf=4 * 4096 * 512 - 1) != 0
+    assert call(slices=1) != 0
+    assert call(bias=None) != 0
+    assert call(act=2) != 0

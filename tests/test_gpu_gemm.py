@@ -504,6 +504,57 @@ def test_gemm_splitk_forward_matches_fp64(rows, k, n, pad, opad):
     assert ran > 0
 
 
+@pytest.mark.parametrize("rows,k,n,pad,opad", SPLITK_CASES)
+def test_gemm_splitk_img_is_bitwise_the_plain_splitk(rows, k, n, pad, opad):
+    """hg_gemm_f32_splitk_img (the split-K forward with W as its prebuilt operand image) writes the
+    same bits as hg_gemm_f32_splitk on the same tile and slice count (the occupancy tiles 30 / 31 /
+    32 as tiles 25 / 22 / 21), columns past n untouched; the tiles with two chunks per stage are
+    refused (profiles/r6_gemm/roll_splitk_img.json: measured, not routed)."""
+    _need_gpu()
+    from humanoid import _native as N
+    L = N.lib()
+    torch.manual_seed(rows + k + n + 2)
+    dev = "cuda:0"
+    x = torch.randn(rows, k + pad, device=dev)[:, :k]
+    W = torch.randn(n, k, device=dev) / k ** 0.5
+    b = torch.randn(n, device=dev) * 0.1
+    nb = int(L.hg_gemm_x6_image_bytes(n, k))
+    img = torch.full((nb // 4,), float("nan"), device=dev)
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    assert L.hg_gemm_x6_image_jobs((vp * 1)(W.data_ptr()), (i64 * 1)(W.stride(0)), (ctypes.c_int * 1)(0),
+                                   (i64 * 1)(n), (i64 * 1)(k), (vp * 1)(img.data_ptr()), 1, _stream()) == 0
+    base = {30: 25, 31: 22, 32: 21}
+    ran = 0
+    for tile in (20, 21, 22, 23, 25, 27, 28, 30, 31, 32):
+        for S in (2, 4):
+            if (S - 1) * L.hg_gemm_splitk_kslice(k, S) >= k:
+                continue
+            for act in (1, 0):
+                ys = []
+                for fn in ("plain", "img"):
+                    ws = torch.full((S * rows * n,), float("nan"), device=dev)
+                    y = torch.full((rows, n + opad), 7.0, device=dev)
+                    if fn == "plain":
+                        rc = L.hg_gemm_f32_splitk(x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), b.data_ptr(),
+                                                  y.data_ptr(), y.stride(0), ws.data_ptr(), ws.numel(), rows, n, k,
+                                                  act, base.get(tile, tile), S, _stream())
+                    else:
+                        rc = L.hg_gemm_f32_splitk_img(x.data_ptr(), x.stride(0), img.data_ptr(), nb, b.data_ptr(),
+                                                      y.data_ptr(), y.stride(0), ws.data_ptr(), ws.numel(), rows, n,
+                                                      k, act, tile, S, _stream())
+                    assert rc == 0
+                    ys.append(y)
+                assert torch.equal(ys[0], ys[1]), f"tile {tile} S {S} act {act}"
+                ran += 1
+    assert ran > 0
+    ws = torch.empty(2 * rows * n, device=dev)
+    y = torch.empty(rows, n, device=dev)
+    for tile in (24, 26, 29):
+        assert L.hg_gemm_f32_splitk_img(x.data_ptr(), x.stride(0), img.data_ptr(), nb, b.data_ptr(), y.data_ptr(), n,
+                                        ws.data_ptr(), ws.numel(), rows, n, k, 1, tile, 2, _stream()) != 0
+    torch.cuda.synchronize()
+
+
 def test_rollout_first_layer_routes_to_splitk():
     """The rollout's 4096-row 705 -> 512 hidden layer goes through hg_gemm_f32_splitk
     (_GEMM_FWD_SPLITK) and matches the one-pass route within the stated bound; 24576 rows keep
