@@ -1791,3 +1791,50 @@ def test_wave_balancing_does_not_change_results(monkeypatch):
                      ("root_states", "dof_pos", "dof_vel", "torques", "contact_forces", "rigid_state", "rew_buf")})
     for k in outs[0]:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+def test_learn_is_bitwise_reproducible():
+    """The whole loop (collection: K_step, K_post, K_window, the fused rollout launches; update:
+    the eager first update, the captured graphs of the second, the replay of the third) is a
+    deterministic function of the seeds: two OnPolicyRunner.learn(3) runs from one seed give the
+    same parameters, optimizer state, env state, rollout slots and loss statistics bit for bit (no
+    atomics with run-dependent order on the path; the property DESIGN §7's identical training
+    curves rest on)."""
+    _need_gpu()
+    from humanoid.envs import XBotLCfg, XBotLCfgPPO
+    from humanoid.envs.custom.humanoid_env import XBotLFreeEnv
+    from humanoid.algo.ppo import OnPolicyRunner
+    from humanoid.utils.helpers import SimParams, class_to_dict, set_seed
+    runs = []
+    for _ in range(2):
+        set_seed(11)
+        cfg = XBotLCfg()
+        cfg.env.num_envs = 256
+        cfg.seed = 11
+        env = XBotLFreeEnv(cfg, SimParams(), "hg_sim", "cuda:0", True)
+        tcfg = XBotLCfgPPO()
+        tcfg.runner.num_steps_per_env = 24
+        tcfg.seed = 11
+        runner = OnPolicyRunner(env, class_to_dict(tcfg), log_dir=None, device="cuda:0")
+        runner.learn(3, init_at_random_ep_len=True)
+        torch.cuda.synchronize()
+        alg, st = runner.alg, runner.alg.storage
+        assert alg._graphs is not None, "the third update should replay a captured graph"
+        out = {"p%d" % i: p.detach().cpu().clone() for i, p in enumerate(alg.actor_critic.parameters())}
+        for i, group in enumerate(alg.optimizer.state.values()):
+            for k, v in group.items():
+                if torch.is_tensor(v):
+                    out["opt%d_%s" % (i, k)] = v.detach().cpu().clone()
+        for k in ("root_states", "dof_pos", "dof_vel", "obs_buf", "privileged_obs_buf", "rew_buf", "episode_length_buf"):
+            out[k] = getattr(env, k).detach().cpu().clone()
+        for k in ("rewards", "actions", "actions_log_prob", "values", "returns", "advantages"):
+            out["st_" + k] = getattr(st, k).detach().cpu().clone()
+        out["stats"] = torch.tensor([float(runner.last_iteration_stats[k]) for k in ("value_loss", "surrogate_loss")],
+                                    dtype=torch.float64)
+        runs.append(out)
+        del runner, env
+        torch.cuda.synchronize()
+    assert runs[0].keys() == runs[1].keys()
+    for k in runs[0]:
+        assert torch.isfinite(runs[0][k].double()).all(), k
+        assert torch.equal(runs[0][k], runs[1][k]), k
